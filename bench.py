@@ -1,0 +1,250 @@
+"""Benchmark: GbmCVNNPricer training steps on MI355X (BASELINE.json metric / config C2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1] [--store all|terminal]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" is one full training step (reference gbm_trainer.py:1532-1597): Sobol draw of B
+contracts, GBM simulation of P paths x T steps per contract (full [B][T][P] path matrix
+written to HBM, the reference kernel's output contract), forward normalisation, put payoff,
+M-batch mean + N-point DFT -> targets, CVNN forward/backward, Adam, grad norm.  Weak scaling:
+every rank processes B contracts per step (contract-sharded data parallel, one RCCL all-reduce).
+
+Rank 0 prints ONE JSON line.  `value` = contracts x paths per second over the whole job.
+The roofline object is for the dominant kernel (contract_kernel, the fused path/CF kernel),
+timed with HIP events on its own stream after the timed region; `cpu_baseline` is the
+oracle (CPU restatement: C/OpenMP paths + numpy.fft + torch-cpu CVNN) on a bounded sample.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # name: (B per GPU, T, N, M, hidden widths, description)
+    "c1": (64, 16, 256, 4, [32], "C1: 64 contracts x 1024 paths (N=256 x M=4), T=16, 2-layer CVNN 6->32->256 fp32"),
+    "c2": (4096, 16, 256, 256, [32, 32],
+           "C2: 4096 contracts x 65536 paths (N=256 x M=256), T=16, 3-layer CVNN 6->32->32->256 fp32"),
+}
+
+
+def parse() -> argparse.Namespace:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--store", default="all", choices=["all", "terminal"])
+    ap.add_argument("--kernel-iters", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU-baseline sample")
+    return ap.parse_args()
+
+
+def algorithmic_bytes_per_contract(T: int, N: int, M: int, store_all: bool) -> int:
+    """path matrix store + terminal-row re-read + complex64 targets (+ 48 B contract in)."""
+    P = N * M
+    return (T * P * 4 if store_all else P * 4) + P * 4 + N * 8
+
+
+def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: float) -> dict:
+    """Oracle step on the host cores: MC for a time-boxed sample of the B contracts
+    (extrapolated to B) + one full-size CVNN/Adam step on torch-cpu."""
+    import numpy as np
+    import torch
+
+    import oracle
+    from tests.helpers import make_domain_bounds, make_test_cvnn
+
+    oracle.build()
+    threads = oracle.num_threads()
+    torch.set_num_threads(threads)
+    lo, hi = make_domain_bounds().arrays()
+    contracts = oracle.sobol_contracts(7, 0, B, lo, hi)
+    done, t_mc = 0, 0.0
+    chunk = max(1, threads)
+    targets = []
+    while done < B and t_mc < budget_s * 0.8:
+        n = min(chunk, B - done)
+        t0 = time.perf_counter()
+        targets.append(oracle.training_targets(contracts[done:done + n], T, N, M, seed=7, ordinal0=done))
+        t_mc += time.perf_counter() - t0
+        done += n
+    mc_per_contract = t_mc / done
+    model = make_test_cvnn(n_inputs=6, n_outputs=N, seed=123, dtype=torch.float32, device="cpu",
+                           hidden_layers=len(widths))
+    adam = torch.optim.Adam(model.parameters(), lr=1e-2)
+    x = torch.tensor(contracts, dtype=torch.float32)
+    tg = torch.from_numpy(np.concatenate(targets))
+    tg = tg.repeat((B + tg.shape[0] - 1) // tg.shape[0], 1)[:B]
+    oracle.torch_step(model, x, torch.zeros_like(x), tg, adam)  # warm
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        oracle.torch_step(model, x, torch.zeros_like(x), tg, adam)
+    t_nn = (time.perf_counter() - t0) / reps
+    step_s = mc_per_contract * B + t_nn
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {
+        "value": B * N * M / step_s,
+        "unit": "contracts*paths/s",
+        "steps_per_sec": 1.0 / step_s,
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle MC (f64 path recursion, OpenMP {threads} threads) on {done}/{B} contracts "
+                   f"x {N * M} paths x T={T} ({t_mc:.1f}s), extrapolated x{B / done:.1f}, "
+                   f"+ full B={B} CVNN/Adam step on torch-cpu ({t_nn * 1e3:.1f} ms)"),
+        "cpu_model": cpu_model,
+    }
+
+
+def main() -> None:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from spectralmc_amd import _lib, dp
+    from spectralmc_amd.gbm_trainer import GbmCVNNPricer
+    from spectralmc_amd.models.numerical import Precision
+    from tests.helpers import (
+        expect_success,
+        make_black_scholes_config,
+        make_domain_bounds,
+        make_gbm_cvnn_config,
+        make_simulation_params,
+        make_test_cvnn,
+        make_training_config,
+    )
+
+    ctx = dp.init_from_env()
+    world = ctx.world_size if ctx else 1
+    rank = ctx.rank if ctx else 0
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    B, T, N, M, widths, desc = CONFIGS[args.config]
+    P = N * M
+    sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=M, threads_per_block=256,
+                                mc_seed=7, buffer_size=512, dtype=Precision.float32)
+    model = make_test_cvnn(n_inputs=6, n_outputs=N, seed=123, dtype=torch.float32, device=dev,
+                           hidden_layers=len(widths))
+    cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                               domain_bounds=make_domain_bounds())
+    pricer = expect_success(GbmCVNNPricer.create(cfg))
+    pricer.store_paths = args.store == "all"
+    pricer.warmup_steps = max(1, min(2, args.warmup))
+    tcfg = make_training_config(num_batches=args.warmup + args.steps, batch_size=B, learning_rate=1e-2)
+    session = expect_success(pricer.open_session(tcfg))
+
+    for _ in range(args.warmup):
+        expect_success(session.step())
+    session.sync()
+    if ctx:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        expect_success(session.step())
+    session.sync()
+    torch.cuda.synchronize()
+    if ctx:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if ctx:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final = session.close()
+
+    # ---- dominant kernel, timed alone with HIP events on its own stream ----------------
+    eng = session.engine
+    stream = torch.cuda.Stream(device=dev)
+    L = _lib.lib()
+    launches_per_call = (eng.B + eng.chunk - 1) // eng.chunk
+    with torch.cuda.stream(stream):
+        b = eng.buffers
+
+        def run_kernel() -> None:
+            _lib.check(L.smc_train_targets(_lib.ptr(b.contracts), eng.B, eng.T, eng.N, eng.M, eng.seed, None, 0,
+                                           eng._scheme, eng._norm, eng._dtype_code, eng.store_mode,
+                                           _lib.ptr(eng.paths), eng.chunk, _lib.ptr(eng.rowsum),
+                                           _lib.ptr(b.targets), _lib.stream_handle(stream)))
+
+        run_kernel()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _ in range(args.kernel_iters):
+            run_kernel()
+        ev1.record(stream)
+    ev1.synchronize()
+    kernel_ms = ev0.elapsed_time(ev1) / (args.kernel_iters * launches_per_call)
+    contracts_per_launch = min(eng.chunk, eng.B)
+    bytes_launch = algorithmic_bytes_per_contract(T, N, M, pricer.store_paths) * contracts_per_launch + \
+        48 * contracts_per_launch
+    achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            with open(tpath) as f:
+                tj = json.load(f)
+            key = f"{args.config}_{args.store}"
+            if key in tj:
+                traffic = tj[key]["hbm_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
+            traffic = None
+
+    total_units = world * B * P * args.steps
+    value = total_units / elapsed
+    line = {
+        "metric": "training-steps/sec (contracts*paths/s) + HBM GB/s, GBM 4096x65536",
+        "value": value,
+        "unit": "contracts*paths/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "steps_per_sec": args.steps / elapsed,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: Sobol contracts (seed 7, make_domain_bounds defaults), random-init CVNN (seed 123)",
+        "config": {"workload": desc, "contracts_per_gpu": B, "global_contracts": world * B, "paths": P,
+                   "timesteps": T, "network_size": N, "batches_per_mc_run": M,
+                   "path_store": args.store, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "kernel": "contract_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_launch,
+                     "contracts_per_launch": contracts_per_launch},
+        "final_loss": final.loss,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(B, T, N, M, widths, args.cpu_seconds)
+        line["cpu_baseline"] = cb
+        line["speedup_vs_cpu"] = value / cb["value"]
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if ctx:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

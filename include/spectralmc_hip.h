@@ -1,0 +1,130 @@
+/*
+ * spectralmc_hip.h — C ABI of the MI355X (gfx950) GbmCVNNPricer hot path.
+ *
+ * One shared library, libspectralmc_hip.so, exports these symbols with plain
+ * pointers and sizes (no torch / HIP C++ types in the signatures).  Every entry
+ * point is stream-ordered on the caller's `hipStream_t` (passed as `void*`,
+ * NULL = legacy default stream), allocates nothing per call, performs no host
+ * synchronisation and no hidden H2D/D2H copy, so a caller may capture any
+ * sequence of these calls into a hipGraph.  All device buffers are caller-owned.
+ *
+ * Reference seams replaced (Tuee22/SpectralMC @ 2026-01-02, paths relative to
+ * the reference repository root):
+ *   smc_sobol_*          scipy.stats.qmc.Sobol(d, scramble=True, seed) + fast_forward + random,
+ *                        as used by SobolSampler.create / sample
+ *                        (src/spectralmc/sobol_sampler.py:177-203, 222-246)
+ *   smc_gbm_simulate     ConcurrentNormGenerator.get_matrix + SimulateBlackScholes[grid, tpb, stream]
+ *                        (src/spectralmc/async_normals.py:388-398, src/spectralmc/gbm.py:224-257, 400-426)
+ *   smc_gbm_normalize    forward normalisation sims *= forwards / row_means
+ *                        (src/spectralmc/gbm.py:428-440)
+ *   smc_cf_targets       put payoff + reshape(M, N) + FFT(axis=1) + mean(axis=0)
+ *                        (src/spectralmc/gbm.py:464-474, src/spectralmc/gbm_trainer.py:806-817)
+ *   smc_train_targets    the fused per-step Monte-Carlo side of _run_batch: all of the above for
+ *                        B contracts in one launch sequence (src/spectralmc/gbm_trainer.py:1546-1556)
+ *   smc_normals          the normal matrix the engine consumes for contract ordinal m
+ *                        (async_normals.py:212-216 stream semantics; values are this library's RNG)
+ *
+ * Status codes are mapped to the reference's error dataclasses by the Python
+ * host layer (spectralmc_amd/_lib.py); smc_last_error_string() gives the text of
+ * the last failure on the calling thread.
+ */
+#ifndef SPECTRALMC_HIP_H
+#define SPECTRALMC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMC_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------- */
+#define SMC_OK                      0
+#define SMC_ERR_INVALID_ARGUMENT    1  /* null pointer, bad enum, dim out of range    */
+#define SMC_ERR_INVALID_SHAPE       2  /* sizes the kernels cannot take (e.g. N>4096)  */
+#define SMC_ERR_SEED_OUT_OF_RANGE   3  /* seed/skip outside what the engine accepts    */
+#define SMC_ERR_SEQUENCE_EXHAUSTED  4  /* Sobol index would pass 2^30 points           */
+#define SMC_ERR_MEMORY_LIMIT        5  /* reference gbm.py:106-137 path-count guard     */
+#define SMC_ERR_HIP                 6  /* HIP runtime error (launch / device)           */
+
+/* ---- enums (values mirror the reference enums' order) ------------------- */
+#define SMC_SCHEME_LOG_EULER     0  /* PathScheme.LOG_EULER   effects/montecarlo.py:24-29 */
+#define SMC_SCHEME_SIMPLE_EULER  1  /* PathScheme.SIMPLE_EULER                           */
+#define SMC_NORM_RAW             0  /* ForwardNormalization.RAW  effects/montecarlo.py:30-35 */
+#define SMC_NORM_NORMALIZE       1  /* ForwardNormalization.NORMALIZE                    */
+#define SMC_DTYPE_F32            0  /* Precision.float32 (paths f32, targets complex64)  */
+#define SMC_DTYPE_F64            1  /* Precision.float64 (paths f64, targets complex128) */
+#define SMC_STORE_TERMINAL       1  /* keep only the terminal row [B][P] (scratch)        */
+#define SMC_STORE_ALL            2  /* materialise the full path matrix [B][T][P]         */
+
+#define SMC_SOBOL_BITS 30           /* scipy Sobol bits=30: at most 2^30 points          */
+
+typedef struct smc_sobol smc_sobol;
+
+int32_t     smc_abi_version(void);
+const char* smc_last_error_string(void);
+
+/* ---- scrambled Sobol (SciPy-bit-exact) ---------------------------------- */
+/* Build the LMS+digital-shift scrambled generator SciPy builds for
+ * Sobol(d=dim, scramble=True, seed=seed), then fast_forward(skip).
+ * dim in [1, 64]; seed in [0, 2^63). */
+int32_t smc_sobol_create(int32_t dim, uint64_t seed, uint64_t skip, smc_sobol** out);
+void    smc_sobol_destroy(smc_sobol* h);
+/* Host copies of the scrambled tables and the host cursor (next point index). */
+int32_t smc_sobol_state(const smc_sobol* h, uint32_t* shift /*[dim]*/, uint32_t* sv /*[dim*30]*/,
+                        uint64_t* cursor);
+int32_t smc_sobol_fast_forward(smc_sobol* h, uint64_t n);
+/* Host draw of n raw points in [0,1) (Sobol.random(n)); advances the host cursor. */
+int32_t smc_sobol_random_host(smc_sobol* h, int64_t n, double* out /*[n][dim] host*/);
+/* Table image for the device draw: tables[0..dim) = shift, tables[dim + d*30 + c] = sv[d][c].
+ * The caller copies it into a device buffer of dim*31 u32 it owns. */
+int32_t smc_sobol_export_tables(const smc_sobol* h, uint32_t* tables /*[dim*31] host*/);
+/* Device draw from an uploaded table image: point i of the batch is sequence index
+ *   (*index_dev if index_dev != NULL else 0) + index0 + i
+ * scaled as lower + (upper - lower) * x in f64 exactly as sobol_sampler.py:239.
+ * out_f64: [n][dim] f64 (required); out_f32: [n][dim] f32 copy or NULL (CVNN input,
+ * gbm_trainer.py:1775-1783).  The caller guarantees the index range stays < 2^30. */
+int32_t smc_sobol_draw(const uint32_t* tables_dev, int32_t dim, const int64_t* index_dev,
+                       int64_t index0, int64_t n, const double* lower_dev, const double* upper_dev,
+                       double* out_f64, float* out_f32, void* stream);
+
+/* ---- GBM Monte-Carlo engine --------------------------------------------- */
+/* contracts_dev: [B][6] f64 rows in BlackScholes.Inputs order X0, K, T, r, d, v.
+ * Contract b uses normal stream ordinal (*ordinal_dev if non-NULL else 0) + ordinal0 + b.
+ * paths_dev: [B][T][P] of the dtype (raw, un-normalised paths; row t = value after step t+1).
+ * rowsum_dev: [B][T] f64 sums over the P paths of each row (may be NULL). */
+int32_t smc_gbm_simulate(const double* contracts_dev, int64_t n_contracts, int32_t timesteps,
+                         int64_t n_paths, uint64_t mc_seed, const int64_t* ordinal_dev,
+                         int64_t ordinal0, int32_t scheme, int32_t dtype,
+                         void* paths_dev, double* rowsum_dev, void* stream);
+/* In-place forward normalisation of a [B][T][P] path matrix from its row sums. */
+int32_t smc_gbm_normalize(const double* contracts_dev, int64_t n_contracts, int32_t timesteps,
+                          int64_t n_paths, int32_t dtype, void* paths_dev,
+                          const double* rowsum_dev, void* stream);
+/* CF targets from a stored raw path matrix ([B][T][P], row T-1 is read) and its
+ * row sums: targets[b][k] = FFT_N(mean_M(put.reshape(M, N)))[k], N*M == P. */
+int32_t smc_cf_targets(const double* contracts_dev, int64_t n_contracts, int32_t timesteps,
+                       int32_t network_size, int32_t batches_per_mc_run, int32_t normalization,
+                       int32_t dtype, const void* paths_dev, const double* rowsum_dev,
+                       void* targets_dev, void* stream);
+/* Fused training targets: simulate + (store) + normalise + payoff + M-mean + DFT for
+ * B contracts.  store_mode SMC_STORE_ALL writes the full matrix into paths_dev, which
+ * holds `chunk_contracts` contracts ([chunk][T][P]) and is reused chunk by chunk;
+ * SMC_STORE_TERMINAL needs paths_dev of [chunk][P].  targets_dev: [B][N] complex. */
+int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int32_t timesteps,
+                          int32_t network_size, int32_t batches_per_mc_run, uint64_t mc_seed,
+                          const int64_t* ordinal_dev, int64_t ordinal0, int32_t scheme,
+                          int32_t normalization, int32_t dtype, int32_t store_mode,
+                          void* paths_dev, int64_t chunk_contracts, double* rowsum_dev,
+                          void* targets_dev, void* stream);
+/* The [rows][cols] N(0,1) matrix of contract ordinal m (the values smc_gbm_simulate
+ * draws for path p, step t, laid out [t][p]). */
+int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t cols,
+                    int32_t dtype, void* out_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPECTRALMC_HIP_H */

@@ -1,0 +1,213 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+CPU restatement of the reference GbmCVNNPricer training step (Tuee22/SpectralMC @
+2026-01-02), used as the parity checker by ``tests/``, by ``__graft_entry__.smoke()`` and
+as the CPU baseline in ``bench.py``.  The product package ``spectralmc_amd`` never imports
+this module; its HIP path fails loudly when its extension is missing instead of falling back
+here.
+
+Pieces and what pins them
+-------------------------
+* Sobol contracts  -> ``scipy.stats.qmc.Sobol`` itself (the reference's own dependency,
+  scipy 1.15.3 here; ``sobol_sampler.py:192,197,238-239``).  Pinned by golden vectors made
+  with the reference's ``SobolSampler`` (tests/golden/make_golden.py).
+* Normals + paths  -> ``oracle/gbm_oracle.c`` (f64 recursion / dtype stores as the Numba
+  kernel, ``gbm.py:241-257``).  Philox pinned by Random123 KAT vectors; normal-level parity
+  with CuPy XORWOW is unpinned (CuPy absent).  The path arithmetic is additionally pinned by
+  closed-form cases (v = 0, T = 0) and the reference test's Black-price acceptance
+  (``tests/test_gbm.py:103-139``).
+* Normalisation, payoff, FFT, batch mean -> numpy in the sim dtype, in the reference's order
+  (``gbm.py:428-438,464-474``; ``gbm_trainer.py:814-817``: FFT each batch row, then mean).
+* CVNN step -> torch-cpu restatement of ``_torch_step`` (``gbm_trainer.py:819-835``) on a CPU
+  copy of the model; the model's weights/forward are pinned by golden vectors made with the
+  reference's ``cvnn_factory.build_model``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libsmc_oracle.so")
+_lib: ctypes.CDLL | None = None
+
+FIELDS = ("X0", "K", "T", "r", "d", "v")  # BlackScholes.Inputs order, gbm.py:270-275
+
+
+def build() -> str:
+    """Compile the C restatement (gcc, no GPU)."""
+    subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+    return _LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_philox4x32_10.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_normals.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
+                                     ctypes.c_int32, ctypes.c_void_p]
+        L.oracle_gbm_paths.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
+                                       ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
+        L.oracle_num_threads.restype = ctypes.c_int32
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray | None) -> int | None:
+    return None if a is None else a.ctypes.data
+
+
+def _np_dtype(dtype: str) -> type:
+    return {"float32": np.float32, "float64": np.float64}[dtype]
+
+
+# --------------------------------------------------------------------------- RNG
+def philox4x32_10(ctr: tuple[int, int, int, int], key: tuple[int, int]) -> tuple[int, ...]:
+    c = np.array(ctr, dtype=np.uint32)
+    k = np.array(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    lib().oracle_philox4x32_10(_ptr(c), _ptr(k), _ptr(out))
+    return tuple(int(x) for x in out)
+
+
+def normals(seed: int, ordinal: int, rows: int, cols: int, dtype: str = "float32") -> np.ndarray:
+    out = np.empty((rows, cols), dtype=_np_dtype(dtype))
+    lib().oracle_normals(seed, ordinal, rows, cols, 1 if dtype == "float64" else 0, _ptr(out))
+    return out
+
+
+# --------------------------------------------------------------------------- Sobol
+def sobol_contracts(seed: int, skip: int, n: int, lower: np.ndarray, upper: np.ndarray) -> np.ndarray:
+    """SobolSampler._sample_nonzero arithmetic (sobol_sampler.py:238-239) on SciPy's engine."""
+    import warnings
+
+    from scipy.stats.qmc import Sobol
+
+    eng = Sobol(d=len(lower), scramble=True, seed=seed)
+    if skip:
+        eng.fast_forward(skip)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        raw = eng.random(n)
+    return lower + (upper - lower) * raw
+
+
+# --------------------------------------------------------------------------- paths
+def gbm_paths(contracts: np.ndarray, timesteps: int, n_paths: int, seed: int, ordinal0: int = 0,
+              scheme: int = 0, dtype: str = "float32", want_paths: bool = False,
+              threads: int = 0) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
+    """(paths [B,T,P] or None, terminal [B,P], rowsum [B,T] f64) of the raw paths."""
+    contracts = np.ascontiguousarray(contracts, dtype=np.float64)
+    B = contracts.shape[0]
+    dt = _np_dtype(dtype)
+    paths = np.empty((B, timesteps, n_paths), dtype=dt) if want_paths else None
+    terminal = np.empty((B, n_paths), dtype=dt)
+    rowsum = np.empty((B, timesteps), dtype=np.float64)
+    lib().oracle_gbm_paths(_ptr(contracts), B, timesteps, n_paths, seed, ordinal0, scheme,
+                           1 if dtype == "float64" else 0, _ptr(paths), _ptr(terminal), _ptr(rowsum), threads)
+    return paths, terminal, rowsum
+
+
+def _times(Tm: float, timesteps: int, dt_np: type) -> np.ndarray:
+    """cp.linspace(dt, T, timesteps, dtype) (gbm.py:429): f64 grid cast, last point exact."""
+    dt = Tm / timesteps
+    grid = np.linspace(dt, Tm, timesteps, dtype=np.float64)
+    return grid.astype(dt_np)
+
+
+def normalize_paths(contracts: np.ndarray, paths: np.ndarray, rowsum: np.ndarray) -> np.ndarray:
+    """sims *= forwards / row_means (gbm.py:428-438) in the sim dtype."""
+    out = paths.copy()
+    dt_np = paths.dtype.type
+    B, T, P = paths.shape
+    for b in range(B):
+        X0, _, Tm, r, d, _ = (float(x) for x in contracts[b])
+        times = _times(Tm, T, dt_np)
+        forwards = dt_np(X0) * np.exp(dt_np(r - d) * times)
+        means = (rowsum[b] / P).astype(dt_np)
+        out[b] *= (forwards / means)[:, None]
+    return out
+
+
+def cf_targets(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndarray, network_size: int,
+               batches: int, normalize: bool = True) -> np.ndarray:
+    """Per contract: put payoff on the (normalised) terminal row, FFT of each of the M batch
+    rows of length N, mean over batches (gbm.py:464-474, gbm_trainer.py:814-817)."""
+    dt_np = terminal.dtype.type
+    B, P = terminal.shape
+    assert P == network_size * batches
+    X0 = contracts[:, 0]
+    K = contracts[:, 1].astype(dt_np)
+    Tm = contracts[:, 2].astype(dt_np)
+    r = contracts[:, 3]
+    d = contracts[:, 4]
+    F = X0.astype(dt_np) * np.exp((r - d).astype(dt_np) * Tm)
+    df = np.exp((-r).astype(dt_np) * Tm)
+    if normalize:
+        mean = (terminal_sum / P).astype(dt_np)
+        scale = (F / mean).astype(dt_np)
+        sims_T = (terminal * scale[:, None]).astype(dt_np)
+    else:
+        sims_T = terminal
+    put = df[:, None] * np.maximum(K[:, None] - sims_T, dt_np(0))
+    mat = put.reshape(B, batches, network_size)
+    spec = np.fft.fft(mat, axis=2).mean(axis=1)
+    return spec.astype(np.complex64 if dt_np is np.float32 else np.complex128)
+
+
+def training_targets(contracts: np.ndarray, timesteps: int, network_size: int, batches: int, seed: int,
+                     ordinal0: int = 0, scheme: int = 0, normalize: bool = True, dtype: str = "float32",
+                     threads: int = 0) -> np.ndarray:
+    """The Monte-Carlo side of one training step for a batch of contracts."""
+    _, terminal, rowsum = gbm_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme, dtype,
+                                    want_paths=False, threads=threads)
+    return cf_targets(contracts, terminal, rowsum[:, -1], network_size, batches, normalize)
+
+
+# --------------------------------------------------------------------------- CVNN step
+@dataclass
+class StepResult:
+    loss: float
+    grad_norm: float
+
+
+def torch_step(model, real_in, imag_in, targets, optimizer) -> StepResult:
+    """_torch_step (gbm_trainer.py:819-835) on whatever device the tensors live on (CPU here)."""
+    import torch
+
+    pred_r, pred_i = model(real_in, imag_in)
+    loss = torch.nn.functional.mse_loss(pred_r, torch.real(targets)) + torch.nn.functional.mse_loss(
+        pred_i, torch.imag(targets))
+    optimizer.zero_grad(set_to_none=True)
+    loss.backward()
+    optimizer.step()
+    grad_norm = float(torch.nn.utils.clip_grad_norm_(model.parameters(), float("inf")))
+    return StepResult(float(loss.item()), grad_norm)
+
+
+# --------------------------------------------------------------------------- KAT
+def black_put(X0: float, K: float, T: float, r: float, d: float, v: float) -> float:
+    """Closed-form Black-Scholes put (QuantLib blackFormula as used in quantlib.py:19-42)."""
+    df = math.exp(-r * T)
+    fwd = X0 * math.exp((r - d) * T)
+    if T <= 0 or v <= 0:
+        return df * max(K - fwd, 0.0)
+    sd = v * math.sqrt(T)
+    d1 = (math.log(fwd / K) + 0.5 * sd * sd) / sd
+    d2 = d1 - sd
+    ncdf = lambda x: 0.5 * math.erfc(-x / math.sqrt(2.0))  # noqa: E731
+    return df * (K * ncdf(-d2) - fwd * ncdf(-d1))
+
+
+def num_threads() -> int:
+    return int(lib().oracle_num_threads())

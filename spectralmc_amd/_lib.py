@@ -1,0 +1,135 @@
+"""ctypes binding of ``libspectralmc_hip.so`` — the C ABI declared in ``include/spectralmc_hip.h``.
+
+There is deliberately no fallback: if the shared library is missing, or a device entry
+point is called without a ROCm GPU, the call raises.  Build the library with
+``python __graft_entry__.py`` (or ``make -C spectralmc_amd/csrc``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Any
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libspectralmc_hip.so")
+
+# status codes (spectralmc_hip.h)
+SMC_OK = 0
+SMC_ERR_INVALID_ARGUMENT = 1
+SMC_ERR_INVALID_SHAPE = 2
+SMC_ERR_SEED_OUT_OF_RANGE = 3
+SMC_ERR_SEQUENCE_EXHAUSTED = 4
+SMC_ERR_MEMORY_LIMIT = 5
+SMC_ERR_HIP = 6
+
+SCHEME_LOG_EULER = 0
+SCHEME_SIMPLE_EULER = 1
+NORM_RAW = 0
+NORM_NORMALIZE = 1
+DTYPE_F32 = 0
+DTYPE_F64 = 1
+STORE_TERMINAL = 1
+STORE_ALL = 2
+SOBOL_BITS = 30
+ABI_VERSION = 1
+
+_c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
+
+# name -> (restype, argtypes); every symbol the header declares.
+SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
+    "smc_abi_version": (_c_i32, []),
+    "smc_last_error_string": (ctypes.c_char_p, []),
+    "smc_sobol_create": (_c_i32, [_c_i32, _c_u64, _c_u64, ctypes.POINTER(_c_vp)]),
+    "smc_sobol_destroy": (None, [_c_vp]),
+    "smc_sobol_state": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp]),
+    "smc_sobol_fast_forward": (_c_i32, [_c_vp, _c_u64]),
+    "smc_sobol_random_host": (_c_i32, [_c_vp, _c_i64, _c_vp]),
+    "smc_sobol_export_tables": (_c_i32, [_c_vp, _c_vp]),
+    "smc_sobol_draw": (_c_i32, [_c_vp, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "smc_gbm_simulate": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i64, _c_u64, _c_vp, _c_i64, _c_i32, _c_i32,
+                                  _c_vp, _c_vp, _c_vp]),
+    "smc_gbm_normalize": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i64, _c_i32, _c_vp, _c_vp, _c_vp]),
+    "smc_cf_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_vp, _c_vp, _c_vp,
+                                _c_vp]),
+    "smc_train_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_u64, _c_vp, _c_i64, _c_i32,
+                                   _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp]),
+    "smc_normals": (_c_i32, [_c_u64, _c_i64, _c_i32, _c_i64, _c_i32, _c_vp, _c_vp]),
+}
+
+
+class HipExtensionMissing(ImportError):
+    """libspectralmc_hip.so is not built (no silent CPU fallback exists)."""
+
+
+class SmcError(RuntimeError):
+    """Non-zero status from the C ABI."""
+
+    def __init__(self, code: int, message: str) -> None:
+        super().__init__(f"libspectralmc_hip status {code}: {message}")
+        self.code = code
+        self.message = message
+
+
+class DeviceUnavailable(RuntimeError):
+    """A device entry point was called without a ROCm GPU."""
+
+
+_lock = threading.Lock()
+_lib: ctypes.CDLL | None = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise HipExtensionMissing(
+                    f"{LIB_PATH} not found: build it with `python __graft_entry__.py` "
+                    "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, (restype, argtypes) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = restype
+                fn.argtypes = argtypes
+            if handle.smc_abi_version() != ABI_VERSION:
+                raise HipExtensionMissing(f"{LIB_PATH}: ABI {handle.smc_abi_version()} != {ABI_VERSION}")
+            _lib = handle
+    return _lib
+
+
+def last_error() -> str:
+    raw = lib().smc_last_error_string()
+    return raw.decode() if raw else ""
+
+
+def check(status: int) -> None:
+    if status != SMC_OK:
+        raise SmcError(status, last_error())
+
+
+def require_device() -> None:
+    import torch
+
+    if not torch.cuda.is_available() or torch.version.hip is None:
+        raise DeviceUnavailable("the HIP path needs a ROCm GPU (torch.cuda on ROCm); no CPU fallback exists")
+
+
+def ptr(t: Any) -> int | None:
+    """Raw device/host address of a torch tensor / numpy array (None passes NULL)."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return int(t.data_ptr())
+    return int(t.ctypes.data)
+
+
+def stream_handle(stream: Any = None) -> int | None:
+    """hipStream_t of a torch stream (default: the current stream)."""
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream) or None

@@ -1,0 +1,93 @@
+// Device RNG of the GBM engine: one independent N(0,1) stream per (contract ordinal, path).
+//
+// The reference draws a fresh (T, P) normal matrix per contract from CuPy's XORWOW
+// generator (reference src/spectralmc/async_normals.py:212-216) and reads it from HBM in
+// the path kernel (gbm.py:248).  Here the normals never touch memory: each lane derives
+// its path's stream in registers.
+//
+//   seed state  = Philox4x32-10( counter = (path_lo, path_hi, ordinal_lo, ordinal_hi),
+//                                key     = (mc_seed_lo, mc_seed_hi) )      [Salmon et al. 2011]
+//   u32 stream  = xoshiro128** seeded with that 128-bit state          [Blackman & Vigna 2018]
+//   normals     = Box-Muller on consecutive u32 pairs (a, b):
+//                   u1 = ((a >> 8) + 1) * 2^-24 in (0, 1],  u2 = (b >> 8) * 2^-24 in [0, 1)   (f32)
+//                   u1 = (a + 1) * 2^-32,                   u2 = b * 2^-32                    (f64)
+//                   z0 = sqrt(-2 ln u1) cos(2 pi u2),  z1 = sqrt(-2 ln u1) sin(2 pi u2)
+//   normal t of a path is z_(t mod 2) of pair t / 2.
+//
+// Philox runs once per path (its round keys are wave-uniform, so the key schedule lives
+// in SGPRs); each further u32 costs ~10 integer VALU ops with no 32-bit multiply, which
+// keeps the path kernel on the HBM side of the VALU/HBM ridge.  oracle/gbm_oracle.c
+// restates the same stream on the CPU.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace smc {
+
+__device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3,
+                                              uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int round = 0; round < 10; ++round) {
+    const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c0;
+    const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c2;
+    const uint32_t n0 = static_cast<uint32_t>(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = static_cast<uint32_t>(p0 >> 32) ^ c3 ^ k1;
+    c1 = static_cast<uint32_t>(p1);
+    c3 = static_cast<uint32_t>(p0);
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+struct PathStream {
+  uint32_t s0, s1, s2, s3;
+
+  __device__ __forceinline__ PathStream(uint64_t mc_seed, uint64_t ordinal, uint64_t path) {
+    s0 = static_cast<uint32_t>(path);
+    s1 = static_cast<uint32_t>(path >> 32);
+    s2 = static_cast<uint32_t>(ordinal);
+    s3 = static_cast<uint32_t>(ordinal >> 32);
+    philox4x32_10(s0, s1, s2, s3, static_cast<uint32_t>(mc_seed), static_cast<uint32_t>(mc_seed >> 32));
+    s0 |= static_cast<uint32_t>((s0 | s1 | s2 | s3) == 0u);  // xoshiro forbids the zero state
+  }
+
+  __device__ __forceinline__ uint32_t next() {
+    const uint32_t result = __builtin_rotateleft32(s1 * 5u, 7) * 9u;
+    const uint32_t t = s1 << 9;
+    s2 ^= s0;
+    s3 ^= s1;
+    s1 ^= s2;
+    s0 ^= s3;
+    s2 ^= t;
+    s3 = __builtin_rotateleft32(s3, 11);
+    return result;
+  }
+
+  // Two N(0,1) draws, single precision, hardware transcendentals
+  // (v_log_f32 = log2, v_sin/cos_f32 take revolutions).
+  __device__ __forceinline__ void normal_pair(float& z0, float& z1) {
+    const uint32_t a = next(), b = next();
+    const float u1 = static_cast<float>((a >> 8) + 1u) * 0x1p-24f;
+    const float u2 = static_cast<float>(b >> 8) * 0x1p-24f;
+    const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln 2 log2(u1)
+    z0 = r * __builtin_amdgcn_cosf(u2);
+    z1 = r * __builtin_amdgcn_sinf(u2);
+  }
+
+  __device__ __forceinline__ void normal_pair(double& z0, double& z1) {
+    const uint32_t a = next(), b = next();
+    const double u1 = (static_cast<double>(a) + 1.0) * 0x1p-32;
+    const double u2 = static_cast<double>(b) * 0x1p-32;
+    const double r = sqrt(-2.0 * log(u1));
+    double s, c;
+    sincospi(2.0 * u2, &s, &c);
+    z0 = r * c;
+    z1 = r * s;
+  }
+};
+
+}  // namespace smc

@@ -1,0 +1,120 @@
+"""Device-resident Monte-Carlo side of one GbmCVNNPricer training step.
+
+Replaces the reference's per-step host loop (gbm_trainer.py:1539-1561):
+
+    sampler.sample(B)                      -> Sobol kernel writes contracts (B,6) f64 + CVNN input (B,6)
+    [_simulate_fft(c) for c in contracts]  -> ONE fused launch (per chunk): paths, normalisation,
+                                              put payoff, M-mean and the N-point DFT -> targets (B,N)
+    cp.asarray + torch.from_dlpack         -> targets are written in place into a torch tensor
+    _split_inputs (host list -> H2D)       -> already on the device
+
+Everything is enqueued on the caller's (current) HIP stream with no host synchronisation.
+The Sobol index and the normal-stream ordinal of the batch are read by the kernels from a
+small device cursor that the step itself advances, so one recorded step can be replayed as
+a hipGraph indefinitely (see GbmCVNNPricer.train).
+
+Data-parallel layout (one process per GPU): rank r of W draws global contracts
+[base + r*B, base + (r+1)*B) of the step's W*B, for both the Sobol index and the normal
+ordinal, and the cursor advances by W*B per step — so W ranks with B contracts each see the
+same contracts and normals as one rank with W*B.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .gbm import BlackScholesConfig, dtype_code, normalization_code, scheme_code
+from .models.numerical import Precision
+from .sobol_sampler import SobolSampler, draw_device
+
+DEFAULT_PATH_BUFFER_BYTES = int(float(os.environ.get("SMC_PATH_BUFFER_GB", "16")) * (1 << 30))
+
+
+@dataclass(frozen=True)
+class StepBuffers:
+    contracts: torch.Tensor   # (B, 6) f64, BlackScholes.Inputs field order
+    real_in: torch.Tensor     # (B, 6) CVNN dtype
+    imag_in: torch.Tensor     # (B, 6) zeros
+    targets: torch.Tensor     # (B, N) complex
+
+
+class TrainingEngine:
+    """Owns the device buffers of the Monte-Carlo step and launches its kernels."""
+
+    def __init__(self, cfg: BlackScholesConfig, sampler: SobolSampler, batch_size: int, *, model_dtype: torch.dtype,
+                 device: torch.device, rank: int = 0, world_size: int = 1, store_paths: bool = True,
+                 path_buffer_bytes: int | None = None) -> None:
+        _lib.require_device()
+        sp = cfg.sim_params
+        self.cfg = cfg
+        self.B = batch_size
+        self.T = sp.timesteps
+        self.N = sp.network_size
+        self.M = sp.batches_per_mc_run
+        self.P = sp.total_paths()
+        self.seed = sp.mc_seed
+        self.rank = rank
+        self.world_size = world_size
+        self.device = device
+        self.sim_dtype = sp.dtype
+        self._dtype_code = dtype_code(sp.dtype)
+        self._scheme = scheme_code(cfg.path_scheme)
+        self._norm = normalization_code(cfg.normalization)
+        self.store_mode = _lib.STORE_ALL if store_paths else _lib.STORE_TERMINAL
+        sim_torch = sp.dtype.to_torch()
+        cplx = torch.complex64 if sp.dtype == Precision.float32 else torch.complex128
+
+        self._sampler = sampler
+        self.dim = len(sampler.fields)
+        lo, hi = sampler.bounds
+        self.tables = torch.from_numpy(sampler.engine.tables().view("int32")).to(device)
+        self.lower = torch.from_numpy(lo).to(device)
+        self.upper = torch.from_numpy(hi).to(device)
+        # [global Sobol index of the step's first contract, global normal ordinal of it]
+        self.cursor = torch.zeros(2, dtype=torch.int64, device=device)
+
+        B = batch_size
+        contracts = torch.empty((B, self.dim), dtype=torch.float64, device=device)
+        real_in = torch.empty((B, self.dim), dtype=model_dtype, device=device)
+        self.buffers = StepBuffers(contracts=contracts, real_in=real_in,
+                                   imag_in=torch.zeros_like(real_in),
+                                   targets=torch.empty((B, self.N), dtype=cplx, device=device))
+        self.rowsum = torch.empty((B, self.T), dtype=torch.float64, device=device)
+        per_contract = (self.T * self.P if store_paths else self.P) * torch.finfo(sim_torch).bits // 8
+        budget = path_buffer_bytes if path_buffer_bytes is not None else DEFAULT_PATH_BUFFER_BYTES
+        self.chunk = max(1, min(B, budget // per_contract))
+        shape = (self.chunk, self.T, self.P) if store_paths else (self.chunk, self.P)
+        self.paths = torch.empty(shape, dtype=sim_torch, device=device)
+        self._f32_in = model_dtype == torch.float32
+
+    @property
+    def global_batch(self) -> int:
+        return self.B * self.world_size
+
+    def set_position(self, sobol_index: int, ordinal: int) -> None:
+        """Host -> device cursor (outside any captured region)."""
+        self.cursor.copy_(torch.tensor([sobol_index, ordinal], dtype=torch.int64), non_blocking=False)
+
+    def enqueue_step(self) -> StepBuffers:
+        """Launch contracts + targets of the next step on the current stream, advance the cursor."""
+        L = _lib.lib()
+        stream = _lib.stream_handle()
+        b = self.buffers
+        offset = self.rank * self.B
+        draw_device(self.tables, self.dim, self.cursor[0:1], offset, self.B, self.lower, self.upper, b.contracts,
+                    b.real_in if self._f32_in else None)
+        if not self._f32_in:
+            b.real_in.copy_(b.contracts)
+        _lib.check(L.smc_train_targets(
+            _lib.ptr(b.contracts), self.B, self.T, self.N, self.M, self.seed, _lib.ptr(self.cursor[1:2]), offset,
+            self._scheme, self._norm, self._dtype_code, self.store_mode, _lib.ptr(self.paths), self.chunk,
+            _lib.ptr(self.rowsum), _lib.ptr(b.targets), stream))
+        self.cursor.add_(self.global_batch)
+        return b
+
+
+__all__ = ["TrainingEngine", "StepBuffers", "DEFAULT_PATH_BUFFER_BYTES"]

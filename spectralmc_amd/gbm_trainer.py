@@ -1,0 +1,674 @@
+"""GbmCVNNPricer: Sobol contracts -> GBM Monte-Carlo -> CF targets -> CVNN + Adam
+(reference ``src/spectralmc/gbm_trainer.py``).
+
+Same public API and step semantics as the reference trainer; the execution model is
+MI355X-first:
+
+* one HIP stream, no host synchronisation inside a step: the Monte-Carlo side is two
+  launches (engine.py), the CVNN side is torch on hipBLASLt/rocBLAS;
+* after ``warmup_steps`` eager steps the whole step (contracts, targets, forward, MSE,
+  backward, Adam, grad norm, cursor advance) is captured once as a hipGraph and replayed
+  (``torch.cuda.CUDAGraph`` is HIP graphs on ROCm);
+* gradients live in one flat buffer, so data-parallel training (one process per GPU,
+  ``torch.distributed`` "nccl" = RCCL) needs exactly one all-reduce per step (spectralmc_amd/dp.py);
+* loss / grad-norm stay on the device; the host reads them once, after the last step.
+
+Step semantics restated from the reference (``_run_batch`` 1532-1597, ``_torch_step`` 819-835):
+    contracts = Sobol(seed=mc_seed)[sobol_skip : sobol_skip + B]  (scaled into the domain bounds)
+    targets[b] = mean_m FFT_N(put payoff of contract b's normalised paths, batch m)
+    loss = mse(Re pred, Re targets) + mse(Im pred, Im targets);  backward;  Adam.step()
+    grad_norm = || all grads ||_2 (clip_grad_norm_(params, inf) after the step)
+    sobol_skip += B; normal ordinal += B; global_step += 1
+"""
+
+from __future__ import annotations
+
+import asyncio
+import math
+import warnings
+from dataclasses import dataclass
+from typing import Callable, Iterable, Literal, Protocol, Sequence, runtime_checkable
+
+import numpy as np
+import torch
+from pydantic import BaseModel, ConfigDict, PositiveInt, ValidationError
+
+from . import _lib
+from .engine import TrainingEngine
+from .errors.gbm import EngineFailure, NormalsUnavailable
+from .errors.sampler import SamplerValidationFailed, SequenceExhausted
+from .errors.trainer import (
+    InvalidTrainerConfig,
+    InvalidTrainingConfig,
+    OptimizerStateSerializationFailed,
+    PredictionFailed,
+    SamplerInitFailed,
+    TrainerError,
+)
+from .gbm import FIELDS, BlackScholes, BlackScholesConfig, SimulationParams
+from .models.cpu_gpu_transfer import module_state_device_dtype
+from .models.numerical import Precision
+from .models.torch import AdamOptimizerState, AnyDType, Device, FullPrecisionDType, build_adam_optimizer_state
+from .result import Failure, Result, Success
+from .sobol_sampler import MAX_POINTS, DomainBounds, SobolSampler, build_sobol_config
+from .validation import validate_model
+
+nn = torch.nn
+optim = torch.optim
+
+LOGGER_NAME = __name__
+
+
+# ============================================================================ commit plans
+@dataclass(frozen=True)
+class NoCommit:
+    kind: Literal["NoCommit"] = "NoCommit"
+
+
+@dataclass(frozen=True)
+class FinalCommit:
+    kind: Literal["FinalCommit"] = "FinalCommit"
+    commit_message_template: str = "Training checkpoint at step {step}"
+
+
+@dataclass(frozen=True)
+class IntervalCommit:
+    interval: PositiveInt
+    kind: Literal["IntervalCommit"] = "IntervalCommit"
+    commit_message_template: str = "Training checkpoint at step {step}"
+
+
+@dataclass(frozen=True)
+class FinalAndIntervalCommit:
+    interval: PositiveInt
+    kind: Literal["FinalAndIntervalCommit"] = "FinalAndIntervalCommit"
+    commit_message_template: str = "Training checkpoint at step {step}"
+
+
+CommitPlan = NoCommit | FinalCommit | IntervalCommit | FinalAndIntervalCommit
+
+
+# ============================================================================ protocol & configs
+@runtime_checkable
+class ComplexValuedModel(Protocol):
+    """``(real, imag) -> (real, imag)`` network plus the nn.Module subset the trainer uses."""
+
+    def __call__(self, __real: torch.Tensor, __imag: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]: ...
+    def parameters(self) -> Iterable[nn.Parameter]: ...
+    def named_parameters(self) -> Iterable[tuple[str, nn.Parameter]]: ...
+    def state_dict(self, destination=None, prefix: str = "", keep_vars: bool = False) -> dict[str, torch.Tensor]: ...
+    def load_state_dict(self, state_dict: dict[str, torch.Tensor], strict: bool = True) -> None: ...
+    def to(self, device: torch.device, dtype: torch.dtype) -> nn.Module: ...
+    def train(self, mode: bool = True) -> None: ...
+    def eval(self) -> None: ...
+
+
+@dataclass(frozen=True)
+class TrainingConfig:
+    """num_batches steps of batch_size contracts per rank (per GPU) at learning_rate."""
+
+    num_batches: int
+    batch_size: int
+    learning_rate: float
+
+
+def build_training_config(*, num_batches: int, batch_size: int, learning_rate: float
+                          ) -> Result[TrainingConfig, InvalidTrainingConfig]:
+    def bad(msg: str) -> Failure[InvalidTrainingConfig]:
+        return Failure(InvalidTrainingConfig(num_batches=num_batches, batch_size=batch_size,
+                                             learning_rate=learning_rate, message=msg))
+
+    if num_batches <= 0:
+        return bad("num_batches must be > 0")
+    if batch_size <= 0:
+        return bad("batch_size must be > 0")
+    if not (0.0 < learning_rate < 1.0):
+        return bad("learning_rate must be in (0, 1)")
+    return Success(TrainingConfig(num_batches=num_batches, batch_size=batch_size, learning_rate=learning_rate))
+
+
+class GbmCVNNPricerConfig(BaseModel):
+    """Frozen, resumable trainer snapshot (reference gbm_trainer.py:301-313)."""
+
+    cfg: BlackScholesConfig
+    domain_bounds: DomainBounds[BlackScholes.Inputs]
+    cvnn: ComplexValuedModel
+    optimizer_state: AdamOptimizerState | None = None
+    global_step: int = 0
+    sobol_skip: int = 0
+    torch_cpu_rng_state: bytes | None = None
+    torch_cuda_rng_states: list[bytes] | None = None
+
+    model_config = ConfigDict(arbitrary_types_allowed=True, frozen=True, extra="forbid")
+
+
+def build_gbm_cvnn_pricer_config(**kwargs: object) -> Result[GbmCVNNPricerConfig, ValidationError]:
+    return validate_model(GbmCVNNPricerConfig, **kwargs)
+
+
+@dataclass(frozen=True)
+class StepMetrics:
+    step: int
+    batch_time: float
+    loss: float
+    grad_norm: float
+    lr: float
+    optimizer: optim.Optimizer
+    model: ComplexValuedModel
+
+
+StepLogger = Callable[[StepMetrics], None]
+
+
+@dataclass(frozen=True)
+class TrainingResult:
+    updated_config: GbmCVNNPricerConfig
+    final_loss: float
+    total_batches: int
+    final_grad_norm: float
+
+
+@dataclass(frozen=True)
+class _BatchState:
+    sobol_skip: int
+    global_step: int
+    loss: float
+    grad_norm: float
+
+
+# ============================================================================ creation errors
+@dataclass(frozen=True)
+class DeviceDTypeError:
+    kind: Literal["DeviceDTypeError"] = "DeviceDTypeError"
+    message: str = ""
+    underlying_error: object | None = None
+
+
+@dataclass(frozen=True)
+class DeviceNotCUDA:
+    kind: Literal["DeviceNotCUDA"] = "DeviceNotCUDA"
+    device: Device = Device.cpu
+    message: str = "GbmCVNNPricer requires a GPU (ROCm) device"
+
+
+@dataclass(frozen=True)
+class CudaUnavailableForRNGRestore:
+    kind: Literal["CudaUnavailableForRNGRestore"] = "CudaUnavailableForRNGRestore"
+    message: str = "Cannot restore GPU RNG state: no GPU available but the checkpoint carries one"
+
+
+GbmPricerError = DeviceDTypeError | DeviceNotCUDA | CudaUnavailableForRNGRestore
+
+
+def _gpu_count() -> int:
+    return torch.cuda.device_count() if torch.cuda.is_available() else 0
+
+
+def _split_inputs(inputs: Sequence[BlackScholes.Inputs], *, dtype: torch.dtype, device: torch.device
+                  ) -> tuple[torch.Tensor, torch.Tensor]:
+    """Pydantic contracts -> (real, imag=0) CVNN input rows (gbm_trainer.py:1775-1783)."""
+    rows = [[float(getattr(c, f)) for f in FIELDS] for c in inputs]
+    real = torch.tensor(rows, dtype=dtype, device=device)
+    return real, torch.zeros_like(real)
+
+
+# ============================================================================ the step
+class _StepProgram:
+    """The per-step device program; eager or recorded once into a hipGraph and replayed."""
+
+    def __init__(self, pricer: "GbmCVNNPricer", engine: TrainingEngine, adam: optim.Optimizer,
+                 params: list[nn.Parameter], dp) -> None:
+        self.pricer = pricer
+        self.engine = engine
+        self.adam = adam
+        self.params = params
+        self.dp = dp
+        dev = params[0].device
+        numel = sum(p.numel() for p in params)
+        # flat [grads..., loss] buffer: one all-reduce carries both in data-parallel runs
+        self.flat = torch.zeros(numel + 1, dtype=params[0].dtype, device=dev)
+        off = 0
+        for p in params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.loss_slot = self.flat[numel:]
+        self.loss = torch.zeros((), dtype=params[0].dtype, device=dev)
+        self.grad_norm = torch.zeros((), dtype=params[0].dtype, device=dev)
+        self.graphs: list[torch.cuda.CUDAGraph] = []
+
+    # -- pieces -------------------------------------------------------------------------
+    def _forward_backward(self) -> None:
+        buf = self.engine.enqueue_step()
+        self.flat.zero_()
+        pred_r, pred_i = self.pricer._cvnn(buf.real_in, buf.imag_in)
+        loss = nn.functional.mse_loss(pred_r, torch.real(buf.targets)) + nn.functional.mse_loss(
+            pred_i, torch.imag(buf.targets))
+        loss.backward()
+        self.loss_slot.copy_(loss.detach().reshape(1))
+
+    def _update(self) -> None:
+        self.adam.step()
+        grads = [p.grad for p in self.params]
+        self.grad_norm.copy_(torch.linalg.vector_norm(torch.stack(torch._foreach_norm(grads, 2.0)), 2.0))
+        self.loss.copy_(self.loss_slot[0])
+
+    def _reduce(self) -> None:
+        if self.dp is not None:
+            self.dp.all_reduce_mean(self.flat)
+
+    def run_eager(self) -> None:
+        self._forward_backward()
+        self._reduce()
+        self._update()
+
+    def capture(self) -> None:
+        """Record the step (two graphs around the all-reduce when data-parallel)."""
+        pool = torch.cuda.graph_pool_handle()
+        if self.dp is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                self._forward_backward()
+                self._update()
+            self.graphs = [g]
+        else:
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1, pool=pool):
+                self._forward_backward()
+            with torch.cuda.graph(g2, pool=pool):
+                self._update()
+            self.graphs = [g1, g2]
+
+    def replay(self) -> None:
+        if len(self.graphs) == 1:
+            self.graphs[0].replay()
+        else:
+            self.graphs[0].replay()
+            self._reduce()
+            self.graphs[1].replay()
+
+
+# ============================================================================ trainer
+class GbmCVNNPricer:
+    """Coordinates the MC engine, the CF targets and CVNN optimisation on one GPU (per process)."""
+
+    #: eager steps before the step is captured as a hipGraph (0 disables capture)
+    warmup_steps: int = 2
+    #: materialise the full [B][T][P] path matrix each step (the reference kernel's output contract)
+    store_paths: bool = True
+
+    @staticmethod
+    def create(cfg: GbmCVNNPricerConfig) -> Result["GbmCVNNPricer", GbmPricerError]:
+        dd = module_state_device_dtype(cfg.cvnn.state_dict())
+        if isinstance(dd, Failure):
+            return Failure(DeviceDTypeError(message=f"Failed to get device/dtype from CVNN: {dd.error}",
+                                            underlying_error=dd.error))
+        device, dtype = dd.value
+        if device is not Device.cuda:
+            return Failure(DeviceNotCUDA(device=device, message=f"Model on {device}, but a GPU is required"))
+        if cfg.torch_cuda_rng_states is not None and _gpu_count() == 0:
+            return Failure(CudaUnavailableForRNGRestore())
+        pricer = GbmCVNNPricer.__new__(GbmCVNNPricer)
+        pricer._initialize(cfg, device, dtype)
+        return Success(pricer)
+
+    def _initialize(self, cfg: GbmCVNNPricerConfig, device: Device, dtype: AnyDType) -> None:
+        self._cfg = cfg.cfg
+        self._sim_params: SimulationParams = cfg.cfg.sim_params
+        self._cvnn: ComplexValuedModel = cfg.cvnn
+        self._domain_bounds = cfg.domain_bounds
+        self._optimizer_state = cfg.optimizer_state
+        self._global_step = cfg.global_step
+        self._sobol_skip = cfg.sobol_skip
+        self._device = device
+        self._torch_device = next(iter(cfg.cvnn.parameters())).device
+        assert isinstance(dtype, FullPrecisionDType), f"CVNN must use a full-precision dtype, got {dtype}"
+        self._dtype: FullPrecisionDType = dtype
+        assert self._dtype.to_precision() == self._sim_params.dtype, (
+            f"Error: gbm sim dtype {self._sim_params.dtype} does not match cvnn dtype {self._dtype}")
+        self._complex_dtype: Precision = self._dtype.to_precision().to_complex().unwrap()
+        self._mc_engine = BlackScholes(cfg.cfg)
+        self._sampler_result = SobolSampler.create(
+            BlackScholes.Inputs, self._domain_bounds,
+            config=build_sobol_config(seed=self._sim_params.mc_seed, skip=self._sobol_skip).unwrap())
+        if cfg.torch_cpu_rng_state is not None:
+            torch.set_rng_state(torch.from_numpy(np.frombuffer(cfg.torch_cpu_rng_state, dtype=np.uint8).copy()))
+        if cfg.torch_cuda_rng_states is not None:
+            count = _gpu_count()
+            assert count == len(cfg.torch_cuda_rng_states), (
+                f"GPU RNG state count ({len(cfg.torch_cuda_rng_states)}) does not match device count ({count})")
+            torch.cuda.set_rng_state_all([torch.from_numpy(np.frombuffer(s, dtype=np.uint8).copy())
+                                          for s in cfg.torch_cuda_rng_states])
+
+    # ------------------------------------------------------------------ checkpointing
+    @property
+    def mc_engine(self) -> BlackScholes:
+        return self._mc_engine
+
+    def snapshot(self) -> Result[GbmCVNNPricerConfig, NormalsUnavailable]:
+        cpu_rng = torch.get_rng_state().cpu().numpy().tobytes()
+        cuda_rng = [s.cpu().numpy().tobytes() for s in torch.cuda.get_rng_state_all()] if _gpu_count() else None
+        if cuda_rng is None:
+            from .errors.gbm import CudaRNGUnavailable
+
+            return Failure(NormalsUnavailable(error=CudaRNGUnavailable(reason="cuda_unavailable")))
+        eng = self._mc_engine.snapshot()
+        if isinstance(eng, Failure):
+            return eng
+        res = build_gbm_cvnn_pricer_config(cfg=eng.value, domain_bounds=self._domain_bounds, cvnn=self._cvnn,
+                                           optimizer_state=self._optimizer_state, global_step=self._global_step,
+                                           sobol_skip=self._sobol_skip, torch_cpu_rng_state=cpu_rng,
+                                           torch_cuda_rng_states=cuda_rng)
+        if isinstance(res, Failure):
+            raise AssertionError(f"GbmCVNNPricerConfig validation failed: {res.error}")
+        return res
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _validate_commit_plan(plan: CommitPlan) -> Result[CommitPlan, InvalidTrainerConfig]:
+        if isinstance(plan, (IntervalCommit, FinalAndIntervalCommit)) and plan.interval <= 0:
+            return Failure(InvalidTrainerConfig(message="commit interval must be positive for blockchain commit plan"))
+        return Success(plan)
+
+    @staticmethod
+    def _should_commit_now(store, plan: CommitPlan, global_step: int) -> tuple[bool, str]:
+        if isinstance(plan, (IntervalCommit, FinalAndIntervalCommit)):
+            return store is not None and global_step % plan.interval == 0, plan.commit_message_template
+        return False, ""
+
+    @staticmethod
+    def _should_commit_final(store, plan: CommitPlan) -> tuple[bool, str]:
+        if isinstance(plan, (FinalCommit, FinalAndIntervalCommit)):
+            return store is not None, plan.commit_message_template
+        return False, ""
+
+    def _torch_step(self, real_in: torch.Tensor, imag_in: torch.Tensor, targets: torch.Tensor,
+                    optimizer: optim.Optimizer) -> tuple[torch.Tensor, float]:
+        """One eager forward/backward/Adam step (reference semantics, host-synchronising)."""
+        pred_r, pred_i = self._cvnn(real_in, imag_in)
+        loss = nn.functional.mse_loss(pred_r, torch.real(targets)) + nn.functional.mse_loss(
+            pred_i, torch.imag(targets))
+        optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        optimizer.step()
+        grad_norm = float(torch.nn.utils.clip_grad_norm_(self._cvnn.parameters(), float("inf")))
+        return loss, grad_norm
+
+    def _make_adam(self, lr: float) -> Result[optim.Optimizer, OptimizerStateSerializationFailed]:
+        params = list(self._cvnn.parameters())
+        adam = optim.Adam(params, lr=lr, foreach=True, capturable=True)
+        if self._optimizer_state is not None:
+            sd = self._optimizer_state.to_torch()
+            if isinstance(sd, Failure):
+                return Failure(OptimizerStateSerializationFailed(
+                    message=f"Failed to deserialize optimizer state: {sd.error}"))
+            adam.load_state_dict(sd.value)
+            for group in adam.param_groups:
+                group["capturable"] = True
+                group["foreach"] = True
+            for p in params:
+                st = adam.state.get(p)
+                if st and "step" in st:
+                    step = st["step"]
+                    st["step"] = (step if isinstance(step, torch.Tensor) else torch.tensor(float(step))).to(
+                        device=p.device, dtype=torch.float32)
+        return Success(adam)
+
+    def _adam_snapshot(self, adam: optim.Optimizer) -> Result[AdamOptimizerState, OptimizerStateSerializationFailed]:
+        sd = adam.state_dict()
+        sd["state"] = {pid: {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in st.items()}
+                       for pid, st in sd["state"].items()}
+        res = AdamOptimizerState.from_torch(sd)
+        if isinstance(res, Failure):
+            return Failure(OptimizerStateSerializationFailed(message=f"Failed to capture optimizer snapshot: {res.error}"))
+        return res
+
+    # ------------------------------------------------------------------ training
+    def open_session(self, config: TrainingConfig) -> Result["TrainingSession", TrainerError]:
+        """Set up a device training session (engine buffers, Adam, step program) for ``config``."""
+        if isinstance(self._sampler_result, Failure):
+            return Failure(SamplerInitFailed(error=self._sampler_result.error))
+        adam_res = self._make_adam(config.learning_rate)
+        if isinstance(adam_res, Failure):
+            return adam_res
+        from . import dp as _dp
+
+        try:
+            return Success(TrainingSession(self, config, self._sampler_result.value, adam_res.value, _dp.current()))
+        except _lib.SmcError as exc:
+            return Failure(EngineFailure(code=exc.code, message=exc.message))
+
+    def train(self, config: TrainingConfig, *, logger: StepLogger | None = None, blockchain_store=None,
+              commit_plan: CommitPlan = NoCommit()) -> Result[TrainingResult, TrainerError]:
+        plan = self._validate_commit_plan(commit_plan)
+        if isinstance(plan, Failure):
+            return plan
+        if not isinstance(commit_plan, NoCommit) and blockchain_store is None:
+            return Failure(InvalidTrainerConfig(message="commit_plan requires blockchain_store to be provided"))
+        if isinstance(self._sampler_result, Failure):
+            return Failure(SamplerInitFailed(error=self._sampler_result.error))
+        sampler = self._sampler_result.value
+        lo, _hi = sampler.bounds
+        if not _bounds_always_valid(lo):
+            # Rows could violate BlackScholes.Inputs: keep the reference's error by validating
+            # every batch on the host (slow path; never taken with positive bounds).
+            return self._train_checked(config, sampler, logger, blockchain_store, commit_plan)
+        opened = self.open_session(config)
+        if isinstance(opened, Failure):
+            return opened
+        session = opened.value
+        try:
+            for _ in range(config.num_batches):
+                stepped = session.step()
+                if isinstance(stepped, Failure):
+                    return stepped
+                if logger is not None:
+                    loss, gn = session.read_metrics()
+                    logger(StepMetrics(step=session.global_step, batch_time=float("nan"), loss=loss, grad_norm=gn,
+                                       lr=config.learning_rate, optimizer=session.adam, model=self._cvnn))
+                do_commit, template = self._should_commit_now(blockchain_store, commit_plan, session.global_step)
+                if do_commit:
+                    session.sync()
+                    self._global_step, self._sobol_skip = session.global_step, session.sobol_skip
+                    loss, _ = session.read_metrics()
+                    self._commit_to_blockchain(blockchain_store, session.adam, template, loss,
+                                               batch=session.global_step)
+        except _lib.SmcError as exc:
+            return Failure(EngineFailure(code=exc.code, message=exc.message))
+        final_state = session.close()
+        return self._finish(session.adam, final_state, config, blockchain_store, commit_plan)
+
+    def _train_checked(self, config: TrainingConfig, sampler: SobolSampler, logger, blockchain_store,
+                       commit_plan: CommitPlan) -> Result[TrainingResult, TrainerError]:
+        """Host-validated variant for domains that admit invalid contracts (e.g. X0 lower <= 0)."""
+        adam_res = self._make_adam(config.learning_rate)
+        if isinstance(adam_res, Failure):
+            return adam_res
+        adam = adam_res.value
+        self._cvnn.train()
+        sobol_skip, global_step = self._sobol_skip, self._global_step
+        loss_v, gn = 0.0, 0.0
+        try:
+            engine = TrainingEngine(self._cfg, sampler, config.batch_size, model_dtype=self._dtype.to_torch(),
+                                    device=self._torch_device, store_paths=self.store_paths)
+        except _lib.SmcError as exc:
+            return Failure(EngineFailure(code=exc.code, message=exc.message))
+        engine.set_position(sobol_skip, self._mc_engine.ordinal)
+        for _ in range(config.num_batches):
+            buf = engine.enqueue_step()
+            host = buf.contracts.cpu().numpy()
+            for row in host:
+                res = validate_model(BlackScholes.Inputs, **{f: float(row[i]) for i, f in enumerate(FIELDS)})
+                if isinstance(res, Failure):
+                    return Failure(SamplerInitFailed(error=SamplerValidationFailed(error=res.error)))
+            loss, gn = self._torch_step(buf.real_in, buf.imag_in, buf.targets, adam)
+            loss_v = float(loss.item())
+            sobol_skip += config.batch_size
+            global_step += 1
+            self._mc_engine.advance(config.batch_size)
+        sampler.skip(sobol_skip - self._sobol_skip)
+        return self._finish(adam, _BatchState(sobol_skip, global_step, loss_v, gn), config, blockchain_store,
+                            commit_plan)
+
+    def _finish(self, adam: optim.Optimizer, st: _BatchState, config: TrainingConfig, blockchain_store,
+                commit_plan: CommitPlan) -> Result[TrainingResult, TrainerError]:
+        opt = self._adam_snapshot(adam)
+        if isinstance(opt, Failure):
+            return opt
+        self._optimizer_state = opt.value
+        self._global_step = st.global_step
+        self._sobol_skip = st.sobol_skip
+        do_commit, template = self._should_commit_final(blockchain_store, commit_plan)
+        if do_commit:
+            self._commit_to_blockchain(blockchain_store, adam, template, st.loss, batch=config.num_batches)
+        snap = self.snapshot()
+        if isinstance(snap, Failure):
+            return snap
+        return Success(TrainingResult(updated_config=snap.value, final_loss=st.loss, total_batches=config.num_batches,
+                                      final_grad_norm=st.grad_norm))
+
+    async def train_via_effects(self, config: TrainingConfig, *, logger: StepLogger | None = None,
+                                blockchain_store=None, commit_plan: CommitPlan = NoCommit()
+                                ) -> Result[TrainingResult, TrainerError]:
+        return self.train(config, logger=logger, blockchain_store=blockchain_store, commit_plan=commit_plan)
+
+    def _commit_to_blockchain(self, store, adam: optim.Optimizer, template: str, loss: float, batch: int) -> None:
+        """Synchronous commit of the current snapshot; failures are logged, training continues."""
+        import logging
+
+        log = logging.getLogger(LOGGER_NAME)
+        try:
+            opt = self._adam_snapshot(adam)
+            if isinstance(opt, Failure):
+                log.error("Skipping commit at step %s: %s", self._global_step, opt.error)
+                return
+            self._optimizer_state = opt.value
+            snap = self.snapshot()
+            if isinstance(snap, Failure):
+                log.error("Skipping commit at step %s: %s", self._global_step, snap.error)
+                return
+            message = template.format(step=self._global_step, loss=loss, batch=batch)
+            from .storage import commit_snapshot
+
+            try:
+                asyncio.get_running_loop()
+                log.warning("Skipping commit at step %s: called from a running event loop", self._global_step)
+                return
+            except RuntimeError:
+                pass
+            asyncio.run(commit_snapshot(store, snap.value, message))
+        except Exception as exc:  # storage failures never stop training (reference 1296-1302)
+            log.error("Failed to commit at step %s: %s", self._global_step, exc)
+
+    # ------------------------------------------------------------------ inference
+    def predict_price(self, inputs: Sequence[BlackScholes.Inputs]
+                      ) -> Result[list[BlackScholes.HostPricingResults], TrainerError]:
+        """CVNN spectrum -> mean of the IFFT = DC/N -> put; call by put-call parity
+        (reference gbm_trainer.py:1709-1767)."""
+        if len(inputs) == 0:
+            return Success([])
+        self._cvnn.eval()
+        try:
+            real_in, imag_in = _split_inputs(inputs, dtype=self._dtype.to_torch(), device=self._torch_device)
+            with torch.no_grad():
+                pred_r, pred_i = self._cvnn(real_in, imag_in)
+                spectrum = torch.complex(pred_r, pred_i)
+                coeffs = torch.fft.ifft(spectrum, dim=1).mean(dim=1).cpu()
+            out: list[BlackScholes.HostPricingResults] = []
+            for coeff, c in zip(coeffs, inputs, strict=True):
+                re, im = float(coeff.real), float(coeff.imag)
+                if abs(im) > 1.0e-6:
+                    warnings.warn(f"IFFT imaginary component {im:.3e} exceeds tolerance.", RuntimeWarning)
+                disc = math.exp(-c.r * c.T)
+                fwd = c.X0 * math.exp((c.r - c.d) * c.T)
+                put = re
+                call = put + fwd - c.K * disc
+                put_i = disc * max(c.K - fwd, 0.0)
+                call_i = disc * max(fwd - c.K, 0.0)
+                res = validate_model(BlackScholes.HostPricingResults, underlying=fwd, put_price=put, call_price=call,
+                                     put_price_intrinsic=put_i, call_price_intrinsic=call_i,
+                                     put_convexity=put - put_i, call_convexity=call - call_i)
+                if isinstance(res, Failure):
+                    raise AssertionError(f"HostPricingResults validation failed: {res.error}")
+                out.append(res.value)
+            return Success(out)
+        except Exception as exc:
+            return Failure(PredictionFailed(message=str(exc)))
+
+
+class TrainingSession:
+    """A live training run on the device: ``step()`` enqueues one full training step
+    (eager for the first ``warmup_steps``, then one captured hipGraph replay); ``close()``
+    synchronises once and returns the final counters / metrics."""
+
+    def __init__(self, pricer: GbmCVNNPricer, config: TrainingConfig, sampler: SobolSampler,
+                 adam: optim.Optimizer, ctx) -> None:
+        self.pricer = pricer
+        self.config = config
+        self.sampler = sampler
+        self.adam = adam
+        self.ctx = ctx
+        world, rank = (ctx.world_size, ctx.rank) if ctx is not None else (1, 0)
+        self.global_batch = config.batch_size * world
+        pricer._cvnn.train()
+        dev = pricer._torch_device
+        self.engine = TrainingEngine(pricer._cfg, sampler, config.batch_size, model_dtype=pricer._dtype.to_torch(),
+                                     device=dev, rank=rank, world_size=world, store_paths=pricer.store_paths)
+        self.params = list(pricer._cvnn.parameters())
+        self.program = _StepProgram(pricer, self.engine, adam, self.params, ctx)
+        self.sobol_skip0 = pricer._sobol_skip
+        self.sobol_skip = pricer._sobol_skip
+        self.global_step = pricer._global_step
+        self.steps = 0
+        self.engine.set_position(self.sobol_skip, pricer._mc_engine.ordinal)
+        self.stream = torch.cuda.Stream(device=dev)
+        self.stream.wait_stream(torch.cuda.current_stream(dev))
+        self._closed = False
+
+    def step(self) -> Result[int, TrainerError]:
+        if self.sobol_skip + self.global_batch > MAX_POINTS:
+            return Failure(SamplerInitFailed(error=SequenceExhausted(requested_end=self.sobol_skip + self.global_batch)))
+        prog = self.program
+        with torch.cuda.stream(self.stream):
+            warm = self.pricer.warmup_steps
+            if warm > 0 and self.steps >= warm and not prog.graphs:
+                prog.capture()
+            if prog.graphs:
+                prog.replay()
+            else:
+                prog.run_eager()
+        self.steps += 1
+        self.sobol_skip += self.global_batch
+        self.global_step += 1
+        self.pricer._mc_engine.advance(self.global_batch)
+        return Success(self.global_step)
+
+    def sync(self) -> None:
+        self.stream.synchronize()
+
+    def read_metrics(self) -> tuple[float, float]:
+        self.sync()
+        return float(self.program.loss), float(self.program.grad_norm)
+
+    def close(self) -> _BatchState:
+        if self._closed:
+            raise RuntimeError("session already closed")
+        self._closed = True
+        self.sync()
+        dev = self.pricer._torch_device
+        torch.cuda.current_stream(dev).wait_stream(self.stream)
+        loss, gn = (float(self.program.loss), float(self.program.grad_norm)) if self.steps else (0.0, 0.0)
+        for p in self.params:  # detach the flat-buffer grad views from the parameters
+            p.grad = p.grad.clone()
+        self.sampler.skip(self.sobol_skip - self.sobol_skip0)
+        return _BatchState(self.sobol_skip, self.global_step, loss, gn)
+
+
+def _bounds_always_valid(lower: np.ndarray) -> bool:
+    """x in [0,1) maps to [lower, upper): rows satisfy X0>0, K>0, T>=0, v>=0 if the lower bounds do."""
+    X0, K, T, _r, _d, v = (float(x) for x in lower)
+    return X0 > 0 and K > 0 and T >= 0 and v >= 0
+
+
+__all__ = ("TrainingSession", "GbmCVNNPricerConfig", "StepMetrics", "TrainingResult", "GbmCVNNPricer", "TrainingConfig",
+           "build_training_config", "ComplexValuedModel", "NoCommit", "FinalCommit", "IntervalCommit",
+           "FinalAndIntervalCommit", "CommitPlan", "build_gbm_cvnn_pricer_config")

@@ -1,0 +1,95 @@
+"""libspectralmc_hip.so: loads, exports every symbol include/spectralmc_hip.h declares, host-side
+Sobol is bit-exact with the reference's golden vectors, and argument errors come back as status
+codes without touching a GPU.  CPU only (no kernel launches)."""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from spectralmc_amd import _lib
+from spectralmc_amd.sobol_sampler import SobolEngine
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "spectralmc_hip.h")
+
+
+def declared_symbols() -> list[str]:
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(smc_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol() -> None:
+    L = _lib.lib()
+    names = declared_symbols()
+    assert len(names) >= 14
+    for name in names:
+        assert hasattr(L, name), name
+    assert set(names) == set(_lib.SIGNATURES), "ctypes signature table out of sync with the header"
+    assert L.smc_abi_version() == _lib.ABI_VERSION
+
+
+@pytest.mark.parametrize("seed", [7, 31, 42, 123])
+@pytest.mark.parametrize("skip", [0, 8, 4096])
+def test_host_sobol_bit_exact_with_reference(golden, seed, skip) -> None:
+    lo, hi = golden["bounds_lower"], golden["bounds_upper"]
+    eng = SobolEngine(6, seed, skip)
+    got = lo + (hi - lo) * eng.random(64)
+    np.testing.assert_array_equal(got, golden[f"sobol_s{seed}_k{skip}"])
+    got2 = lo + (hi - lo) * eng.random(32)
+    np.testing.assert_array_equal(got2, golden[f"sobol_s{seed}_k{skip}_next"])
+    assert eng.cursor == skip + 96
+
+
+def test_sobol_tables_layout() -> None:
+    eng = SobolEngine(6, 7, 0)
+    shift, sv = eng.state()
+    tab = eng.tables()
+    np.testing.assert_array_equal(tab[:6], shift)
+    np.testing.assert_array_equal(tab[6:].reshape(6, 30), sv)
+    # first point of a scrambled sequence is the digital shift itself
+    np.testing.assert_array_equal(eng.random(1)[0], shift.astype(np.float64) * 2.0 ** -30)
+
+
+def test_sobol_argument_errors() -> None:
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    assert L.smc_sobol_create(0, 7, 0, ctypes.byref(h)) == _lib.SMC_ERR_INVALID_ARGUMENT
+    assert "dim" in _lib.last_error()
+    assert L.smc_sobol_create(65, 7, 0, ctypes.byref(h)) == _lib.SMC_ERR_INVALID_ARGUMENT
+    assert L.smc_sobol_create(6, 7, (1 << 30) + 1, ctypes.byref(h)) == _lib.SMC_ERR_SEQUENCE_EXHAUSTED
+    assert L.smc_sobol_create(6, 1 << 63, 0, ctypes.byref(h)) == _lib.SMC_ERR_SEED_OUT_OF_RANGE
+    eng = SobolEngine(6, 7, (1 << 30) - 4)
+    with pytest.raises(_lib.SmcError) as exc:
+        eng.random(5)
+    assert exc.value.code == _lib.SMC_ERR_SEQUENCE_EXHAUSTED
+
+
+def test_engine_argument_errors_do_not_launch() -> None:
+    L = _lib.lib()
+    # NULL contracts / bad shapes / bad enums are rejected before any HIP call
+    assert L.smc_gbm_simulate(None, 1, 16, 1024, 7, None, 0, 0, 0, None, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
+    dummy = ctypes.c_double(0.0)
+    p = ctypes.addressof(dummy)
+    assert L.smc_gbm_simulate(p, 1, 0, 1024, 7, None, 0, 0, 0, p, None, None) == _lib.SMC_ERR_INVALID_SHAPE
+    assert L.smc_gbm_simulate(p, 1, 16, 1024, 7, None, 0, 5, 0, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
+    assert L.smc_gbm_simulate(p, 1, 16, 1024, 7, None, 0, 0, 9, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
+    assert L.smc_train_targets(p, 4, 16, 0, 4, 7, None, 0, 0, 1, 0, 2, p, 4, None, p, None) == \
+        _lib.SMC_ERR_INVALID_SHAPE
+    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 3, p, 4, None, p, None) == \
+        _lib.SMC_ERR_INVALID_ARGUMENT
+    # an N too large for the LDS budget is a shape error, reported before launching
+    assert L.smc_train_targets(p, 4, 16, 1 << 14, 1, 7, None, 0, 0, 1, 0, 2, p, 4, None, p, None) == \
+        _lib.SMC_ERR_INVALID_SHAPE
+    assert L.smc_normals(7, 0, 0, 10, 0, p, None) == _lib.SMC_ERR_INVALID_SHAPE
+    assert L.smc_sobol_draw(None, 6, None, 0, 4, p, p, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
+
+
+def test_zero_contracts_is_a_noop() -> None:
+    L = _lib.lib()
+    dummy = ctypes.c_double(0.0)
+    p = ctypes.addressof(dummy)
+    assert L.smc_train_targets(p, 0, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 4, None, p, None) == _lib.SMC_OK

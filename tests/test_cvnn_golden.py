@@ -1,0 +1,137 @@
+"""CVNN layers and factory vs the reference's golden vectors (weights bit-exact; forward and one
+Adam step on torch-cpu).  CPU only."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from spectralmc_amd.cvnn import ComplexLinear, CovarianceComplexBatchNorm, modReLU, zReLU
+from spectralmc_amd.cvnn_factory import (
+    ActivationCfg,
+    ActivationKind,
+    ExplicitWidth,
+    LinearCfg,
+    ResidualCfg,
+    SequentialCfg,
+    build_cvnn_config,
+    build_model,
+)
+from spectralmc_amd.models.torch import FullPrecisionDType
+
+CASES = {
+    "e2e": (123, [32], 128, torch.float32),
+    "c1": (123, [32], 256, torch.float32),
+    "c2": (123, [32, 32], 256, torch.float32),
+    "c2f64": (123, [32, 32], 256, torch.float64),
+    "tmpl": (999, [32], 128, torch.float32),
+}
+
+
+def make(seed: int, widths: list[int], n_out: int, dtype: torch.dtype) -> torch.nn.Module:
+    layers = [LinearCfg(width=ExplicitWidth(value=w), activation=ActivationCfg(kind=ActivationKind.MOD_RELU))
+              for w in widths]
+    cfg = build_cvnn_config(dtype=FullPrecisionDType.from_torch(dtype).unwrap(), layers=layers, seed=seed).unwrap()
+    return build_model(n_inputs=6, n_outputs=n_out, cfg=cfg).unwrap()
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_build_model_weights_bit_exact(golden, name) -> None:
+    net = make(*CASES[name])
+    sd = net.state_dict()
+    keys = sorted(k.split("__", 1)[1] for k in golden if k.startswith(f"cvnn_{name}__"))
+    assert sorted(sd) == keys
+    for k in keys:
+        np.testing.assert_array_equal(sd[k].numpy(), golden[f"cvnn_{name}__{k}"], err_msg=k)
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_forward_and_one_adam_step(golden, name) -> None:
+    seed, widths, n_out, dtype = CASES[name]
+    net = make(seed, widths, n_out, dtype)
+    x = torch.tensor(golden["sobol_s7_k0"], dtype=dtype)
+    with torch.no_grad():
+        yr, yi = net(x, torch.zeros_like(x))
+    np.testing.assert_array_equal(yr.numpy(), golden[f"cvnn_{name}_fwd_re"])
+    np.testing.assert_array_equal(yi.numpy(), golden[f"cvnn_{name}_fwd_im"])
+    targets = torch.tensor(golden[f"cvnn_{name}_step_targets"])
+    adam = torch.optim.Adam(net.parameters(), lr=1e-2)
+    pr, pi = net(x, torch.zeros_like(x))
+    loss = torch.nn.functional.mse_loss(pr, targets.real) + torch.nn.functional.mse_loss(pi, targets.imag)
+    adam.zero_grad(set_to_none=True)
+    loss.backward()
+    adam.step()
+    gn = float(torch.nn.utils.clip_grad_norm_(net.parameters(), float("inf")))
+    assert float(loss.detach()) == pytest.approx(float(golden[f"cvnn_{name}_step_loss"]), rel=1e-6)
+    assert gn == pytest.approx(float(golden[f"cvnn_{name}_step_gradnorm"]), rel=1e-6)
+    for k, v in net.state_dict().items():
+        np.testing.assert_allclose(v.numpy(), golden[f"cvnn_{name}_after__{k}"], rtol=1e-6, atol=1e-7, err_msg=k)
+
+
+def test_state_dict_keys_match_reference_nesting() -> None:
+    net = make(123, [32, 32], 256, torch.float32)
+    assert "layers.0.layers.0.layers.0.real_weight" in net.state_dict()
+    assert "layers.1.imag_bias" in net.state_dict()
+    assert sum(p.numel() for p in net.parameters()) == 19_520  # SURVEY §8a a10, C2 CVNN
+
+
+def test_complex_linear_known_answer() -> None:
+    """(A x - B y) + i(B x + A y) + b on a 2x2 case (reference tests/test_cvnn.py:91-118 style)."""
+    lin = ComplexLinear(2, 2)
+    with torch.no_grad():
+        lin.real_weight.copy_(torch.tensor([[1.0, 2.0], [3.0, 4.0]]))
+        lin.imag_weight.copy_(torch.tensor([[0.5, -1.0], [2.0, 0.0]]))
+        lin.real_bias.copy_(torch.tensor([0.1, -0.2]))
+        lin.imag_bias.copy_(torch.tensor([0.3, 0.4]))
+    x = torch.tensor([[1.0, -1.0]])
+    y = torch.tensor([[2.0, 0.5]])
+    re, im = lin(x, y)
+    A = np.array([[1.0, 2.0], [3.0, 4.0]])
+    Bm = np.array([[0.5, -1.0], [2.0, 0.0]])
+    z = np.array([1.0, -1.0]) + 1j * np.array([2.0, 0.5])
+    want = (A + 1j * Bm) @ z + np.array([0.1 + 0.3j, -0.2 + 0.4j])
+    np.testing.assert_allclose(re.detach().numpy()[0], want.real, rtol=1e-6)
+    np.testing.assert_allclose(im.detach().numpy()[0], want.imag, rtol=1e-6)
+
+
+def test_modrelu_and_zrelu() -> None:
+    act = modReLU(1)
+    with torch.no_grad():
+        act.bias.fill_(-1.0)
+    re, im = act(torch.tensor([[3.0]]), torch.tensor([[4.0]]))  # |z| = 5 -> scale 4/5
+    assert float(re) == pytest.approx(2.4, rel=1e-5) and float(im) == pytest.approx(3.2, rel=1e-5)
+    re, im = act(torch.tensor([[0.3]]), torch.tensor([[0.4]]))  # below threshold -> 0
+    assert float(re) == 0.0 and float(im) == 0.0
+    zr, zi = zReLU()(torch.tensor([1.0, -1.0, 2.0]), torch.tensor([1.0, 1.0, -2.0]))
+    assert zr.tolist() == [1.0, 0.0, 0.0] and zi.tolist() == [1.0, 0.0, 0.0]
+
+
+def test_covariance_bn_whitens() -> None:
+    torch.manual_seed(0)
+    bn = CovarianceComplexBatchNorm(4)
+    re = torch.randn(4096, 4) * 3 + 1
+    im = 0.5 * re + torch.randn(4096, 4)
+    with torch.no_grad():
+        wr, wi = bn(re, im)
+    assert float(wr.mean().abs()) < 1e-4 and float(wi.mean().abs()) < 1e-4
+    cov = torch.stack([wr.flatten(), wi.flatten()]).cov()
+    np.testing.assert_allclose(cov.numpy(), np.eye(2), atol=5e-3)
+
+
+def test_residual_factory_builds() -> None:
+    cfg = build_cvnn_config(
+        dtype=FullPrecisionDType.float32,
+        layers=[ResidualCfg(body=SequentialCfg(layers=[LinearCfg(width=ExplicitWidth(value=16))]),
+                            activation=ActivationCfg(kind=ActivationKind.Z_RELU))],
+        seed=5).unwrap()
+    net = build_model(n_inputs=6, n_outputs=8, cfg=cfg).unwrap()
+    re, im = net(torch.randn(3, 6), torch.zeros(3, 6))
+    assert re.shape == (3, 8) and im.shape == (3, 8)
+
+
+def test_build_model_leaves_caller_rng_untouched() -> None:
+    torch.manual_seed(77)
+    before = torch.get_rng_state()
+    make(123, [32], 128, torch.float32)
+    assert torch.equal(before, torch.get_rng_state())

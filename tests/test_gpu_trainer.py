@@ -1,0 +1,183 @@
+"""GbmCVNNPricer on the HIP path vs the oracle step, plus the reference trainer's determinism
+contracts (tests/test_gbm_trainer.py:170-320): lock-step bit-exactness, snapshot/resume,
+Adam state round trip, predict_price."""
+
+from __future__ import annotations
+
+import copy
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from spectralmc.gbm import BlackScholes
+from spectralmc.gbm_trainer import GbmCVNNPricer
+from spectralmc.models.numerical import Precision
+from tests.helpers import (
+    expect_success,
+    make_black_scholes_config,
+    make_domain_bounds,
+    make_gbm_cvnn_config,
+    make_simulation_params,
+    make_test_cvnn,
+    make_training_config,
+    max_param_diff,
+)
+
+pytestmark = pytest.mark.gpu
+
+T, N, M = 16, 128, 4
+
+
+def _sim(dtype: Precision = Precision.float32, mc_seed: int = 7):
+    return make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=M, threads_per_block=256,
+                                  mc_seed=mc_seed, buffer_size=512, dtype=dtype)
+
+
+def _pricer(seed: int = 123, dtype: torch.dtype = torch.float32, warmup: int | None = None, **cfg_kw):
+    prec = Precision.float32 if dtype == torch.float32 else Precision.float64
+    sp = _sim(prec)
+    model = make_test_cvnn(n_inputs=6, n_outputs=N, seed=seed, dtype=dtype)
+    cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                               domain_bounds=make_domain_bounds(), **cfg_kw)
+    p = expect_success(GbmCVNNPricer.create(cfg))
+    if warmup is not None:
+        p.warmup_steps = warmup
+    return p, model
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_one_step_matches_oracle(oracle, dtype) -> None:
+    B = 32
+    pricer, model = _pricer(dtype=dtype, warmup=0)
+    cpu_model = copy.deepcopy(model).cpu()
+    res = expect_success(pricer.train(make_training_config(num_batches=1, batch_size=B, learning_rate=1e-2)))
+
+    lo, hi = make_domain_bounds().arrays()
+    contracts = oracle.sobol_contracts(7, 0, B, lo, hi)
+    sdt = "float32" if dtype == torch.float32 else "float64"
+    targets = oracle.training_targets(contracts, T, N, M, seed=7, ordinal0=0, dtype=sdt)
+    adam = torch.optim.Adam(cpu_model.parameters(), lr=1e-2)
+    x = torch.tensor(contracts, dtype=dtype)
+    ref = oracle.torch_step(cpu_model, x, torch.zeros_like(x), torch.from_numpy(targets), adam)
+
+    assert res.final_loss == pytest.approx(ref.loss, rel=1e-4)          # spectral-loss match, 1e-4 rel
+    assert res.final_grad_norm == pytest.approx(ref.grad_norm, rel=1e-3)
+    for (name, pg), pc in zip(model.named_parameters(), cpu_model.parameters(), strict=True):
+        a, b = pg.detach().cpu().double(), pc.detach().double()
+        rel = float((a - b).norm() / max(float(b.norm()), 1e-12))
+        assert rel < 1e-4, (name, rel)
+
+
+def test_graph_replay_matches_eager() -> None:
+    eager, m_e = _pricer(warmup=0)
+    graph, m_g = _pricer(warmup=1)
+    cfg = make_training_config(num_batches=5, batch_size=16)
+    r_e = expect_success(eager.train(cfg))
+    r_g = expect_success(graph.train(cfg))
+    assert max_param_diff(m_e, m_g) == 0.0
+    assert r_e.final_loss == r_g.final_loss
+
+
+def test_lockstep_training_is_bit_exact() -> None:
+    a, ma = _pricer()
+    b, mb = _pricer()
+    assert max_param_diff(ma, mb) == 0.0
+    cfg = make_training_config(num_batches=4, batch_size=24)
+    expect_success(a.train(cfg))
+    expect_success(b.train(cfg))
+    assert max_param_diff(ma, mb) == 0.0
+
+
+def test_snapshot_restore_continues_identically() -> None:
+    cfg2 = make_training_config(num_batches=2, batch_size=16)
+    straight, m_s = _pricer()
+    expect_success(straight.train(make_training_config(num_batches=4, batch_size=16)))
+
+    first, m_f = _pricer()
+    r1 = expect_success(first.train(cfg2))
+    snap = r1.updated_config
+    assert snap.global_step == 2 and snap.sobol_skip == 32
+    assert snap.cfg.sim_params.skip == 32  # normal matrices served (async_normals.py:400-413)
+    resumed = expect_success(GbmCVNNPricer.create(snap))
+    expect_success(resumed.train(cfg2))
+    assert max_param_diff(m_s, m_f) == 0.0
+
+
+def test_adam_state_round_trip() -> None:
+    p, _ = _pricer()
+    r = expect_success(p.train(make_training_config(num_batches=2, batch_size=8)))
+    st = r.updated_config.optimizer_state
+    assert st is not None and len(st.param_states) == len(list(r.updated_config.cvnn.parameters()))
+    back = expect_success(st.to_torch())
+    again = expect_success(type(st).from_torch(back))
+    for pid, ps in st.param_states.items():
+        assert ps.step == 2
+        assert torch.equal(expect_success(ps.exp_avg.to_torch()), expect_success(again.param_states[pid].exp_avg.to_torch()))
+
+
+def test_multi_chunk_equals_single_chunk(monkeypatch) -> None:
+    import spectralmc_amd.engine as eng
+
+    a, ma = _pricer(warmup=0)
+    expect_success(a.train(make_training_config(num_batches=2, batch_size=20)))
+    monkeypatch.setattr(eng, "DEFAULT_PATH_BUFFER_BYTES", 3 * T * N * M * 4)  # 3 contracts per launch
+    b, mb = _pricer(warmup=0)
+    expect_success(b.train(make_training_config(num_batches=2, batch_size=20)))
+    assert max_param_diff(ma, mb) == 0.0
+
+
+def test_terminal_only_store_mode_same_result() -> None:
+    a, ma = _pricer()
+    b, mb = _pricer()
+    b.store_paths = False
+    cfg = make_training_config(num_batches=3, batch_size=16)
+    expect_success(a.train(cfg))
+    expect_success(b.train(cfg))
+    assert max_param_diff(ma, mb) == 0.0
+
+
+def test_predict_price_finite_and_parity() -> None:
+    p, _ = _pricer()
+    expect_success(p.train(make_training_config(num_batches=3, batch_size=16)))
+    contracts = [BlackScholes.Inputs(X0=100.0, K=95.0, T=0.5, r=0.03, d=0.01, v=0.25),
+                 BlackScholes.Inputs(X0=120.0, K=105.0, T=1.0, r=0.02, d=0.0, v=0.30)]
+    out = expect_success(p.predict_price(contracts))
+    assert len(out) == 2
+    for r, c in zip(out, contracts):
+        vals = r.model_dump().values()
+        assert all(math.isfinite(v) for v in vals)
+        fwd = c.X0 * math.exp((c.r - c.d) * c.T)
+        assert r.call_price - r.put_price == pytest.approx(fwd - c.K * math.exp(-c.r * c.T), rel=1e-9, abs=1e-9)
+    assert expect_success(p.predict_price([])) == []
+
+
+def test_gbm_engine_price_vs_black(oracle) -> None:
+    """BlackScholes.price_to_host against the closed form (reference tests/test_gbm.py:103-139)."""
+    sp = make_simulation_params(timesteps=1, network_size=256, batches_per_mc_run=1024, mc_seed=31,
+                                buffer_size=1, dtype=Precision.float32)
+    bs = BlackScholes(make_black_scholes_config(sim_params=sp))
+    rng = np.random.default_rng(31)
+    errs = []
+    for _ in range(16):
+        c = BlackScholes.Inputs(X0=float(rng.uniform(50, 150)), K=float(rng.uniform(50, 150)),
+                                T=float(rng.uniform(0.1, 2.0)), r=float(rng.uniform(0.0, 0.08)),
+                                d=float(rng.uniform(0.0, 0.04)), v=float(rng.uniform(0.1, 0.6)))
+        host = expect_success(bs.price_to_host(c))
+        ref = oracle.black_put(c.X0, c.K, c.T, c.r, c.d, c.v)
+        if ref > 1.0:
+            errs.append((host.put_price - ref) / ref)
+    rmspe = float(np.sqrt(np.mean(np.square(errs))))
+    assert rmspe < 0.02
+    snap = expect_success(bs.snapshot())
+    assert snap.sim_params.skip == 16
+
+
+def test_normalized_paths_hit_forwards() -> None:
+    sp = make_simulation_params(timesteps=8, network_size=64, batches_per_mc_run=64, mc_seed=5, buffer_size=1)
+    bs = BlackScholes(make_black_scholes_config(sim_params=sp))
+    c = BlackScholes.Inputs(X0=80.0, K=90.0, T=1.5, r=0.04, d=0.01, v=0.35)
+    sr = expect_success(bs._simulate(c))
+    means = sr.sims.double().mean(dim=1)
+    torch.testing.assert_close(means, sr.forwards.double(), rtol=2e-6, atol=0)
