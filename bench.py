@@ -44,6 +44,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
+    ap.add_argument("--math", default="portable", choices=["portable", "hw"])
     ap.add_argument("--kernel-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU-baseline sample")
@@ -147,6 +148,7 @@ def main() -> None:
                                domain_bounds=make_domain_bounds())
     pricer = expect_success(GbmCVNNPricer.create(cfg))
     pricer.store_paths = args.store == "all"
+    pricer.math_mode = args.math
     pricer.warmup_steps = max(1, min(2, args.warmup))
     tcfg = make_training_config(num_batches=args.warmup + args.steps, batch_size=B, learning_rate=1e-2)
     session = expect_success(pricer.open_session(tcfg))
@@ -182,7 +184,7 @@ def main() -> None:
         def run_kernel() -> None:
             _lib.check(L.smc_train_targets(_lib.ptr(b.contracts), eng.B, eng.T, eng.N, eng.M, eng.seed, None, 0,
                                            eng._scheme, eng._norm, eng._dtype_code, eng.store_mode,
-                                           _lib.ptr(eng.paths), eng.chunk, _lib.ptr(eng.rowsum),
+                                           _lib.ptr(eng.paths), eng.chunk, None,
                                            _lib.ptr(b.targets), _lib.stream_handle(stream)))
 
         run_kernel()
@@ -204,7 +206,7 @@ def main() -> None:
         try:
             with open(tpath) as f:
                 tj = json.load(f)
-            key = f"{args.config}_{args.store}"
+            key = f"{args.config}_{args.store}_{args.math}"
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
@@ -228,7 +230,7 @@ def main() -> None:
         "data": "synthetic: Sobol contracts (seed 7, make_domain_bounds defaults), random-init CVNN (seed 123)",
         "config": {"workload": desc, "contracts_per_gpu": B, "global_contracts": world * B, "paths": P,
                    "timesteps": T, "network_size": N, "batches_per_mc_run": M,
-                   "path_store": args.store, "parallelism": f"dp{world}"},
+                   "path_store": args.store, "math": args.math, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": "contract_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_launch,

@@ -55,6 +55,9 @@ extern "C" {
 #define SMC_NORM_NORMALIZE       1  /* ForwardNormalization.NORMALIZE                    */
 #define SMC_DTYPE_F32            0  /* Precision.float32 (paths f32, targets complex64)  */
 #define SMC_DTYPE_F64            1  /* Precision.float64 (paths f64, targets complex128) */
+#define SMC_MATH_HW          0x100  /* flag, OR into `scheme` (engine calls) or `dtype` (smc_normals):
+                                      f32 hardware transcendentals (v_exp/v_log/v_sin/v_cos/v_sqrt)
+                                      instead of the portable, CPU-reproducible kernels */
 #define SMC_STORE_TERMINAL       1  /* keep only the terminal row [B][P] (scratch)        */
 #define SMC_STORE_ALL            2  /* materialise the full path matrix [B][T][P]         */
 

@@ -10,14 +10,21 @@
  *   normals   reference src/spectralmc/async_normals.py:212-216 draws a (T, P) N(0,1) matrix
  *             per contract from CuPy XORWOW (absent here: normal-level parity with CuPy is
  *             unpinned).  Here: Philox4x32-10 (Salmon et al., SC'11; KAT-pinned in tests)
- *             seeds xoshiro128** (Blackman & Vigna) per (contract ordinal, path); Box-Muller
- *             in double precision, rounded to the sim dtype like the reference's normal array.
- *   paths     reference src/spectralmc/gbm.py:241-257: the Numba kernel's arguments are Python
- *             floats, so the recursion runs in f64 and only the stores round to the sim dtype.
+ *             seeds xoshiro128+ (Blackman & Vigna) per (contract ordinal, path); Box-Muller.
+ *             f32: ln / sin / cos from the portable IEEE-only kernels below (bit-identical
+ *             to the device's); f64: libm.
+ *
+ * Two modes:
+ *   REFERENCE  (oracle_gbm_paths): reference src/spectralmc/gbm.py:241-257 — the Numba
+ *             kernel's arguments are Python floats, so the recursion runs in f64 and only the
+ *             stores round to the sim dtype.
  *             LOG_EULER:    X *= exp((r - d - v^2/2) dt + v dW),  dW = Z sqrt(dt)
  *             SIMPLE_EULER: X += (r - d) X dt + v X dW;  X = |X|
- *   row sums  reference gbm.py:437 (cp.mean over the P stored values): f64 sum of the stored
- *             values, divided by P by the caller.
+ *             Row sums: f64 sums of the stored values (gbm.py:437 cp.mean, up to order).
+ *   KERNEL     (oracle_kernel_*): the same GBM recursion in f32 with the portable exp2, the
+ *             HIP engine's reduction orders (per-lane chunk sums, wave butterfly, waves 0..7)
+ *             and its CF arithmetic — an exact restatement of what the f32 HIP kernels compute,
+ *             so GPU results can be checked bit-for-bit.
  *
  * Build: make -C oracle   (gcc -O2 -fopenmp, no GPU needed)
  */
@@ -60,10 +67,10 @@ typedef struct {
 
 static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
 
-/* xoshiro128** 1.1, reference implementation order. */
+/* xoshiro128+ 1.0, reference implementation order. */
 static inline uint32_t xoshiro_next(xoshiro128* g) {
   uint32_t* s = g->s;
-  const uint32_t result = rotl32(s[1] * 5u, 7) * 9u;
+  const uint32_t result = s[0] + s[3];
   const uint32_t t = s[1] << 9;
   s[2] ^= s[0];
   s[3] ^= s[1];
@@ -74,6 +81,111 @@ static inline uint32_t xoshiro_next(xoshiro128* g) {
   return result;
 }
 
+
+/* ---- portable f32 math: op-for-op restatement of spectralmc_amd/csrc/smc_math.h ------
+ * (coefficients from tools/fit_poly.py; compile with -ffp-contract=off) */
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+static float log1p_q(float f) {
+  float q = 0.08743945509195328f;
+  q = fmaf(q, f, -0.14377330243587494f);
+  q = fmaf(q, f, 0.14949095249176025f);
+  q = fmaf(q, f, -0.16560696065425873f);
+  q = fmaf(q, f, 0.19956977665424347f);
+  q = fmaf(q, f, -0.2500215470790863f);
+  q = fmaf(q, f, 0.3333418369293213f);
+  q = fmaf(q, f, -0.49999988079071045f);
+  q = fmaf(q, f, 1.0f);
+  return q;
+}
+
+static float log_pos(float u) {
+  const uint32_t bits = f2u(u);
+  int e = (int)(bits >> 23) - 127;
+  uint32_t mb = (bits & 0x007FFFFFu) | 0x3F800000u;
+  const int hi = mb > 0x3FB504F3u;
+  if (hi) { mb -= 0x00800000u; e += 1; }
+  const float f = u2f(mb) - 1.0f;
+  const float lf = f * log1p_q(f);
+  return fmaf((float)e, 0.693147182f, lf);
+}
+
+static void sincos2pi_u24(uint32_t j, float* s_out, float* c_out) {
+  const int k = (int)((j + (1u << 21)) >> 22);
+  const int rem = (int)j - (k << 22);
+  const float r = (float)rem * 0x1p-24f;
+  const float r2 = r * r;
+  float sp = 41.48561096191406f;
+  sp = fmaf(sp, r2, -76.69829559326172f);
+  sp = fmaf(sp, r2, 81.60520935058594f);
+  sp = fmaf(sp, r2, -41.34170150756836f);
+  sp = fmaf(sp, r2, 6.2831854820251465f);
+  const float s = r * sp;
+  float c = 59.24250793457031f;
+  c = fmaf(c, r2, -85.44358825683594f);
+  c = fmaf(c, r2, 64.93932342529297f);
+  c = fmaf(c, r2, -19.739208221435547f);
+  c = fmaf(c, r2, 1.0f);
+  const int odd = k & 1;
+  const uint32_t sflip = (uint32_t)(k & 2) << 30;
+  const uint32_t cflip = (uint32_t)((k + 1) & 2) << 30;
+  *s_out = u2f(f2u(odd ? c : s) ^ sflip);
+  *c_out = u2f(f2u(odd ? s : c) ^ cflip);
+}
+
+static float exp2_any(float y) {
+  const float n = rintf(y);
+  const float f = y - n;
+  float p = 0.00015337577497120947f;
+  p = fmaf(p, f, 0.0013399859890341759f);
+  p = fmaf(p, f, 0.009618519805371761f);
+  p = fmaf(p, f, 0.05550329014658928f);
+  p = fmaf(p, f, 0.24022646248340607f);
+  p = fmaf(p, f, 0.6931471824645996f);
+  p = fmaf(p, f, 1.0f);
+  return ldexpf(p, (int)n);
+}
+
+static float exp_any(float x) { return exp2_any(x * 1.44269502f); }
+
+static void twiddle(int64_t j, int64_t N, double* s_out, double* c_out) {
+  const int64_t num = 4 * j;
+  const int64_t k = (2 * num + N) / (2 * N);
+  const int64_t rem = num - k * N;
+  const double r = (double)rem / (double)(4 * N);
+  const double x = r * 6.283185307179586;
+  const double u = x * x;
+  double s = 2.8114572543455206e-15;
+  s = fma(s, -u, 7.647163731819816e-13);
+  s = fma(s, -u, 1.6059043836821613e-10);
+  s = fma(s, -u, 2.505210838544172e-08);
+  s = fma(s, -u, 2.7557319223985893e-06);
+  s = fma(s, -u, 0.0001984126984126984);
+  s = fma(s, -u, 0.008333333333333333);
+  s = fma(s, -u, 0.16666666666666666);
+  s = fma(s, -u, 1.0);
+  s = s * x;
+  double c = 1.5619206968586225e-16;
+  c = fma(c, -u, 4.779477332387385e-14);
+  c = fma(c, -u, 1.1470745597729725e-11);
+  c = fma(c, -u, 2.08767569878681e-09);
+  c = fma(c, -u, 2.755731922398589e-07);
+  c = fma(c, -u, 2.48015873015873e-05);
+  c = fma(c, -u, 0.001388888888888889);
+  c = fma(c, -u, 0.041666666666666664);
+  c = fma(c, -u, 0.5);
+  c = fma(c, -u, 1.0);
+  const int q = (int)(k & 3);
+  const double sb = (q & 1) ? c : s, cb = (q & 1) ? s : c;
+  *s_out = (q & 2) ? -sb : sb;
+  *c_out = ((q + 1) & 2) ? -cb : cb;
+}
+
+float oracle_log_pos(float u) { return log_pos(u); }
+float oracle_exp2(float y) { return exp2_any(y); }
+void oracle_sincos2pi_u24(uint32_t j, float* s, float* c) { sincos2pi_u24(j, s, c); }
+
 static void path_stream(uint64_t seed, uint64_t ordinal, uint64_t path, xoshiro128* g) {
   const uint32_t ctr[4] = {(uint32_t)path, (uint32_t)(path >> 32), (uint32_t)ordinal, (uint32_t)(ordinal >> 32)};
   const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
@@ -81,26 +193,25 @@ static void path_stream(uint64_t seed, uint64_t ordinal, uint64_t path, xoshiro1
   if ((g->s[0] | g->s[1] | g->s[2] | g->s[3]) == 0u) g->s[0] = 1u;
 }
 
-/* One Box-Muller pair; f32 streams use 24-bit uniforms, f64 streams 32-bit ones. */
+/* One Box-Muller pair.  f32: 24-bit uniforms and the portable kernels (bit-identical to the
+ * device); f64: 32-bit uniforms and libm. */
 static void normal_pair(xoshiro128* g, int is_f64, double* z0, double* z1) {
   const uint32_t a = xoshiro_next(g), b = xoshiro_next(g);
-  double u1, u2;
   if (is_f64) {
-    u1 = ((double)a + 1.0) * 0x1p-32;
-    u2 = (double)b * 0x1p-32;
+    const double u1 = ((double)a + 1.0) * 0x1p-32;
+    const double u2 = (double)b * 0x1p-32;
+    const double r = sqrt(-2.0 * log(u1));
+    const double th = 6.283185307179586476925286766559 * u2;
+    *z0 = r * cos(th);
+    *z1 = r * sin(th);
   } else {
-    u1 = (double)((a >> 8) + 1u) * 0x1p-24;
-    u2 = (double)(b >> 8) * 0x1p-24;
+    const float u1 = (float)((a >> 8) + 1u) * 0x1p-24f;
+    const float r = sqrtf(-2.0f * log_pos(u1));
+    float sn, cs;
+    sincos2pi_u24(b >> 8, &sn, &cs);
+    *z0 = (double)(r * cs);
+    *z1 = (double)(r * sn);
   }
-  const double r = sqrt(-2.0 * log(u1));
-  const double th = 6.283185307179586476925286766559 * u2;
-  double zc = r * cos(th), zs = r * sin(th);
-  if (!is_f64) {  /* the reference keeps normals in the sim dtype (async_normals.py:215) */
-    zc = (double)(float)zc;
-    zs = (double)(float)zs;
-  }
-  *z0 = zc;
-  *z1 = zs;
 }
 
 /* normals[t][p] of contract ordinal `ordinal` (dtype 0: f32 out, 1: f64 out). */
@@ -195,4 +306,143 @@ int32_t oracle_num_threads(void) {
 #else
   return 1;
 #endif
+}
+
+/* ======================================================================================
+ * KERNEL mode: exact restatement of the f32 HIP engine (spectralmc_amd/csrc/gbm.hip).
+ * ====================================================================================== */
+#define K_THREADS 512
+#define K_PPL 4
+#define K_CHUNK (K_THREADS * K_PPL)
+#define K_WAVES (K_THREADS / 64)
+
+/* paths: [B][T][P] (optional), terminal [B][P] (optional), rowsum [B][T] (required) */
+void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t P, uint64_t seed, int64_t ordinal0,
+                         int32_t scheme, float* paths, float* terminal, double* rowsum) {
+  const double kLog2e = 1.4426950408889634;
+  float* X = (float*)malloc(sizeof(float) * (size_t)T * (size_t)P);
+  double* lane_acc = (double*)malloc(sizeof(double) * (size_t)K_THREADS * (size_t)T);
+  for (int64_t b = 0; b < B; ++b) {
+    const double* c = contracts + 6 * b;
+    const double dt = c[2] / (double)T;
+    const double sq = sqrt(dt);
+    float ca, cb;
+    if (scheme == 0) {
+      const double drift = c[3] - c[4] - 0.5 * c[5] * c[5];
+      ca = (float)(drift * dt * kLog2e);
+      cb = (float)(c[5] * sq * kLog2e);
+    } else {
+      ca = (float)((c[3] - c[4]) * dt);
+      cb = (float)(c[5] * sq);
+    }
+    const float x0 = (float)c[0];
+    const uint64_t ordinal = (uint64_t)(ordinal0 + b);
+#pragma omp parallel for schedule(static)
+    for (int64_t p = 0; p < P; ++p) {
+      xoshiro128 g;
+      path_stream(seed, ordinal, (uint64_t)p, &g);
+      float x = x0, z0 = 0.0f, z1 = 0.0f;
+      for (int t = 0; t < T; ++t) {
+        if ((t & 1) == 0) {
+          double d0, d1;
+          normal_pair(&g, 0, &d0, &d1);
+          z0 = (float)d0;
+          z1 = (float)d1;
+        }
+        const float z = (t & 1) ? z1 : z0;
+        if (scheme == 0)
+          x = x * exp2_any(fmaf(cb, z, ca));
+        else
+          x = fabsf(fmaf(x, fmaf(cb, z, ca), x));
+        X[(int64_t)t * P + p] = x;
+      }
+    }
+    if (paths) memcpy(paths + b * (int64_t)T * P, X, sizeof(float) * (size_t)T * (size_t)P);
+    if (terminal) memcpy(terminal + b * P, X + (int64_t)(T - 1) * P, sizeof(float) * (size_t)P);
+    /* per lane: sequential over chunks of f32 4-path partial sums, accumulated in f64 */
+    memset(lane_acc, 0, sizeof(double) * (size_t)K_THREADS * (size_t)T);
+    for (int64_t chunk = 0; chunk < P; chunk += K_CHUNK)
+      for (int lane = 0; lane < K_THREADS; ++lane) {
+        const int64_t p0 = chunk + (int64_t)K_PPL * lane;
+        for (int t = 0; t < T; ++t) {
+          float part = 0.0f;
+          for (int j = 0; j < K_PPL; ++j) part += (p0 + j < P) ? X[(int64_t)t * P + p0 + j] : 0.0f;
+          lane_acc[(size_t)lane * T + t] += (double)part;
+        }
+      }
+    for (int t = 0; t < T; ++t) {
+      double tot = 0.0;
+      for (int w = 0; w < K_WAVES; ++w) {
+        double v[64], nv[64];
+        for (int l = 0; l < 64; ++l) v[l] = lane_acc[(size_t)(64 * w + l) * T + t];
+        for (int off = 32; off >= 1; off >>= 1) {
+          for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+          memcpy(v, nv, sizeof(v));
+        }
+        tot += v[0];
+      }
+      rowsum[b * T + t] = tot;
+    }
+  }
+  free(lane_acc);
+  free(X);
+}
+
+/* targets: [B][N] interleaved complex64 (re, im) */
+void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, int32_t normalize,
+                      const float* terminal, const double* terminal_sum, float* targets) {
+  const int64_t P = (int64_t)N * M;
+  const int G = N <= K_THREADS ? K_THREADS / N : 1;
+  const int items = N * G;
+  double* part = (double*)malloc(sizeof(double) * (size_t)items);
+  double* avg = (double*)malloc(sizeof(double) * (size_t)N);
+  double* cs = (double*)malloc(sizeof(double) * (size_t)N);
+  double* sn = (double*)malloc(sizeof(double) * (size_t)N);
+  for (int j = 0; j < N; ++j) twiddle(j, N, &sn[j], &cs[j]);
+  for (int64_t b = 0; b < B; ++b) {
+    const double* c = contracts + 6 * b;
+    const float Tm = (float)c[2];
+    const float F = (float)c[0] * exp_any((float)(c[3] - c[4]) * Tm);
+    const float df = exp_any((float)(-c[3]) * Tm);
+    const float s = normalize ? F / (float)(terminal_sum[b] / (double)P) : 1.0f;
+    const float K = (float)c[1];
+    const float* row = terminal + b * P;
+    for (int item = 0; item < items; ++item) {
+      const int n = item % N, g = item / N;
+      double sum = 0.0;
+      for (int m = g; m < M; m += G) {
+        const float xs = row[(int64_t)m * N + n] * s;
+        const float diff = K - xs;
+        const float pay = df * (diff > 0.0f ? diff : 0.0f);
+        sum += (double)pay;
+      }
+      part[item] = sum;
+    }
+    for (int n = 0; n < N; ++n) {
+      double tot = 0.0;
+      for (int g = 0; g < G; ++g) tot += part[g * N + n];
+      avg[n] = tot / (double)M;
+    }
+    float* out = targets + 2 * b * N;
+    for (int k = 0; k <= N / 2; ++k) {
+      double re = 0.0, im = 0.0;
+      int idx = 0;
+      for (int n = 0; n < N; ++n) {
+        re = fma(avg[n], cs[idx], re);
+        im = fma(-avg[n], sn[idx], im);
+        idx += k;
+        if (idx >= N) idx -= N;
+      }
+      out[2 * k] = (float)re;
+      out[2 * k + 1] = (float)im;
+      if (k != 0 && 2 * k != N) {
+        out[2 * (N - k)] = (float)re;
+        out[2 * (N - k) + 1] = (float)(-im);
+      }
+    }
+  }
+  free(part);
+  free(avg);
+  free(cs);
+  free(sn);
 }

@@ -59,6 +59,15 @@ def lib() -> ctypes.CDLL:
                                        ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
         L.oracle_num_threads.restype = ctypes.c_int32
+        L.oracle_kernel_paths.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
+                                          ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_kernel_cf.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_log_pos.argtypes = [ctypes.c_float]
+        L.oracle_log_pos.restype = ctypes.c_float
+        L.oracle_exp2.argtypes = [ctypes.c_float]
+        L.oracle_exp2.restype = ctypes.c_float
         _lib = L
     return _lib
 
@@ -172,6 +181,38 @@ def training_targets(contracts: np.ndarray, timesteps: int, network_size: int, b
     _, terminal, rowsum = gbm_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme, dtype,
                                     want_paths=False, threads=threads)
     return cf_targets(contracts, terminal, rowsum[:, -1], network_size, batches, normalize)
+
+
+# --------------------------------------------------------------------------- kernel mode
+def kernel_paths(contracts: np.ndarray, timesteps: int, n_paths: int, seed: int, ordinal0: int = 0,
+                 scheme: int = 0, want_paths: bool = False) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
+    """f32 KERNEL mode: exact restatement of the HIP engine (paths, terminal, rowsum in its order)."""
+    contracts = np.ascontiguousarray(contracts, dtype=np.float64)
+    B = contracts.shape[0]
+    paths = np.empty((B, timesteps, n_paths), dtype=np.float32) if want_paths else None
+    terminal = np.empty((B, n_paths), dtype=np.float32)
+    rowsum = np.empty((B, timesteps), dtype=np.float64)
+    lib().oracle_kernel_paths(_ptr(contracts), B, timesteps, n_paths, seed, ordinal0, scheme, _ptr(paths),
+                              _ptr(terminal), _ptr(rowsum))
+    return paths, terminal, rowsum
+
+
+def kernel_cf(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndarray, network_size: int,
+              batches: int, normalize: bool = True) -> np.ndarray:
+    contracts = np.ascontiguousarray(contracts, dtype=np.float64)
+    terminal = np.ascontiguousarray(terminal, dtype=np.float32)
+    terminal_sum = np.ascontiguousarray(terminal_sum, dtype=np.float64)
+    out = np.empty((contracts.shape[0], network_size), dtype=np.complex64)
+    lib().oracle_kernel_cf(_ptr(contracts), contracts.shape[0], network_size, batches, int(normalize),
+                           _ptr(terminal), _ptr(terminal_sum), _ptr(out))
+    return out
+
+
+def kernel_targets(contracts: np.ndarray, timesteps: int, network_size: int, batches: int, seed: int,
+                   ordinal0: int = 0, scheme: int = 0, normalize: bool = True) -> tuple[np.ndarray, np.ndarray]:
+    """(targets [B,N] complex64, rowsum [B,T]) exactly as the f32 HIP engine computes them."""
+    _, terminal, rowsum = kernel_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme)
+    return kernel_cf(contracts, terminal, rowsum[:, -1], network_size, batches, normalize), rowsum
 
 
 # --------------------------------------------------------------------------- CVNN step

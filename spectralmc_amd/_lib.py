@@ -13,7 +13,7 @@ import threading
 from typing import Any
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspectralmc_hip.so")
+LIB_PATH = os.environ.get("SMC_LIB_PATH") or os.path.join(_HERE, "libspectralmc_hip.so")
 
 # status codes (spectralmc_hip.h)
 SMC_OK = 0
@@ -31,6 +31,7 @@ NORM_NORMALIZE = 1
 DTYPE_F32 = 0
 DTYPE_F64 = 1
 STORE_TERMINAL = 1
+MATH_HW = 0x100
 STORE_ALL = 2
 SOBOL_BITS = 30
 ABI_VERSION = 1

@@ -23,7 +23,10 @@
 
 #include <cmath>
 
+#pragma clang fp contract(off)
+
 #include "smc_internal.h"
+#include "smc_math.h"
 #include "smc_rng.h"
 
 namespace smc {
@@ -53,6 +56,7 @@ struct EngineArgs {
   int32_t normalize;
   int32_t store;              // SMC_STORE_TERMINAL or SMC_STORE_ALL
   int32_t simulate;           // 0: paths/rowsum already in memory (smc_cf_targets)
+  int32_t all_rows;           // 1: sum every row (rowsum[B][T]); 0: terminal row only
   void* paths;
   double* rowsum;             // [B][T] or NULL
   void* targets;              // [B][N] complex or NULL
@@ -90,9 +94,9 @@ __device__ __forceinline__ double wave_sum(double x) {
   return x;
 }
 
-// One step of the path recursion.  For f32 log-Euler the coefficients are pre-scaled by
-// log2(e) so the step is fma + v_exp_f32 + mul.
-template <typename Real, bool LOG_EULER>
+// One step of the path recursion.  f32 log-Euler works in log2 units (coefficients
+// pre-scaled by log2 e) with the portable exp2 of smc_math.h; f64 uses OCML exp.
+template <typename Real, bool LOG_EULER, bool HW>
 struct Stepper {
   Real a, b;
 
@@ -112,7 +116,8 @@ struct Stepper {
 
   __device__ __forceinline__ Real operator()(Real x, Real z) const {
     if constexpr (LOG_EULER) {
-      if constexpr (sizeof(Real) == 4) return x * __builtin_amdgcn_exp2f(fmaf(b, z, a));
+      if constexpr (sizeof(Real) == 4 && HW) return x * __builtin_amdgcn_exp2f(fmaf(b, z, a));
+      else if constexpr (sizeof(Real) == 4) return x * math::exp2_any(fmaf(b, z, a));
       else return x * exp(fma(b, z, a));
     }
     if constexpr (sizeof(Real) == 4) return fabsf(fmaf(x, fmaf(b, z, a), x));
@@ -120,92 +125,125 @@ struct Stepper {
   }
 };
 
-// ---- phase 1: simulate the contract's P paths ----------------------------------------
-// Returns (in lds_tot[0..T)) the f64 sum over paths of every row.
-template <typename Real, int TT, bool LOG_EULER>
-__device__ void simulate_contract(const EngineArgs& a, const Contract& c, uint64_t ordinal,
-                                  int64_t b, double* lds_acc, double* lds_tot) {
+constexpr int kRowBlock = 16;  // rows accumulated in registers per pass over the paths
+
+// The 4 paths p0..p0+3 of one lane: steps [0, t0) are replayed without output (only when
+// T > kRowBlock), rows [t0, t0 + nrows) are stored and added to acc[].  MASKED handles the
+// ragged last chunk (nvalid < 4) and P % 4 != 0 with scalar stores; otherwise one dwordx4
+// store per row, addressed as (wave-uniform row base) + (32-bit lane offset).
+template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS, bool MASKED, bool FULLBLOCK>
+__device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
+                                           uint64_t ordinal, int64_t chunk, int nvalid, int t0, int nrows,
+                                           Real* contract_base, double (&acc)[ALLROWS ? kRowBlock : 1]) {
   using V4 = typename Vec4T<Real>::type;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int T = TT > 0 ? TT : a.T;
+  const int T = a.T;
   const int64_t P = a.P;
   const bool store_all = a.store == SMC_STORE_ALL;
-  Real* base = static_cast<Real*>(a.paths) + (store_all ? b * T * P : b * P);
-  const bool vec_ok = (P % kPathsPerLane) == 0;
-  const Stepper<Real, LOG_EULER> step(c, T);
-  const Real x0 = static_cast<Real>(c.X0);
-
-  if constexpr (TT == 0) {
-    for (int i = tid; i < kWaves * T; i += kThreads) lds_acc[i] = 0.0;
-    __syncthreads();
+  const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
+  PathStream s[kPathsPerLane] = {PathStream(a.seed, ordinal, p0), PathStream(a.seed, ordinal, p0 + 1),
+                                 PathStream(a.seed, ordinal, p0 + 2), PathStream(a.seed, ordinal, p0 + 3)};
+  Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
+#pragma unroll
+  for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
+  for (int t = 0; t < t0; t += 2) {  // t0 is a multiple of kRowBlock (even)
+#pragma unroll
+    for (int j = 0; j < kPathsPerLane; ++j) {
+      s[j].template normal_pair<HW>(zl[j], zh[j]);
+      x[j] = step(step(x[j], zl[j]), zh[j]);
+    }
   }
-  double acc[TT > 0 ? TT : 1];
+  // wave-uniform row base (SGPR pair) + 32-bit per-lane byte offset
+  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(Real)) * threadIdx.x;
+  Real* chunk_base = contract_base + chunk;
 #pragma unroll
-  for (int t = 0; t < (TT > 0 ? TT : 1); ++t) acc[t] = 0.0;
-
-  for (int64_t chunk = 0; chunk < P; chunk += kChunk) {
-    const int64_t p0 = chunk + kPathsPerLane * tid;
-    const int nvalid = static_cast<int>(p0 >= P ? 0 : (P - p0 >= kPathsPerLane ? kPathsPerLane : P - p0));
-    const bool full = vec_ok && nvalid == kPathsPerLane;
-    PathStream s[kPathsPerLane] = {PathStream(a.seed, ordinal, p0), PathStream(a.seed, ordinal, p0 + 1),
-                                   PathStream(a.seed, ordinal, p0 + 2), PathStream(a.seed, ordinal, p0 + 3)};
-    Real x[kPathsPerLane], zh[kPathsPerLane], zl[kPathsPerLane];
+  for (int i = 0; i < kRowBlock; ++i) {
+    if (FULLBLOCK || i < nrows) {
+      const int t = t0 + i;
+      if ((i & 1) == 0) {
 #pragma unroll
-    for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
-
-    auto body = [&](int t) {
-      if ((t & 1) == 0) {
-#pragma unroll
-        for (int j = 0; j < kPathsPerLane; ++j) s[j].normal_pair(zl[j], zh[j]);
+        for (int j = 0; j < kPathsPerLane; ++j) s[j].template normal_pair<HW>(zl[j], zh[j]);
       }
 #pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (t & 1) ? zh[j] : zl[j]);
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (i & 1) ? zh[j] : zl[j]);
       if (store_all || t == T - 1) {
-        Real* row = base + (store_all ? static_cast<int64_t>(t) * P : 0) + p0;
-        if (full) {
+        char* row = reinterpret_cast<char*>(chunk_base + (store_all ? static_cast<int64_t>(t) * P : 0));
+        if constexpr (!MASKED) {
           V4 v4;
           v4.x = x[0];
           v4.y = x[1];
           v4.z = x[2];
           v4.w = x[3];
-          *reinterpret_cast<V4*>(row) = v4;
+          *reinterpret_cast<V4*>(row + lane_off) = v4;
         } else {
+          Real* r = reinterpret_cast<Real*>(row + lane_off);
 #pragma unroll
           for (int j = 0; j < kPathsPerLane; ++j)
-            if (j < nvalid) row[j] = x[j];
+            if (j < nvalid) r[j] = x[j];
         }
       }
-      Real part = 0;
+      if (ALLROWS || t == T - 1) {
+        Real part = 0;
 #pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) part += (j < nvalid) ? x[j] : Real(0);
-      return static_cast<double>(part);
-    };
-
-    if constexpr (TT > 0) {
-#pragma unroll
-      for (int t = 0; t < TT; ++t) acc[t] += body(t);
-    } else {
-      for (int t = 0; t < T; ++t) {
-        const double w = wave_sum(body(t));
-        if (lane == 0) lds_acc[wave * T + t] += w;
+        for (int j = 0; j < kPathsPerLane; ++j) part += (!MASKED || j < nvalid) ? x[j] : Real(0);
+        acc[ALLROWS ? i : 0] += static_cast<double>(part);
       }
     }
   }
+}
 
-  if constexpr (TT > 0) {
+// ---- phase 1: simulate the contract's P paths ----------------------------------------
+// Fills lds_tot[0..T) (ALLROWS) or lds_tot[T-1] with the f64 sum over paths of the row(s),
+// in a fixed order: per lane sequentially over its chunks, wave butterfly (xor 32..1),
+// waves 0..7.  Training needs only the terminal row's sum (its normalisation scale).
+template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
+__device__ void simulate_contract(const EngineArgs& a, const Contract& c, uint64_t ordinal, int64_t b,
+                                  double* lds_acc, double* lds_tot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = a.T;
+  const int64_t P = a.P;
+  const bool store_all = a.store == SMC_STORE_ALL;
+  Real* base = static_cast<Real*>(a.paths) + (store_all ? b * T * P : b * P);
+  const bool vec_ok = (P % kPathsPerLane) == 0;
+  const int64_t full_end = vec_ok ? (P / kChunk) * kChunk : 0;
+  const Stepper<Real, LOG_EULER, HW> step(c, T);
+  const Real x0 = static_cast<Real>(c.X0);
+  constexpr int kAcc = ALLROWS ? kRowBlock : 1;
+
+  for (int t0 = 0; t0 < T; t0 += kRowBlock) {
+    const int nrows = T - t0 < kRowBlock ? T - t0 : kRowBlock;
+    double acc[kAcc];
 #pragma unroll
-    for (int t = 0; t < TT; ++t) {
-      const double w = wave_sum(acc[t]);
-      if (lane == 0) lds_acc[wave * TT + t] = w;
+    for (int i = 0; i < kAcc; ++i) acc[i] = 0.0;
+    int64_t chunk = 0;
+    if (nrows == kRowBlock) {  // branch-free fast path: whole 16-row block, whole 2048-path chunks
+      for (; chunk < full_end; chunk += kChunk)
+        lane_paths<Real, LOG_EULER, HW, ALLROWS, false, true>(a, step, x0, ordinal, chunk, kPathsPerLane, t0, nrows,
+                                                              base, acc);
+    }
+    for (; chunk < P; chunk += kChunk) {  // everything else: ragged rows / paths, scalar stores
+      const int64_t p0 = chunk + kPathsPerLane * tid;
+      const int nvalid = static_cast<int>(p0 >= P ? 0 : (P - p0 >= kPathsPerLane ? kPathsPerLane : P - p0));
+      lane_paths<Real, LOG_EULER, HW, ALLROWS, true, false>(a, step, x0, ordinal, chunk, nvalid, t0, nrows, base,
+                                                            acc);
+    }
+    if (ALLROWS || t0 + nrows == T) {  // rows of this block whose sums are wanted
+#pragma unroll
+      for (int i = 0; i < kAcc; ++i) {
+        if (i < nrows) {
+          const double w = wave_sum(acc[i]);
+          if (lane == 0) lds_acc[wave * kRowBlock + i] = w;
+        }
+      }
+      __syncthreads();
+      const int first = ALLROWS ? 0 : nrows - 1;  // !ALLROWS: only the terminal row, kept in slot 0
+      if (tid >= first && tid < nrows) {
+        double tot = 0.0;
+        for (int w = 0; w < kWaves; ++w) tot += lds_acc[w * kRowBlock + (ALLROWS ? tid : 0)];
+        lds_tot[t0 + tid] = tot;
+      }
+      __syncthreads();
     }
   }
-  __syncthreads();
-  for (int t = tid; t < T; t += kThreads) {
-    double tot = 0.0;
-    for (int w = 0; w < kWaves; ++w) tot += lds_acc[w * T + t];
-    lds_tot[t] = tot;
-  }
-  __syncthreads();
 }
 
 // ---- phases 2+3: normalised put payoff, mean over M batches, real-input DFT ------------
@@ -220,16 +258,16 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
   const Real* row = static_cast<const Real*>(a.paths) + (store_all ? (b * T + (T - 1)) * P : b * P);
 
   // Reference scalar semantics: gbm.py:429-431 evaluate times/forwards/df in the sim dtype.
-  Real F, df, s;
+  Real F, df;
   const Real Tm = static_cast<Real>(c.T);
   if constexpr (sizeof(Real) == 4) {
-    F = static_cast<float>(c.X0) * expf(static_cast<float>(c.r - c.d) * Tm);
-    df = expf(static_cast<float>(-c.r) * Tm);
+    F = static_cast<float>(c.X0) * math::exp_any(static_cast<float>(c.r - c.d) * Tm);
+    df = math::exp_any(static_cast<float>(-c.r) * Tm);
   } else {
     F = c.X0 * exp((c.r - c.d) * Tm);
     df = exp(-c.r * Tm);
   }
-  s = a.normalize ? F / static_cast<Real>(terminal_sum / static_cast<double>(P)) : Real(1);
+  const Real s = a.normalize ? F / static_cast<Real>(terminal_sum / static_cast<double>(P)) : Real(1);
   const Real K = static_cast<Real>(c.K);
 
   const int G = N <= kThreads ? kThreads / N : 1;
@@ -245,16 +283,12 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
     for (int m = g; m < M; m += G) {
       const Real xs = row[static_cast<int64_t>(m) * N + n] * s;  // sims *= scale (rounded to Real)
       const Real diff = K - xs;
-      sum += static_cast<double>(df * (diff > Real(0) ? diff : Real(0)));
+      const Real pay = df * (diff > Real(0) ? diff : Real(0));
+      sum += static_cast<double>(pay);
     }
     part[item] = sum;
   }
-  for (int j = tid; j < N; j += kThreads) {
-    double sj, cj;
-    sincospi(2.0 * static_cast<double>(j) / static_cast<double>(N), &sj, &cj);
-    cs[j] = cj;
-    sn[j] = sj;
-  }
+  for (int j = tid; j < N; j += kThreads) math::twiddle(j, N, sn[j], cs[j]);
   __syncthreads();
   for (int n = tid; n < N; n += kThreads) {
     double tot = 0.0;
@@ -283,27 +317,25 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
   }
 }
 
-template <typename Real, int TT>
+template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
 __global__ __launch_bounds__(kThreads) void contract_kernel(EngineArgs a) {
   extern __shared__ double lds[];
   const int64_t b = blockIdx.x;
   const Contract c = load_contract(a.contracts + b * 6);
-  const int T = TT > 0 ? TT : a.T;
+  const int T = a.T;
   double* lds_tot = lds;               // [T]
   double* lds_work = lds + T;          // simulate: [kWaves][T]; cf: part/avg/cs/sn
   double terminal_sum;
   if (a.simulate) {
     const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
-    if (a.scheme == SMC_SCHEME_LOG_EULER)
-      simulate_contract<Real, TT, true>(a, c, ordinal, b, lds_work, lds_tot);
-    else
-      simulate_contract<Real, TT, false>(a, c, ordinal, b, lds_work, lds_tot);
-    if (a.rowsum)
+    simulate_contract<Real, LOG_EULER, HW, ALLROWS>(a, c, ordinal, b, lds_work, lds_tot);
+    if (ALLROWS && a.rowsum)
       for (int t = threadIdx.x; t < T; t += kThreads) a.rowsum[b * T + t] = lds_tot[t];
     terminal_sum = lds_tot[T - 1];
   } else {
     terminal_sum = a.rowsum[b * T + (T - 1)];
   }
+  if (!ALLROWS && a.rowsum && threadIdx.x == 0 && a.simulate) a.rowsum[b * T + (T - 1)] = terminal_sum;
   if (a.targets) {
     __syncthreads();  // workgroup-scope fence: phase-1 stores of the terminal row are visible
     cf_targets_contract<Real>(a, c, b, terminal_sum, lds_work);
@@ -325,7 +357,7 @@ __global__ __launch_bounds__(256) void normalize_kernel(const double* __restrict
     const double t64 = (t == T - 1) ? c.T : dt + static_cast<double>(t) * step;
     Real F;
     if constexpr (sizeof(Real) == 4)
-      F = static_cast<float>(c.X0) * expf(static_cast<float>(c.r - c.d) * static_cast<float>(t64));
+      F = static_cast<float>(c.X0) * math::exp_any(static_cast<float>(c.r - c.d) * static_cast<float>(t64));
     else
       F = c.X0 * exp((c.r - c.d) * t64);
     const Real scale = F / static_cast<Real>(rowsum[rowi] / static_cast<double>(P));
@@ -334,7 +366,7 @@ __global__ __launch_bounds__(256) void normalize_kernel(const double* __restrict
   }
 }
 
-template <typename Real>
+template <typename Real, bool HW>
 __global__ __launch_bounds__(256) void normals_kernel(uint64_t seed, uint64_t ordinal, int32_t rows,
                                                       int64_t cols, Real* __restrict__ out) {
   const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -342,7 +374,7 @@ __global__ __launch_bounds__(256) void normals_kernel(uint64_t seed, uint64_t or
   PathStream s(seed, ordinal, static_cast<uint64_t>(p));
   Real z0 = 0, z1 = 0;
   for (int t = 0; t < rows; ++t) {
-    if ((t & 1) == 0) s.normal_pair(z0, z1);
+    if ((t & 1) == 0) s.template normal_pair<HW>(z0, z1);
     out[static_cast<int64_t>(t) * cols + p] = (t & 1) ? z1 : z0;
   }
 }
@@ -350,7 +382,7 @@ __global__ __launch_bounds__(256) void normals_kernel(uint64_t seed, uint64_t or
 // ---- host-side launch helpers ------------------------------------------------------------
 size_t lds_bytes(int T, int N, bool cf) {
   size_t doubles = static_cast<size_t>(T);                       // lds_tot
-  size_t work = static_cast<size_t>(kWaves) * T;                 // simulate accumulators
+  size_t work = static_cast<size_t>(kWaves) * kRowBlock;         // per-wave row partials
   if (cf) {
     const size_t cfw = static_cast<size_t>(N > kThreads ? N : kThreads) + 3 * static_cast<size_t>(N);
     if (cfw > work) work = cfw;
@@ -358,9 +390,9 @@ size_t lds_bytes(int T, int N, bool cf) {
   return (doubles + work) * sizeof(double);
 }
 
-template <typename Real, int TT>
-int32_t launch_engine_tt(const EngineArgs& a, size_t lds, hipStream_t stream) {
-  auto kernel = contract_kernel<Real, TT>;
+template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
+int32_t launch_engine_k(const EngineArgs& a, size_t lds, hipStream_t stream) {
+  auto kernel = contract_kernel<Real, LOG_EULER, HW, ALLROWS>;
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds)) != hipSuccess) {
@@ -378,14 +410,34 @@ int32_t launch_engine(const EngineArgs& a, hipStream_t stream) {
   const bool cf = a.targets != nullptr;
   const size_t lds = lds_bytes(a.T, a.N, cf);
   if (lds > kMaxLds) return fail(SMC_ERR_INVALID_SHAPE, "engine: timesteps/network_size exceed the LDS budget");
-  if (a.simulate && a.T == 16) return launch_engine_tt<Real, 16>(a, lds, stream);
-  return launch_engine_tt<Real, 0>(a, lds, stream);
+  const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+  const bool hw = (a.scheme & SMC_MATH_HW) != 0 && sizeof(Real) == 4;
+  const bool allrows = a.all_rows != 0;
+#define SMC_LAUNCH(LE, HWM, AR) \
+  if (log_euler == LE && hw == HWM && allrows == AR) return launch_engine_k<Real, LE, HWM, AR>(a, lds, stream);
+  SMC_LAUNCH(true, false, false)
+  SMC_LAUNCH(true, false, true)
+  SMC_LAUNCH(false, false, false)
+  SMC_LAUNCH(false, false, true)
+  if constexpr (sizeof(Real) == 4) {
+    SMC_LAUNCH(true, true, false)
+    SMC_LAUNCH(true, true, true)
+    SMC_LAUNCH(false, true, false)
+    SMC_LAUNCH(false, true, true)
+  }
+#undef SMC_LAUNCH
+  return fail(SMC_ERR_INVALID_ARGUMENT, "engine: unsupported scheme / math mode");
 }
 
 int32_t dispatch_engine(const EngineArgs& a, int32_t dtype, hipStream_t stream) {
   if (dtype == SMC_DTYPE_F32) return launch_engine<float>(a, stream);
   if (dtype == SMC_DTYPE_F64) return launch_engine<double>(a, stream);
   return fail(SMC_ERR_INVALID_ARGUMENT, "engine: dtype must be SMC_DTYPE_F32 or SMC_DTYPE_F64");
+}
+
+bool valid_scheme(int32_t scheme) {
+  const int32_t base = scheme & 0xff, flags = scheme & ~0xff;
+  return (base == SMC_SCHEME_LOG_EULER || base == SMC_SCHEME_SIMPLE_EULER) && (flags & ~SMC_MATH_HW) == 0;
 }
 
 int32_t validate_common(const double* contracts, int64_t B, int32_t T, int64_t P, int32_t dtype) {
@@ -411,10 +463,9 @@ int32_t smc_gbm_simulate(const double* contracts_dev, int64_t n_contracts, int32
                          int32_t dtype, void* paths_dev, double* rowsum_dev, void* stream) {
   if (int32_t st = validate_common(contracts_dev, n_contracts, timesteps, n_paths, dtype)) return st;
   if (!paths_dev) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_gbm_simulate: paths_dev is NULL");
-  if (scheme != SMC_SCHEME_LOG_EULER && scheme != SMC_SCHEME_SIMPLE_EULER)
-    return fail(SMC_ERR_INVALID_ARGUMENT, "smc_gbm_simulate: bad scheme");
+  if (!valid_scheme(scheme)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_gbm_simulate: bad scheme");
   EngineArgs a{contracts_dev, n_contracts, timesteps, n_paths, 1, 1, mc_seed, ordinal_dev, ordinal0,
-               scheme, 0, SMC_STORE_ALL, 1, paths_dev, rowsum_dev, nullptr};
+               scheme, 0, SMC_STORE_ALL, 1, 1, paths_dev, rowsum_dev, nullptr};
   return dispatch_engine(a, dtype, as_stream(stream));
 }
 
@@ -444,7 +495,7 @@ int32_t smc_cf_targets(const double* contracts_dev, int64_t n_contracts, int32_t
   if (!paths_dev || !rowsum_dev || !targets_dev)
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cf_targets: NULL buffer");
   EngineArgs a{contracts_dev, n_contracts, timesteps, P, network_size, batches_per_mc_run, 0, nullptr, 0,
-               SMC_SCHEME_LOG_EULER, normalization != SMC_NORM_RAW, SMC_STORE_ALL, 0,
+               SMC_SCHEME_LOG_EULER, normalization != SMC_NORM_RAW, SMC_STORE_ALL, 0, 0,
                const_cast<void*>(paths_dev), const_cast<double*>(rowsum_dev), targets_dev};
   return dispatch_engine(a, dtype, as_stream(stream));
 }
@@ -460,15 +511,15 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
   if (!paths_dev || !targets_dev) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_targets: NULL buffer");
   if (store_mode != SMC_STORE_ALL && store_mode != SMC_STORE_TERMINAL)
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_targets: bad store_mode");
-  if (scheme != SMC_SCHEME_LOG_EULER && scheme != SMC_SCHEME_SIMPLE_EULER)
-    return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_targets: bad scheme");
+  if (!valid_scheme(scheme)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_targets: bad scheme");
   if (chunk_contracts <= 0) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_targets: chunk_contracts <= 0");
   const size_t esz = dtype == SMC_DTYPE_F32 ? sizeof(float) : sizeof(double);
   const size_t csz = dtype == SMC_DTYPE_F32 ? 2 * sizeof(float) : 2 * sizeof(double);
   for (int64_t off = 0; off < n_contracts; off += chunk_contracts) {
     const int64_t nb = n_contracts - off < chunk_contracts ? n_contracts - off : chunk_contracts;
     EngineArgs a{contracts_dev + off * 6, nb, timesteps, P, network_size, batches_per_mc_run, mc_seed,
-                 ordinal_dev, ordinal0 + off, scheme, normalization != SMC_NORM_RAW, store_mode, 1, paths_dev,
+                 ordinal_dev, ordinal0 + off, scheme, normalization != SMC_NORM_RAW, store_mode, 1,
+                 rowsum_dev ? 1 : 0, paths_dev,
                  rowsum_dev ? rowsum_dev + off * timesteps : nullptr,
                  static_cast<char*>(targets_dev) + static_cast<size_t>(off) * network_size * csz};
     (void)esz;
@@ -482,11 +533,16 @@ int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t col
   if (!out_dev) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_normals: out_dev is NULL");
   if (rows <= 0 || cols <= 0 || ordinal < 0) return fail(SMC_ERR_INVALID_SHAPE, "smc_normals: bad shape");
   const unsigned blocks = static_cast<unsigned>((cols + 255) / 256);
-  if (dtype == SMC_DTYPE_F32)
-    hipLaunchKernelGGL(normals_kernel<float>, dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
+  const bool hw = (dtype & SMC_MATH_HW) != 0;
+  dtype &= 0xff;
+  if (dtype == SMC_DTYPE_F32 && !hw)
+    hipLaunchKernelGGL((normals_kernel<float, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
+                       static_cast<uint64_t>(ordinal), rows, cols, static_cast<float*>(out_dev));
+  else if (dtype == SMC_DTYPE_F32)
+    hipLaunchKernelGGL((normals_kernel<float, true>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
                        static_cast<uint64_t>(ordinal), rows, cols, static_cast<float*>(out_dev));
   else if (dtype == SMC_DTYPE_F64)
-    hipLaunchKernelGGL(normals_kernel<double>, dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
+    hipLaunchKernelGGL((normals_kernel<double, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
                        static_cast<uint64_t>(ordinal), rows, cols, static_cast<double*>(out_dev));
   else
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_normals: bad dtype");

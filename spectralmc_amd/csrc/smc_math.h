@@ -1,0 +1,147 @@
+// Portable transcendental kernels for the f32 path engine.
+//
+// Every function here is a fixed sequence of IEEE-754 operations that round identically on
+// gfx950 and on an x86 host (fmaf, +, -, *, correctly rounded sqrtf and division, exact
+// ldexpf, integer bit manipulation) — no hardware approximations (v_exp/v_log/v_sin_f32)
+// and no contraction freedom (`fp contract(off)`, every fused op written as fmaf).  The
+// CPU oracle (oracle/gbm_oracle.c, "kernel mode") restates the same sequences, so paths,
+// row sums and CF targets are bit-identical between the GPU and the CPU restatement.
+//
+// Cost on CDNA4: the hardware transcendentals issue at quarter rate, so these full-rate
+// FMA polynomials cost about the same VALU time.
+//
+// Coefficients: tools/fit_poly.py (near-minimax least squares on Chebyshev nodes,
+// rounded to f32): |rel err| log1p 1.4e-7, exp2 7.6e-8; |abs err| sin/cos(2 pi r) 8e-8.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#pragma clang fp contract(off)
+
+namespace smc {
+namespace math {
+
+// ln(1 + f) / f on f in [sqrt(1/2) - 1, sqrt(2) - 1], degree 8
+__device__ __forceinline__ float log1p_q(float f) {
+  float q = 0.08743945509195328f;
+  q = fmaf(q, f, -0.14377330243587494f);
+  q = fmaf(q, f, 0.14949095249176025f);
+  q = fmaf(q, f, -0.16560696065425873f);
+  q = fmaf(q, f, 0.19956977665424347f);
+  q = fmaf(q, f, -0.2500215470790863f);
+  q = fmaf(q, f, 0.3333418369293213f);
+  q = fmaf(q, f, -0.49999988079071045f);
+  q = fmaf(q, f, 1.0f);
+  return q;
+}
+
+// Natural log of a positive normal float.
+__device__ __forceinline__ float log_pos(float u) {
+  uint32_t bits = __float_as_uint(u);
+  int e = static_cast<int>(bits >> 23) - 127;
+  uint32_t mb = (bits & 0x007FFFFFu) | 0x3F800000u;  // m in [1, 2)
+  const bool hi = mb > 0x3FB504F3u;                  // m > sqrt(2): use m / 2, e + 1
+  mb -= hi ? 0x00800000u : 0u;
+  e += hi ? 1 : 0;
+  const float f = __uint_as_float(mb) - 1.0f;        // exact (Sterbenz)
+  const float lf = f * log1p_q(f);
+  return fmaf(static_cast<float>(e), 0.693147182f, lf);
+}
+
+// sin(2 pi r) / r and cos(2 pi r) as polynomials in r^2, r in [-1/8, 1/8]
+__device__ __forceinline__ float sin2pi_s(float r2) {
+  float s = 41.48561096191406f;
+  s = fmaf(s, r2, -76.69829559326172f);
+  s = fmaf(s, r2, 81.60520935058594f);
+  s = fmaf(s, r2, -41.34170150756836f);
+  s = fmaf(s, r2, 6.2831854820251465f);
+  return s;
+}
+
+__device__ __forceinline__ float cos2pi_c(float r2) {
+  float c = 59.24250793457031f;
+  c = fmaf(c, r2, -85.44358825683594f);
+  c = fmaf(c, r2, 64.93932342529297f);
+  c = fmaf(c, r2, -19.739208221435547f);
+  c = fmaf(c, r2, 1.0f);
+  return c;
+}
+
+// (sin, cos)(2 pi j 2^-24) for a 24-bit integer j: exact quarter-turn reduction.
+__device__ __forceinline__ void sincos2pi_u24(uint32_t j, float& s_out, float& c_out) {
+  const int k = static_cast<int>((j + (1u << 21)) >> 22);          // nearest quarter turn, 0..4
+  const int rem = static_cast<int>(j) - (k << 22);                 // [-2^21, 2^21)
+  const float r = static_cast<float>(rem) * 0x1p-24f;              // exact, |r| <= 1/8
+  const float r2 = r * r;
+  const float s = r * sin2pi_s(r2);
+  const float c = cos2pi_c(r2);
+  // rotate by k quarter turns without branches: sin <- (s, c, -s, -c), cos <- (c, -s, -c, s)
+  const bool odd = (k & 1) != 0;
+  const uint32_t sflip = static_cast<uint32_t>(k & 2) << 30;
+  const uint32_t cflip = static_cast<uint32_t>((k + 1) & 2) << 30;
+  s_out = __uint_as_float(__float_as_uint(odd ? c : s) ^ sflip);
+  c_out = __uint_as_float(__float_as_uint(odd ? s : c) ^ cflip);
+}
+
+// 2^f on f in [-1/2, 1/2], degree 6
+__device__ __forceinline__ float exp2_p(float f) {
+  float p = 0.00015337577497120947f;
+  p = fmaf(p, f, 0.0013399859890341759f);
+  p = fmaf(p, f, 0.009618519805371761f);
+  p = fmaf(p, f, 0.05550329014658928f);
+  p = fmaf(p, f, 0.24022646248340607f);
+  p = fmaf(p, f, 0.6931471824645996f);
+  p = fmaf(p, f, 1.0f);
+  return p;
+}
+
+// 2^y: round-to-nearest-even integer split (v_rndne_f32), polynomial, exact ldexp.
+__device__ __forceinline__ float exp2_any(float y) {
+  const float n = rintf(y);
+  const float f = y - n;  // exact, in [-1/2, 1/2]
+  return ldexpf(exp2_p(f), static_cast<int>(n));
+}
+
+__device__ __forceinline__ float exp_any(float x) { return exp2_any(x * 1.44269502f); }
+
+// ---- f64: twiddles cos/sin(2 pi j / N) of the N-point DFT -------------------------------
+// Exact integer reduction to the nearest quarter turn, then Taylor series in x = 2 pi r,
+// |x| <= pi/4 (terms to x^17 / x^18: truncation < 1e-19).
+__device__ __forceinline__ void twiddle(int64_t j, int64_t N, double& s_out, double& c_out) {
+  const int64_t num = 4 * j;
+  const int64_t k = (2 * num + N) / (2 * N);         // round(4 j / N)
+  const int64_t rem = num - k * N;                    // |rem| <= N / 2
+  const double r = static_cast<double>(rem) / static_cast<double>(4 * N);
+  const double x = r * 6.283185307179586;
+  const double u = x * x;
+  double s = 2.8114572543455206e-15;                   // 1/17!
+  s = fma(s, -u, 7.647163731819816e-13);               // 1/15!
+  s = fma(s, -u, 1.6059043836821613e-10);              // 1/13!
+  s = fma(s, -u, 2.505210838544172e-08);               // 1/11!
+  s = fma(s, -u, 2.7557319223985893e-06);              // 1/9!
+  s = fma(s, -u, 0.0001984126984126984);               // 1/7!
+  s = fma(s, -u, 0.008333333333333333);                // 1/5!
+  s = fma(s, -u, 0.16666666666666666);                 // 1/3!
+  s = fma(s, -u, 1.0);
+  s = s * x;
+  double c = 1.5619206968586225e-16;                   // 1/18!
+  c = fma(c, -u, 4.779477332387385e-14);               // 1/16!
+  c = fma(c, -u, 1.1470745597729725e-11);              // 1/14!
+  c = fma(c, -u, 2.08767569878681e-09);                // 1/12!
+  c = fma(c, -u, 2.755731922398589e-07);               // 1/10!
+  c = fma(c, -u, 2.48015873015873e-05);                // 1/8!
+  c = fma(c, -u, 0.001388888888888889);                // 1/6!
+  c = fma(c, -u, 0.041666666666666664);                // 1/4!
+  c = fma(c, -u, 0.5);                                 // 1/2!
+  c = fma(c, -u, 1.0);
+  const int q = static_cast<int>(k & 3);
+  const bool odd = (q & 1) != 0;
+  const double sb = odd ? c : s, cb = odd ? s : c;
+  s_out = (q & 2) ? -sb : sb;
+  c_out = ((q + 1) & 2) ? -cb : cb;
+}
+
+}  // namespace math
+}  // namespace smc

@@ -7,22 +7,28 @@
 //
 //   seed state  = Philox4x32-10( counter = (path_lo, path_hi, ordinal_lo, ordinal_hi),
 //                                key     = (mc_seed_lo, mc_seed_hi) )      [Salmon et al. 2011]
-//   u32 stream  = xoshiro128** seeded with that 128-bit state          [Blackman & Vigna 2018]
+//   u32 stream  = xoshiro128+ seeded with that 128-bit state            [Blackman & Vigna 2018]
+//                 (only the top 24 bits of each output are used: the "+" scrambler's weak
+//                 low bits never reach a normal)
 //   normals     = Box-Muller on consecutive u32 pairs (a, b):
-//                   u1 = ((a >> 8) + 1) * 2^-24 in (0, 1],  u2 = (b >> 8) * 2^-24 in [0, 1)   (f32)
+//                   u1 = ((a >> 8) + 1) * 2^-24 in (0, 1],  j = b >> 8 (angle 2 pi j 2^-24)   (f32)
 //                   u1 = (a + 1) * 2^-32,                   u2 = b * 2^-32                    (f64)
 //                   z0 = sqrt(-2 ln u1) cos(2 pi u2),  z1 = sqrt(-2 ln u1) sin(2 pi u2)
+//                 f32: ln / sin / cos are the portable kernels of smc_math.h, so the normals
+//                 are bit-identical to the CPU restatement.
 //   normal t of a path is z_(t mod 2) of pair t / 2.
 //
 // Philox runs once per path (its round keys are wave-uniform, so the key schedule lives
-// in SGPRs); each further u32 costs ~10 integer VALU ops with no 32-bit multiply, which
-// keeps the path kernel on the HBM side of the VALU/HBM ridge.  oracle/gbm_oracle.c
+// in SGPRs); each further u32 costs 8 integer VALU ops with no 32-bit multiply, which
+// keeps the RNG a minor share of the path kernel's VALU budget.  oracle/gbm_oracle.c
 // restates the same stream on the CPU.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+
+#include "smc_math.h"
 
 namespace smc {
 
@@ -56,7 +62,7 @@ struct PathStream {
   }
 
   __device__ __forceinline__ uint32_t next() {
-    const uint32_t result = __builtin_rotateleft32(s1 * 5u, 7) * 9u;
+    const uint32_t result = s0 + s3;
     const uint32_t t = s1 << 9;
     s2 ^= s0;
     s3 ^= s1;
@@ -67,17 +73,29 @@ struct PathStream {
     return result;
   }
 
-  // Two N(0,1) draws, single precision, hardware transcendentals
-  // (v_log_f32 = log2, v_sin/cos_f32 take revolutions).
+  // Two N(0,1) draws, single precision.  HW = false: portable IEEE-only arithmetic
+  // (smc_math.h), bit-identical to the CPU oracle.  HW = true (SMC_MATH_HW): quarter-rate
+  // hardware transcendentals (v_log / v_sqrt / v_sin / v_cos_f32), ~1 ulp, not reproducible
+  // on a CPU.
+  template <bool HW>
   __device__ __forceinline__ void normal_pair(float& z0, float& z1) {
     const uint32_t a = next(), b = next();
     const float u1 = static_cast<float>((a >> 8) + 1u) * 0x1p-24f;
-    const float u2 = static_cast<float>(b >> 8) * 0x1p-24f;
-    const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln 2 log2(u1)
-    z0 = r * __builtin_amdgcn_cosf(u2);
-    z1 = r * __builtin_amdgcn_sinf(u2);
+    if constexpr (HW) {
+      const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln2 log2 u1
+      const float u2 = static_cast<float>(b >> 8) * 0x1p-24f;
+      z0 = r * __builtin_amdgcn_cosf(u2);  // v_cos_f32 takes revolutions
+      z1 = r * __builtin_amdgcn_sinf(u2);
+    } else {
+      const float r = __builtin_sqrtf(-2.0f * math::log_pos(u1));
+      float sn, cs;
+      math::sincos2pi_u24(b >> 8, sn, cs);
+      z0 = r * cs;
+      z1 = r * sn;
+    }
   }
 
+  template <bool HW>
   __device__ __forceinline__ void normal_pair(double& z0, double& z1) {
     const uint32_t a = next(), b = next();
     const double u1 = (static_cast<double>(a) + 1.0) * 0x1p-32;

@@ -19,6 +19,8 @@
 #include "smc_internal.h"
 #include "sobol_dirnums.h"
 
+#pragma clang fp contract(off)  // numpy rounds (upper - lower) * raw and + lower separately
+
 namespace {
 
 using u128 = unsigned __int128;
@@ -166,9 +168,11 @@ __global__ void sobol_draw_kernel(const uint32_t* __restrict__ tables, int dim,
     for (int c = 0; c < SMC_SOBOL_BITS; ++c)
       x ^= ((g >> c) & 1u) ? svd[c] : 0u;
     const double raw = static_cast<double>(x) * 0x1p-30;
-    // numpy evaluates (upper - lower) * raw + lower with separate roundings: no FMA.
-    const double span = __dsub_rn(upper[d], lower[d]);
-    const double val = __dadd_rn(lower[d], __dmul_rn(span, raw));
+    // numpy evaluates (upper - lower) * raw + lower with separate roundings: no FMA
+    // (the file-level `fp contract(off)` covers these operators; header intrinsics would not).
+    const double span = upper[d] - lower[d];
+    const double prod = span * raw;
+    const double val = lower[d] + prod;
     out[i * dim + d] = val;
     if (out_f32) out_f32[i * dim + d] = static_cast<float>(val);
   }

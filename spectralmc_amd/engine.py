@@ -47,7 +47,7 @@ class TrainingEngine:
 
     def __init__(self, cfg: BlackScholesConfig, sampler: SobolSampler, batch_size: int, *, model_dtype: torch.dtype,
                  device: torch.device, rank: int = 0, world_size: int = 1, store_paths: bool = True,
-                 path_buffer_bytes: int | None = None) -> None:
+                 path_buffer_bytes: int | None = None, math: str = "portable") -> None:
         _lib.require_device()
         sp = cfg.sim_params
         self.cfg = cfg
@@ -62,7 +62,11 @@ class TrainingEngine:
         self.device = device
         self.sim_dtype = sp.dtype
         self._dtype_code = dtype_code(sp.dtype)
-        self._scheme = scheme_code(cfg.path_scheme)
+        if math not in ("portable", "hw"):
+            raise ValueError(f"math must be 'portable' or 'hw', got {math!r}")
+        self.math = math
+        # "hw": f32 hardware transcendentals in the path kernel (faster, ~1 ulp, not CPU-reproducible)
+        self._scheme = scheme_code(cfg.path_scheme) | (_lib.MATH_HW if math == "hw" else 0)
         self._norm = normalization_code(cfg.normalization)
         self.store_mode = _lib.STORE_ALL if store_paths else _lib.STORE_TERMINAL
         sim_torch = sp.dtype.to_torch()
@@ -83,7 +87,6 @@ class TrainingEngine:
         self.buffers = StepBuffers(contracts=contracts, real_in=real_in,
                                    imag_in=torch.zeros_like(real_in),
                                    targets=torch.empty((B, self.N), dtype=cplx, device=device))
-        self.rowsum = torch.empty((B, self.T), dtype=torch.float64, device=device)
         per_contract = (self.T * self.P if store_paths else self.P) * torch.finfo(sim_torch).bits // 8
         budget = path_buffer_bytes if path_buffer_bytes is not None else DEFAULT_PATH_BUFFER_BYTES
         self.chunk = max(1, min(B, budget // per_contract))
@@ -112,7 +115,7 @@ class TrainingEngine:
         _lib.check(L.smc_train_targets(
             _lib.ptr(b.contracts), self.B, self.T, self.N, self.M, self.seed, _lib.ptr(self.cursor[1:2]), offset,
             self._scheme, self._norm, self._dtype_code, self.store_mode, _lib.ptr(self.paths), self.chunk,
-            _lib.ptr(self.rowsum), _lib.ptr(b.targets), stream))
+            None, _lib.ptr(b.targets), stream))  # training needs only the terminal row sum (kept on chip)
         self.cursor.add_(self.global_batch)
         return b
 

@@ -295,6 +295,9 @@ class GbmCVNNPricer:
     warmup_steps: int = 2
     #: materialise the full [B][T][P] path matrix each step (the reference kernel's output contract)
     store_paths: bool = True
+    #: "portable": CPU-reproducible f32 transcendentals (bit-exact vs the oracle's kernel mode);
+    #: "hw": hardware transcendentals (faster, ~1 ulp, parity at the stated fp32 tolerance)
+    math_mode: str = "portable"
 
     @staticmethod
     def create(cfg: GbmCVNNPricerConfig) -> Result["GbmCVNNPricer", GbmPricerError]:
@@ -489,7 +492,7 @@ class GbmCVNNPricer:
         loss_v, gn = 0.0, 0.0
         try:
             engine = TrainingEngine(self._cfg, sampler, config.batch_size, model_dtype=self._dtype.to_torch(),
-                                    device=self._torch_device, store_paths=self.store_paths)
+                                    device=self._torch_device, store_paths=self.store_paths, math=self.math_mode)
         except _lib.SmcError as exc:
             return Failure(EngineFailure(code=exc.code, message=exc.message))
         engine.set_position(sobol_skip, self._mc_engine.ordinal)
@@ -612,7 +615,8 @@ class TrainingSession:
         pricer._cvnn.train()
         dev = pricer._torch_device
         self.engine = TrainingEngine(pricer._cfg, sampler, config.batch_size, model_dtype=pricer._dtype.to_torch(),
-                                     device=dev, rank=rank, world_size=world, store_paths=pricer.store_paths)
+                                     device=dev, rank=rank, world_size=world, store_paths=pricer.store_paths,
+                                     math=pricer.math_mode)
         self.params = list(pricer._cvnn.parameters())
         self.program = _StepProgram(pricer, self.engine, adam, self.params, ctx)
         self.sobol_skip0 = pricer._sobol_skip

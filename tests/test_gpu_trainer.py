@@ -70,6 +70,21 @@ def test_one_step_matches_oracle(oracle, dtype) -> None:
         assert rel < 1e-4, (name, rel)
 
 
+def test_hw_math_trainer_loss_within_tolerance(oracle) -> None:
+    B = 32
+    pricer, model = _pricer(warmup=0)
+    pricer.math_mode = "hw"
+    res = expect_success(pricer.train(make_training_config(num_batches=1, batch_size=B, learning_rate=1e-2)))
+    lo, hi = make_domain_bounds().arrays()
+    contracts = oracle.sobol_contracts(7, 0, B, lo, hi)
+    targets = oracle.training_targets(contracts, T, N, M, seed=7)
+    cpu_model = make_test_cvnn(n_inputs=6, n_outputs=N, seed=123, dtype=torch.float32, device="cpu")
+    x = torch.tensor(contracts, dtype=torch.float32)
+    ref = oracle.torch_step(cpu_model, x, torch.zeros_like(x), torch.from_numpy(targets),
+                            torch.optim.Adam(cpu_model.parameters(), lr=1e-2))
+    assert res.final_loss == pytest.approx(ref.loss, rel=1e-4)
+
+
 def test_graph_replay_matches_eager() -> None:
     eager, m_e = _pricer(warmup=0)
     graph, m_g = _pricer(warmup=1)

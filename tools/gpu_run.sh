@@ -1,0 +1,42 @@
+#!/bin/bash
+# GPU-box driver: runs named steps, each under its own time limit; stops the whole call at
+# the first fault / abort / timeout (exit >= 124, 134, 139) but continues past ordinary test
+# failures (exit 1).  Usage: tools/gpu_run.sh step1 step2 ...   (steps defined below)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {
+  local name=$1 limit=$2; shift 2
+  echo "[$(date +%T)] start $name"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"
+  tail -n 5 "$OUT/$name.log"
+  if [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ]; then
+    echo "fatal exit $rc in $name: stopping"
+    exit "$rc"
+  fi
+}
+
+for step in "$@"; do
+  case "$step" in
+    info)    run info 120 bash -c "rocm-smi --showproductname; nproc; python -c 'import torch;print(torch.__version__, torch.cuda.get_device_name(0))'" ;;
+    engine)  run engine 900 python -m pytest tests/test_gpu_engine.py -q -rf ;;
+    trainer) run trainer 900 python -m pytest tests/test_gpu_trainer.py -q -rf ;;
+    gputests) run gputests 1200 python -m pytest tests -m gpu -q -rf ;;
+    smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)   run bench 600 python bench.py ;;
+    bench_quick) run bench_quick 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    bench_hw) run bench_hw 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --math hw ;;
+    bench_hw_terminal) run bench_hw_terminal 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --store terminal --math hw ;;
+    bench_terminal) run bench_terminal 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --store terminal ;;
+    bench_c1) run bench_c1 600 python bench.py --config c1 --steps 50 --warmup 5 --no-cpu-baseline ;;
+    prof)    cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "all steps done"
