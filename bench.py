@@ -200,6 +200,26 @@ def main() -> None:
         48 * contracts_per_launch
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
 
+    # ---- measured HBM ceilings on this device (STREAM-style, 8 GiB buffers) --------------
+    stream_gbs = {}
+    if rank == 0:
+        n = (8 << 30) // 4
+        buf = torch.empty(n, dtype=torch.float32, device=dev)
+        src = torch.empty(n, dtype=torch.float32, device=dev)
+        for name, fn, nbytes in (("write", lambda: buf.fill_(1.0), 4 * n),
+                                 ("copy", lambda: buf.copy_(src), 8 * n)):
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                fn()
+            e1.record()
+            e1.synchronize()
+            stream_gbs[name] = nbytes * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        del buf, src
+        torch.cuda.empty_cache()
+
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
@@ -234,7 +254,9 @@ def main() -> None:
         "roofline": {"bound": "hbm", "kernel": "contract_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": bytes_launch,
-                     "contracts_per_launch": contracts_per_launch},
+                     "contracts_per_launch": contracts_per_launch,
+                     "measured_stream_gbs": stream_gbs,
+                     "frac_of_measured_write": (achieved / stream_gbs["write"]) if "write" in stream_gbs else None},
         "final_loss": final.loss,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

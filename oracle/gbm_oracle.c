@@ -10,7 +10,8 @@
  *   normals   reference src/spectralmc/async_normals.py:212-216 draws a (T, P) N(0,1) matrix
  *             per contract from CuPy XORWOW (absent here: normal-level parity with CuPy is
  *             unpinned).  Here: Philox4x32-10 (Salmon et al., SC'11; KAT-pinned in tests)
- *             seeds xoshiro128+ (Blackman & Vigna) per (contract ordinal, path); Box-Muller.
+ *             seeds xoshiro128+ (Blackman & Vigna) per (contract ordinal, group of 4 paths);
+ *             per step pair, the group's 4 paths draw one Box-Muller pair each, in path order.
  *             f32: ln / sin / cos from the portable IEEE-only kernels below (bit-identical
  *             to the device's); f64: libm.
  *
@@ -186,8 +187,10 @@ float oracle_log_pos(float u) { return log_pos(u); }
 float oracle_exp2(float y) { return exp2_any(y); }
 void oracle_sincos2pi_u24(uint32_t j, float* s, float* c) { sincos2pi_u24(j, s, c); }
 
-static void path_stream(uint64_t seed, uint64_t ordinal, uint64_t path, xoshiro128* g) {
-  const uint32_t ctr[4] = {(uint32_t)path, (uint32_t)(path >> 32), (uint32_t)ordinal, (uint32_t)(ordinal >> 32)};
+#define GROUP 4  /* paths per stream */
+
+static void path_stream(uint64_t seed, uint64_t ordinal, uint64_t group, xoshiro128* g) {
+  const uint32_t ctr[4] = {(uint32_t)group, (uint32_t)(group >> 32), (uint32_t)ordinal, (uint32_t)(ordinal >> 32)};
   const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   oracle_philox4x32_10(ctr, key, g->s);
   if ((g->s[0] | g->s[1] | g->s[2] | g->s[3]) == 0u) g->s[0] = 1u;
@@ -214,21 +217,39 @@ static void normal_pair(xoshiro128* g, int is_f64, double* z0, double* z1) {
   }
 }
 
+/* Normals of one group of 4 paths: z[t][j] for t < rows (f64 holder of dtype values). */
+static void group_normals(uint64_t seed, uint64_t ordinal, uint64_t group, int32_t rows, int is_f64, double* z) {
+  xoshiro128 g;
+  path_stream(seed, ordinal, group, &g);
+  for (int t = 0; t < rows; t += 2)
+    for (int j = 0; j < GROUP; ++j) {
+      double z0, z1;
+      normal_pair(&g, is_f64, &z0, &z1);
+      z[(int64_t)t * GROUP + j] = z0;
+      if (t + 1 < rows) z[(int64_t)(t + 1) * GROUP + j] = z1;
+    }
+}
+
 /* normals[t][p] of contract ordinal `ordinal` (dtype 0: f32 out, 1: f64 out). */
 void oracle_normals(uint64_t seed, int64_t ordinal, int32_t rows, int64_t cols, int32_t dtype, void* out) {
-#pragma omp parallel for schedule(static)
-  for (int64_t p = 0; p < cols; ++p) {
-    xoshiro128 g;
-    path_stream(seed, (uint64_t)ordinal, (uint64_t)p, &g);
-    double z0 = 0, z1 = 0;
-    for (int t = 0; t < rows; ++t) {
-      if ((t & 1) == 0) normal_pair(&g, dtype == 1, &z0, &z1);
-      const double z = (t & 1) ? z1 : z0;
-      if (dtype == 1)
-        ((double*)out)[(int64_t)t * cols + p] = z;
-      else
-        ((float*)out)[(int64_t)t * cols + p] = (float)z;
+  const int64_t groups = (cols + GROUP - 1) / GROUP;
+#pragma omp parallel
+  {
+    double* z = (double*)malloc(sizeof(double) * (size_t)(rows + 1) * GROUP);
+#pragma omp for schedule(static)
+    for (int64_t gi = 0; gi < groups; ++gi) {
+      group_normals(seed, (uint64_t)ordinal, (uint64_t)gi, rows, dtype == 1, z);
+      for (int t = 0; t < rows; ++t)
+        for (int j = 0; j < GROUP; ++j) {
+          const int64_t p = gi * GROUP + j;
+          if (p >= cols) continue;
+          if (dtype == 1)
+            ((double*)out)[(int64_t)t * cols + p] = z[(int64_t)t * GROUP + j];
+          else
+            ((float*)out)[(int64_t)t * cols + p] = (float)z[(int64_t)t * GROUP + j];
+        }
     }
+    free(z);
   }
 }
 
@@ -257,17 +278,20 @@ void oracle_gbm_paths(const double* contracts, int64_t B, int32_t T, int64_t P, 
     const uint64_t ordinal = (uint64_t)(ordinal0 + b);
     double* rs = rowsum ? rowsum + b * T : NULL;
     if (rs) memset(rs, 0, sizeof(double) * (size_t)T);
+    const int64_t groups = (P + GROUP - 1) / GROUP;
 #pragma omp parallel
     {
       double* local = (double*)calloc((size_t)T, sizeof(double));
+      double* z = (double*)malloc(sizeof(double) * (size_t)(T + 1) * GROUP);
 #pragma omp for schedule(static)
-      for (int64_t p = 0; p < P; ++p) {
-        xoshiro128 g;
-        path_stream(seed, ordinal, (uint64_t)p, &g);
-        double X = X0, z0 = 0, z1 = 0;
+      for (int64_t gi = 0; gi < groups; ++gi) {
+       group_normals(seed, ordinal, (uint64_t)gi, T, is_f64, z);
+       for (int j = 0; j < GROUP; ++j) {
+        const int64_t p = gi * GROUP + j;
+        if (p >= P) break;
+        double X = X0;
         for (int t = 0; t < T; ++t) {
-          if ((t & 1) == 0) normal_pair(&g, is_f64, &z0, &z1);
-          const double dW = ((t & 1) ? z1 : z0) * sqrt_dt;
+          const double dW = z[(int64_t)t * GROUP + j] * sqrt_dt;
           if (scheme == 0) {
             X *= exp(drift_log * dt + v * dW);
           } else {
@@ -290,7 +314,9 @@ void oracle_gbm_paths(const double* contracts, int64_t B, int32_t T, int64_t P, 
           }
           local[t] += stored;
         }
+       }
       }
+      free(z);
       if (rs) {
 #pragma omp critical
         for (int t = 0; t < T; ++t) rs[t] += local[t];
@@ -337,25 +363,28 @@ void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t 
     }
     const float x0 = (float)c[0];
     const uint64_t ordinal = (uint64_t)(ordinal0 + b);
-#pragma omp parallel for schedule(static)
-    for (int64_t p = 0; p < P; ++p) {
-      xoshiro128 g;
-      path_stream(seed, ordinal, (uint64_t)p, &g);
-      float x = x0, z0 = 0.0f, z1 = 0.0f;
-      for (int t = 0; t < T; ++t) {
-        if ((t & 1) == 0) {
-          double d0, d1;
-          normal_pair(&g, 0, &d0, &d1);
-          z0 = (float)d0;
-          z1 = (float)d1;
+    const int64_t groups = (P + GROUP - 1) / GROUP;
+#pragma omp parallel
+    {
+      double* z = (double*)malloc(sizeof(double) * (size_t)(T + 1) * GROUP);
+#pragma omp for schedule(static)
+      for (int64_t gi = 0; gi < groups; ++gi) {
+        group_normals(seed, ordinal, (uint64_t)gi, T, 0, z);
+        for (int j = 0; j < GROUP; ++j) {
+          const int64_t p = gi * GROUP + j;
+          if (p >= P) break;
+          float x = x0;
+          for (int t = 0; t < T; ++t) {
+            const float zt = (float)z[(int64_t)t * GROUP + j];
+            if (scheme == 0)
+              x = x * exp2_any(fmaf(cb, zt, ca));
+            else
+              x = fabsf(fmaf(x, fmaf(cb, zt, ca), x));
+            X[(int64_t)t * P + p] = x;
+          }
         }
-        const float z = (t & 1) ? z1 : z0;
-        if (scheme == 0)
-          x = x * exp2_any(fmaf(cb, z, ca));
-        else
-          x = fabsf(fmaf(x, fmaf(cb, z, ca), x));
-        X[(int64_t)t * P + p] = x;
       }
+      free(z);
     }
     if (paths) memcpy(paths + b * (int64_t)T * P, X, sizeof(float) * (size_t)T * (size_t)P);
     if (terminal) memcpy(terminal + b * P, X + (int64_t)(T - 1) * P, sizeof(float) * (size_t)P);

@@ -140,17 +140,15 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   const int64_t P = a.P;
   const bool store_all = a.store == SMC_STORE_ALL;
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
-  PathStream s[kPathsPerLane] = {PathStream(a.seed, ordinal, p0), PathStream(a.seed, ordinal, p0 + 1),
-                                 PathStream(a.seed, ordinal, p0 + 2), PathStream(a.seed, ordinal, p0 + 3)};
+  PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));  // the lane's group stream
   Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
 #pragma unroll
   for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
   for (int t = 0; t < t0; t += 2) {  // t0 is a multiple of kRowBlock (even)
 #pragma unroll
-    for (int j = 0; j < kPathsPerLane; ++j) {
-      s[j].template normal_pair<HW>(zl[j], zh[j]);
-      x[j] = step(step(x[j], zl[j]), zh[j]);
-    }
+    for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
+#pragma unroll
+    for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(step(x[j], zl[j]), zh[j]);
   }
   // wave-uniform row base (SGPR pair) + 32-bit per-lane byte offset
   const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(Real)) * threadIdx.x;
@@ -161,7 +159,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
       const int t = t0 + i;
       if ((i & 1) == 0) {
 #pragma unroll
-        for (int j = 0; j < kPathsPerLane; ++j) s[j].template normal_pair<HW>(zl[j], zh[j]);
+        for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
       }
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (i & 1) ? zh[j] : zl[j]);
@@ -369,13 +367,20 @@ __global__ __launch_bounds__(256) void normalize_kernel(const double* __restrict
 template <typename Real, bool HW>
 __global__ __launch_bounds__(256) void normals_kernel(uint64_t seed, uint64_t ordinal, int32_t rows,
                                                       int64_t cols, Real* __restrict__ out) {
-  const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (p >= cols) return;
-  PathStream s(seed, ordinal, static_cast<uint64_t>(p));
-  Real z0 = 0, z1 = 0;
+  const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;  // path group
+  if (g * kPathsPerLane >= cols) return;
+  PathStream s(seed, ordinal, static_cast<uint64_t>(g));
+  Real z0[kPathsPerLane], z1[kPathsPerLane];
   for (int t = 0; t < rows; ++t) {
-    if ((t & 1) == 0) s.template normal_pair<HW>(z0, z1);
-    out[static_cast<int64_t>(t) * cols + p] = (t & 1) ? z1 : z0;
+    if ((t & 1) == 0) {
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(z0[j], z1[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kPathsPerLane; ++j) {
+      const int64_t p = g * kPathsPerLane + j;
+      if (p < cols) out[static_cast<int64_t>(t) * cols + p] = (t & 1) ? z1[j] : z0[j];
+    }
   }
 }
 
@@ -532,7 +537,8 @@ int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t col
                     void* stream) {
   if (!out_dev) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_normals: out_dev is NULL");
   if (rows <= 0 || cols <= 0 || ordinal < 0) return fail(SMC_ERR_INVALID_SHAPE, "smc_normals: bad shape");
-  const unsigned blocks = static_cast<unsigned>((cols + 255) / 256);
+  const int64_t groups = (cols + kPathsPerLane - 1) / kPathsPerLane;
+  const unsigned blocks = static_cast<unsigned>((groups + 255) / 256);
   const bool hw = (dtype & SMC_MATH_HW) != 0;
   dtype &= 0xff;
   if (dtype == SMC_DTYPE_F32 && !hw)

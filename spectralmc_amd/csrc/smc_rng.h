@@ -3,9 +3,10 @@
 // The reference draws a fresh (T, P) normal matrix per contract from CuPy's XORWOW
 // generator (reference src/spectralmc/async_normals.py:212-216) and reads it from HBM in
 // the path kernel (gbm.py:248).  Here the normals never touch memory: each lane derives
-// its path's stream in registers.
+// the stream of its group of 4 paths in registers.
 //
-//   seed state  = Philox4x32-10( counter = (path_lo, path_hi, ordinal_lo, ordinal_hi),
+//   paths are grouped g = p / 4 (a lane's 4 paths); one stream per (contract ordinal, group):
+//   seed state  = Philox4x32-10( counter = (g_lo, g_hi, ordinal_lo, ordinal_hi),
 //                                key     = (mc_seed_lo, mc_seed_hi) )      [Salmon et al. 2011]
 //   u32 stream  = xoshiro128+ seeded with that 128-bit state            [Blackman & Vigna 2018]
 //                 (only the top 24 bits of each output are used: the "+" scrambler's weak
@@ -16,12 +17,13 @@
 //                   z0 = sqrt(-2 ln u1) cos(2 pi u2),  z1 = sqrt(-2 ln u1) sin(2 pi u2)
 //                 f32: ln / sin / cos are the portable kernels of smc_math.h, so the normals
 //                 are bit-identical to the CPU restatement.
-//   normal t of a path is z_(t mod 2) of pair t / 2.
+//   draw order: for each step pair (t, t+1), t even: for j = 0..3 (path 4g + j): one Box-Muller
+//   pair (a, b) -> normals t and t+1 of that path.  Draws of paths >= P (ragged last group) are
+//   made and discarded, so the stream position never depends on P.
 //
-// Philox runs once per path (its round keys are wave-uniform, so the key schedule lives
-// in SGPRs); each further u32 costs 8 integer VALU ops with no 32-bit multiply, which
-// keeps the RNG a minor share of the path kernel's VALU budget.  oracle/gbm_oracle.c
-// restates the same stream on the CPU.
+// Philox runs once per group (its round keys are wave-uniform, so the key schedule lives in
+// SGPRs) and is amortised over 4 paths x T steps; each further u32 costs 8 integer VALU ops
+// with no 32-bit multiply.  oracle/gbm_oracle.c restates the same stream on the CPU.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -52,9 +54,9 @@ __device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32
 struct PathStream {
   uint32_t s0, s1, s2, s3;
 
-  __device__ __forceinline__ PathStream(uint64_t mc_seed, uint64_t ordinal, uint64_t path) {
-    s0 = static_cast<uint32_t>(path);
-    s1 = static_cast<uint32_t>(path >> 32);
+  __device__ __forceinline__ PathStream(uint64_t mc_seed, uint64_t ordinal, uint64_t group) {
+    s0 = static_cast<uint32_t>(group);
+    s1 = static_cast<uint32_t>(group >> 32);
     s2 = static_cast<uint32_t>(ordinal);
     s3 = static_cast<uint32_t>(ordinal >> 32);
     philox4x32_10(s0, s1, s2, s3, static_cast<uint32_t>(mc_seed), static_cast<uint32_t>(mc_seed >> 32));

@@ -1,0 +1,49 @@
+"""Kernel-only driver for rocprofv3: launches smc_train_targets on a C2-sized batch
+`--iters` times (no CVNN), for PMC / kernel-trace collection.
+
+    rocprofv3 --pmc SQ_WAVES ... -- python tools/kprof.py --math hw --store all
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from spectralmc_amd import _lib  # noqa: E402
+from spectralmc_amd.sobol_sampler import SobolEngine  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=4096)
+    ap.add_argument("--T", type=int, default=16)
+    ap.add_argument("--N", type=int, default=256)
+    ap.add_argument("--M", type=int, default=256)
+    ap.add_argument("--math", default="hw", choices=["hw", "portable"])
+    ap.add_argument("--store", default="all", choices=["all", "terminal"])
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    lo = np.array([0.001, 0.001, 0.0, -0.2, -0.2, 0.0])
+    hi = np.array([1e4, 2e4, 10.0, 0.2, 0.2, 2.0])
+    c = lo + (hi - lo) * SobolEngine(6, 7).random(a.B)
+    dev = torch.device("cuda", 0)
+    cd = torch.from_numpy(c).to(dev)
+    P = a.N * a.M
+    store = _lib.STORE_ALL if a.store == "all" else _lib.STORE_TERMINAL
+    paths = torch.empty((a.B, a.T, P) if store == _lib.STORE_ALL else (a.B, P), dtype=torch.float32, device=dev)
+    tg = torch.empty((a.B, a.N), dtype=torch.complex64, device=dev)
+    scheme = _lib.SCHEME_LOG_EULER | (_lib.MATH_HW if a.math == "hw" else 0)
+    L = _lib.lib()
+    for _ in range(a.iters):
+        _lib.check(L.smc_train_targets(_lib.ptr(cd), a.B, a.T, a.N, a.M, 7, None, 0, scheme, 1, 0, store,
+                                       _lib.ptr(paths), a.B, None, _lib.ptr(tg), None))
+    torch.cuda.synchronize()
+    print("ok", float(tg.abs().mean()))
+
+
+if __name__ == "__main__":
+    main()
