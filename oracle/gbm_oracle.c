@@ -196,7 +196,7 @@ static void path_stream(uint64_t seed, uint64_t ordinal, uint64_t group, xoshiro
   if ((g->s[0] | g->s[1] | g->s[2] | g->s[3]) == 0u) g->s[0] = 1u;
 }
 
-/* One Box-Muller pair.  f32: 24-bit uniforms and the portable kernels (bit-identical to the
+/* One Box-Muller pair.  f32: 23-bit uniforms and the portable kernels (bit-identical to the
  * device); f64: 32-bit uniforms and libm. */
 static void normal_pair(xoshiro128* g, int is_f64, double* z0, double* z1) {
   const uint32_t a = xoshiro_next(g), b = xoshiro_next(g);
@@ -208,10 +208,11 @@ static void normal_pair(xoshiro128* g, int is_f64, double* z0, double* z1) {
     *z0 = r * cos(th);
     *z1 = r * sin(th);
   } else {
-    const float u1 = (float)((a >> 8) + 1u) * 0x1p-24f;
+    /* u1 = 2 - (1.m) with m = a >> 9: (0, 1] on the 2^-23 grid, exact; angle (b >> 9) 2^-23 rev */
+    const float u1 = 2.0f - u2f(0x3F800000u | (a >> 9));
     const float r = sqrtf(-2.0f * log_pos(u1));
     float sn, cs;
-    sincos2pi_u24(b >> 8, &sn, &cs);
+    sincos2pi_u24((b >> 9) << 1, &sn, &cs);
     *z0 = (double)(r * cs);
     *z1 = (double)(r * sn);
   }

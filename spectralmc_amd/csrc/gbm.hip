@@ -100,6 +100,11 @@ template <typename Real, bool LOG_EULER, bool HW>
 struct Stepper {
   Real a, b;
 
+  // f32 HW normals come out divided by sqrt(2 ln 2) (smc_rng.h); the factor rides on b.
+  static constexpr double zscale() {
+    return sizeof(Real) == 4 && HW ? PathStream::kNormalScale<true> : 1.0;
+  }
+
   __device__ Stepper(const Contract& c, int T) {
     const double dt = c.T / static_cast<double>(T);
     const double sq = sqrt(dt);
@@ -107,10 +112,10 @@ struct Stepper {
       const double drift = c.r - c.d - 0.5 * c.v * c.v;
       const double scale = sizeof(Real) == 4 ? kLog2e : 1.0;
       a = static_cast<Real>(drift * dt * scale);
-      b = static_cast<Real>(c.v * sq * scale);
+      b = static_cast<Real>(c.v * sq * scale * zscale());
     } else {
       a = static_cast<Real>((c.r - c.d) * dt);
-      b = static_cast<Real>(c.v * sq);
+      b = static_cast<Real>(c.v * sq * zscale());
     }
   }
 
@@ -370,6 +375,7 @@ __global__ __launch_bounds__(256) void normals_kernel(uint64_t seed, uint64_t or
   const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;  // path group
   if (g * kPathsPerLane >= cols) return;
   PathStream s(seed, ordinal, static_cast<uint64_t>(g));
+  const Real zs = sizeof(Real) == 4 ? static_cast<Real>(PathStream::kNormalScale<HW>) : Real(1);
   Real z0[kPathsPerLane], z1[kPathsPerLane];
   for (int t = 0; t < rows; ++t) {
     if ((t & 1) == 0) {
@@ -379,7 +385,7 @@ __global__ __launch_bounds__(256) void normals_kernel(uint64_t seed, uint64_t or
 #pragma unroll
     for (int j = 0; j < kPathsPerLane; ++j) {
       const int64_t p = g * kPathsPerLane + j;
-      if (p < cols) out[static_cast<int64_t>(t) * cols + p] = (t & 1) ? z1[j] : z0[j];
+      if (p < cols) out[static_cast<int64_t>(t) * cols + p] = zs * ((t & 1) ? z1[j] : z0[j]);
     }
   }
 }

@@ -9,10 +9,10 @@
 //   seed state  = Philox4x32-10( counter = (g_lo, g_hi, ordinal_lo, ordinal_hi),
 //                                key     = (mc_seed_lo, mc_seed_hi) )      [Salmon et al. 2011]
 //   u32 stream  = xoshiro128+ seeded with that 128-bit state            [Blackman & Vigna 2018]
-//                 (only the top 24 bits of each output are used: the "+" scrambler's weak
+//                 (only the top 23 bits of each output are used: the "+" scrambler's weak
 //                 low bits never reach a normal)
 //   normals     = Box-Muller on consecutive u32 pairs (a, b):
-//                   u1 = ((a >> 8) + 1) * 2^-24 in (0, 1],  j = b >> 8 (angle 2 pi j 2^-24)   (f32)
+//                   u1 = 2 - 1.m(a >> 9) in (0, 1],  angle = (b >> 9) 2^-23 revolutions       (f32)
 //                   u1 = (a + 1) * 2^-32,                   u2 = b * 2^-32                    (f64)
 //                   z0 = sqrt(-2 ln u1) cos(2 pi u2),  z1 = sqrt(-2 ln u1) sin(2 pi u2)
 //                 f32: ln / sin / cos are the portable kernels of smc_math.h, so the normals
@@ -22,8 +22,8 @@
 //   made and discarded, so the stream position never depends on P.
 //
 // Philox runs once per group (its round keys are wave-uniform, so the key schedule lives in
-// SGPRs) and is amortised over 4 paths x T steps; each further u32 costs 8 integer VALU ops
-// with no 32-bit multiply.  oracle/gbm_oracle.c restates the same stream on the CPU.
+// SGPRs) and is amortised over 4 paths x T steps; each further u32 costs 7 integer VALU ops
+// (v_bitop3_b32 xor3) with no 32-bit multiply.  oracle/gbm_oracle.c restates the same stream on the CPU.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -63,35 +63,45 @@ struct PathStream {
     s0 |= static_cast<uint32_t>((s0 | s1 | s2 | s3) == 0u);  // xoshiro forbids the zero state
   }
 
+  // xoshiro128+ 1.0 with the three xor chains merged into v_bitop3_b32 (xor3): 7 VALU ops.
   __device__ __forceinline__ uint32_t next() {
     const uint32_t result = s0 + s3;
     const uint32_t t = s1 << 9;
-    s2 ^= s0;
-    s3 ^= s1;
-    s1 ^= s2;
-    s0 ^= s3;
-    s2 ^= t;
-    s3 = __builtin_rotateleft32(s3, 11);
+    const uint32_t n1 = __builtin_amdgcn_bitop3_b32(s1, s2, s0, 0x96);  // s1 ^ (s2 ^ s0)
+    const uint32_t n0 = __builtin_amdgcn_bitop3_b32(s0, s3, s1, 0x96);  // s0 ^ (s3 ^ s1)
+    const uint32_t n2 = __builtin_amdgcn_bitop3_b32(s2, s0, t, 0x96);   // (s2 ^ s0) ^ t
+    s3 = __builtin_rotateleft32(s3 ^ s1, 11);
+    s0 = n0;
+    s1 = n1;
+    s2 = n2;
     return result;
   }
 
-  // Two N(0,1) draws, single precision.  HW = false: portable IEEE-only arithmetic
-  // (smc_math.h), bit-identical to the CPU oracle.  HW = true (SMC_MATH_HW): quarter-rate
-  // hardware transcendentals (v_log / v_sqrt / v_sin / v_cos_f32), ~1 ulp, not reproducible
-  // on a CPU.
+  // Scale of the f32 normal_pair<HW> output: HW returns z / sqrt(2 ln 2) (the constant is
+  // folded into the caller's volatility coefficient), portable returns z itself.
+  template <bool HW>
+  static constexpr double kNormalScale = HW ? 1.1774100225154747 : 1.0;  // sqrt(2 ln 2)
+
+  // Two N(0,1) draws, single precision, from 23-bit uniforms built by mantissa insertion:
+  //   u1 = 2 - 1.m(a >> 9) in (0, 1]  (exact),  angle = 1.m(b >> 9) revolutions (period 1).
+  // HW = false: portable IEEE-only arithmetic (smc_math.h), bit-identical to the CPU oracle:
+  //   z = sqrt(-2 ln u1) (cos, sin)(2 pi angle).
+  // HW = true (SMC_MATH_HW): v_log / v_sqrt / v_cos / v_sin_f32 (~1 ulp, not reproducible on
+  //   a CPU), returning sqrt(-log2 u1) (cos, sin) = z / kNormalScale<true>:
+  //   2 alignbit + 1 sub + 4 transcendentals + 2 mul per pair.
   template <bool HW>
   __device__ __forceinline__ void normal_pair(float& z0, float& z1) {
     const uint32_t a = next(), b = next();
-    const float u1 = static_cast<float>((a >> 8) + 1u) * 0x1p-24f;
+    const float u1 = 2.0f - __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, a, 9));
     if constexpr (HW) {
-      const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln2 log2 u1
-      const float u2 = static_cast<float>(b >> 8) * 0x1p-24f;
-      z0 = r * __builtin_amdgcn_cosf(u2);  // v_cos_f32 takes revolutions
-      z1 = r * __builtin_amdgcn_sinf(u2);
+      const float r = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u1));
+      const float w = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, b, 9));  // [1, 2) rev
+      z0 = r * __builtin_amdgcn_cosf(w);
+      z1 = r * __builtin_amdgcn_sinf(w);
     } else {
       const float r = __builtin_sqrtf(-2.0f * math::log_pos(u1));
       float sn, cs;
-      math::sincos2pi_u24(b >> 8, sn, cs);
+      math::sincos2pi_u24((b >> 9) << 1, sn, cs);
       z0 = r * cs;
       z1 = r * sn;
     }

@@ -214,7 +214,16 @@ def _split_inputs(inputs: Sequence[BlackScholes.Inputs], *, dtype: torch.dtype, 
 
 # ============================================================================ the step
 class _StepProgram:
-    """The per-step device program; eager or recorded once into a hipGraph and replayed."""
+    """The per-step device program, split into a Monte-Carlo part and a network part so that
+    the two can run on separate HIP streams (see TrainingSession):
+
+        mc()       Sobol draw + fused paths/targets launch into the engine buffers (+ cursor)
+        handoff()  copy the engine's CVNN input + targets into the network's own buffers
+        fwd_bwd()  CVNN forward, spectral MSE, backward into the flat [grads..., loss] buffer
+        reduce()   data-parallel mean of the flat buffer (one RCCL all-reduce)
+        update()   Adam + post-step grad norm
+
+    Each part runs eagerly or is recorded once into a hipGraph and replayed."""
 
     def __init__(self, pricer: "GbmCVNNPricer", engine: TrainingEngine, adam: optim.Optimizer,
                  params: list[nn.Parameter], dp) -> None:
@@ -234,57 +243,84 @@ class _StepProgram:
         self.loss_slot = self.flat[numel:]
         self.loss = torch.zeros((), dtype=params[0].dtype, device=dev)
         self.grad_norm = torch.zeros((), dtype=params[0].dtype, device=dev)
-        self.graphs: list[torch.cuda.CUDAGraph] = []
+        eb = engine.buffers
+        self.real_in = torch.empty_like(eb.real_in)
+        self.imag_in = eb.imag_in  # constant zeros
+        self.targets = torch.empty_like(eb.targets)
+        self.mc_graph: torch.cuda.CUDAGraph | None = None
+        self.nn_graphs: list[torch.cuda.CUDAGraph] = []
 
     # -- pieces -------------------------------------------------------------------------
-    def _forward_backward(self) -> None:
-        buf = self.engine.enqueue_step()
+    def mc(self) -> None:
+        self.engine.enqueue_step()
+
+    def handoff(self) -> None:
+        eb = self.engine.buffers
+        self.real_in.copy_(eb.real_in)
+        self.targets.copy_(eb.targets)
+
+    def fwd_bwd(self) -> None:
         self.flat.zero_()
-        pred_r, pred_i = self.pricer._cvnn(buf.real_in, buf.imag_in)
-        loss = nn.functional.mse_loss(pred_r, torch.real(buf.targets)) + nn.functional.mse_loss(
-            pred_i, torch.imag(buf.targets))
+        pred_r, pred_i = self.pricer._cvnn(self.real_in, self.imag_in)
+        loss = nn.functional.mse_loss(pred_r, torch.real(self.targets)) + nn.functional.mse_loss(
+            pred_i, torch.imag(self.targets))
         loss.backward()
         self.loss_slot.copy_(loss.detach().reshape(1))
 
-    def _update(self) -> None:
+    def update(self) -> None:
         self.adam.step()
         grads = [p.grad for p in self.params]
         self.grad_norm.copy_(torch.linalg.vector_norm(torch.stack(torch._foreach_norm(grads, 2.0)), 2.0))
         self.loss.copy_(self.loss_slot[0])
 
-    def _reduce(self) -> None:
+    def reduce(self) -> None:
         if self.dp is not None:
             self.dp.all_reduce_mean(self.flat)
 
-    def run_eager(self) -> None:
-        self._forward_backward()
-        self._reduce()
-        self._update()
+    # -- eager / graph execution ------------------------------------------------------------
+    @property
+    def captured(self) -> bool:
+        return self.mc_graph is not None
 
-    def capture(self) -> None:
-        """Record the step (two graphs around the all-reduce when data-parallel)."""
+    def capture(self, mc_stream: torch.cuda.Stream, nn_stream: torch.cuda.Stream) -> None:
+        """Record the MC part (own memory pool: it may replay concurrently with the network
+        graphs) and the network part (two graphs around the all-reduce when data-parallel)."""
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=mc_stream):
+            self.mc()
         pool = torch.cuda.graph_pool_handle()
         if self.dp is None:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                self._forward_backward()
-                self._update()
-            self.graphs = [g]
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1, pool=pool, stream=nn_stream):
+                self.fwd_bwd()
+                self.update()
+            self.nn_graphs = [g1]
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1, pool=pool):
-                self._forward_backward()
-            with torch.cuda.graph(g2, pool=pool):
-                self._update()
-            self.graphs = [g1, g2]
+            with torch.cuda.graph(g1, pool=pool, stream=nn_stream):
+                self.fwd_bwd()
+            with torch.cuda.graph(g2, pool=pool, stream=nn_stream):
+                self.update()
+            self.nn_graphs = [g1, g2]
+        self.mc_graph = g
 
-    def replay(self) -> None:
-        if len(self.graphs) == 1:
-            self.graphs[0].replay()
+    def run_mc(self) -> None:
+        if self.mc_graph is not None:
+            self.mc_graph.replay()
         else:
-            self.graphs[0].replay()
-            self._reduce()
-            self.graphs[1].replay()
+            self.mc()
+
+    def run_nn(self) -> None:
+        if not self.nn_graphs:
+            self.fwd_bwd()
+            self.reduce()
+            self.update()
+        elif len(self.nn_graphs) == 1:
+            self.nn_graphs[0].replay()
+        else:
+            self.nn_graphs[0].replay()
+            self.reduce()
+            self.nn_graphs[1].replay()
 
 
 # ============================================================================ trainer
@@ -298,6 +334,8 @@ class GbmCVNNPricer:
     #: "portable": CPU-reproducible f32 transcendentals (bit-exact vs the oracle's kernel mode);
     #: "hw": hardware transcendentals (faster, ~1 ulp, parity at the stated fp32 tolerance)
     math_mode: str = "portable"
+    #: run step s+1's Monte-Carlo part on its own stream, concurrently with step s's network part
+    overlap_mc: bool = True
 
     @staticmethod
     def create(cfg: GbmCVNNPricerConfig) -> Result["GbmCVNNPricer", GbmPricerError]:
@@ -460,8 +498,8 @@ class GbmCVNNPricer:
             return opened
         session = opened.value
         try:
-            for _ in range(config.num_batches):
-                stepped = session.step()
+            for i in range(config.num_batches):
+                stepped = session.step(prefetch_next=i + 1 < config.num_batches)
                 if isinstance(stepped, Failure):
                     return stepped
                 if logger is not None:
@@ -624,22 +662,61 @@ class TrainingSession:
         self.global_step = pricer._global_step
         self.steps = 0
         self.engine.set_position(self.sobol_skip, pricer._mc_engine.ordinal)
-        self.stream = torch.cuda.Stream(device=dev)
-        self.stream.wait_stream(torch.cuda.current_stream(dev))
+        cur = torch.cuda.current_stream(dev)
+        if pricer.overlap_mc:
+            # the network part is ~80 short launches: a high-priority queue lets its workgroups
+            # take CU slots as the long MC kernel frees them instead of queueing behind it
+            self.stream = torch.cuda.Stream(device=dev, priority=-1)
+            self.mc_stream = torch.cuda.Stream(device=dev)
+        else:
+            self.stream = torch.cuda.Stream(device=dev)
+            self.mc_stream = self.stream
+        self.stream.wait_stream(cur)
+        self.mc_stream.wait_stream(cur)
+        self._handed = torch.cuda.Event()    # MC buffers copied to the network's buffers
+        self._nn_done = torch.cuda.Event()   # network finished with its buffers
+        self._nn_started = False
+        self._mc_pending = False             # the MC part of the next step is already enqueued
+        self.mc_events: list[tuple[torch.cuda.Event, torch.cuda.Event]] | None = None
         self._closed = False
 
-    def step(self) -> Result[int, TrainerError]:
+    def step(self, prefetch_next: bool = True) -> Result[int, TrainerError]:
+        """Enqueue one training step.  With ``prefetch_next`` (and ``pricer.overlap_mc``) the MC
+        part of the following step is enqueued on the MC stream right behind this step's
+        hand-off, so it runs concurrently with this step's network part.  Bit-identical to the
+        sequential order: the MC part reads only the device cursor, the network part only its
+        own buffers."""
         if self.sobol_skip + self.global_batch > MAX_POINTS:
             return Failure(SamplerInitFailed(error=SequenceExhausted(requested_end=self.sobol_skip + self.global_batch)))
         prog = self.program
+        warm = self.pricer.warmup_steps
+        if warm > 0 and self.steps >= warm and not prog.captured:
+            if self._mc_pending:  # the pending eager MC launch must finish before capture
+                self.mc_stream.synchronize()
+            prog.capture(self.mc_stream, self.stream)
+        with torch.cuda.stream(self.mc_stream):
+            if not self._mc_pending:
+                prog.run_mc()
+            if self._nn_started:
+                self.mc_stream.wait_event(self._nn_done)
+            prog.handoff()
+            self._handed.record(self.mc_stream)
+            self._mc_pending = False
+            if prefetch_next and self.sobol_skip + 2 * self.global_batch <= MAX_POINTS:
+                if self.mc_events is not None:  # live timing of the MC part on its own stream
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(self.mc_stream)
+                    prog.run_mc()
+                    e1.record(self.mc_stream)
+                    self.mc_events.append((e0, e1))
+                else:
+                    prog.run_mc()
+                self._mc_pending = True
         with torch.cuda.stream(self.stream):
-            warm = self.pricer.warmup_steps
-            if warm > 0 and self.steps >= warm and not prog.graphs:
-                prog.capture()
-            if prog.graphs:
-                prog.replay()
-            else:
-                prog.run_eager()
+            self.stream.wait_event(self._handed)
+            prog.run_nn()
+            self._nn_done.record(self.stream)
+            self._nn_started = True
         self.steps += 1
         self.sobol_skip += self.global_batch
         self.global_step += 1
@@ -658,8 +735,10 @@ class TrainingSession:
             raise RuntimeError("session already closed")
         self._closed = True
         self.sync()
+        self.mc_stream.synchronize()
         dev = self.pricer._torch_device
         torch.cuda.current_stream(dev).wait_stream(self.stream)
+        torch.cuda.current_stream(dev).wait_stream(self.mc_stream)
         loss, gn = (float(self.program.loss), float(self.program.grad_norm)) if self.steps else (0.0, 0.0)
         for p in self.params:  # detach the flat-buffer grad views from the parameters
             p.grad = p.grad.clone()

@@ -196,3 +196,29 @@ def test_normalized_paths_hit_forwards() -> None:
     sr = expect_success(bs._simulate(c))
     means = sr.sims.double().mean(dim=1)
     torch.testing.assert_close(means, sr.forwards.double(), rtol=2e-6, atol=0)
+
+
+def test_overlapped_mc_matches_sequential() -> None:
+    """MC part of step s+1 on its own stream beside step s's network part == one stream."""
+    seq, m_s = _pricer()
+    seq.overlap_mc = False
+    ovl, m_o = _pricer()
+    assert ovl.overlap_mc
+    cfg = make_training_config(num_batches=6, batch_size=16)
+    r_s = expect_success(seq.train(cfg))
+    r_o = expect_success(ovl.train(cfg))
+    assert max_param_diff(m_s, m_o) == 0.0
+    assert r_s.final_loss == r_o.final_loss and r_s.final_grad_norm == r_o.final_grad_norm
+
+
+def test_session_step_without_prefetch_then_close() -> None:
+    """A session driven step by step (prefetch on every step, one unused) ends consistently."""
+    p, m = _pricer()
+    ref, m_r = _pricer()
+    expect_success(ref.train(make_training_config(num_batches=3, batch_size=16)))
+    sess = expect_success(p.open_session(make_training_config(num_batches=3, batch_size=16)))
+    for _ in range(3):
+        expect_success(sess.step())
+    st = sess.close()
+    assert st.global_step == 3 and st.sobol_skip == 48
+    assert max_param_diff(m, m_r) == 0.0
