@@ -32,7 +32,13 @@
 namespace smc {
 namespace {
 
-constexpr int kThreads = 512;
+#ifndef SMC_WG_THREADS
+#define SMC_WG_THREADS 512
+#endif
+#ifndef SMC_MIN_LDS
+#define SMC_MIN_LDS 0
+#endif
+constexpr int kThreads = SMC_WG_THREADS;
 constexpr int kWaves = kThreads / 64;
 constexpr int kPathsPerLane = 4;
 constexpr int kChunk = kThreads * kPathsPerLane;
@@ -398,7 +404,8 @@ size_t lds_bytes(int T, int N, bool cf) {
     const size_t cfw = static_cast<size_t>(N > kThreads ? N : kThreads) + 3 * static_cast<size_t>(N);
     if (cfw > work) work = cfw;
   }
-  return (doubles + work) * sizeof(double);
+  const size_t bytes = (doubles + work) * sizeof(double);
+  return bytes < SMC_MIN_LDS ? SMC_MIN_LDS : bytes;
 }
 
 template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>

@@ -244,26 +244,29 @@ class _StepProgram:
         self.loss = torch.zeros((), dtype=params[0].dtype, device=dev)
         self.grad_norm = torch.zeros((), dtype=params[0].dtype, device=dev)
         eb = engine.buffers
-        self.real_in = torch.empty_like(eb.real_in)
+        # two network input slots: the hand-off of step s fills slot s % 2 while the network may
+        # still be reading slot (s - 1) % 2
+        self.real_in = [torch.empty_like(eb.real_in) for _ in range(2)]
         self.imag_in = eb.imag_in  # constant zeros
-        self.targets = torch.empty_like(eb.targets)
+        self.targets = [torch.empty_like(eb.targets) for _ in range(2)]
         self.mc_graph: torch.cuda.CUDAGraph | None = None
-        self.nn_graphs: list[torch.cuda.CUDAGraph] = []
+        self.nn_graphs: list[list[torch.cuda.CUDAGraph]] = []  # per slot
 
     # -- pieces -------------------------------------------------------------------------
     def mc(self) -> None:
         self.engine.enqueue_step()
 
-    def handoff(self) -> None:
+    def handoff(self, slot: int) -> None:
         eb = self.engine.buffers
-        self.real_in.copy_(eb.real_in)
-        self.targets.copy_(eb.targets)
+        self.real_in[slot].copy_(eb.real_in)
+        self.targets[slot].copy_(eb.targets)
 
-    def fwd_bwd(self) -> None:
+    def fwd_bwd(self, slot: int) -> None:
         self.flat.zero_()
-        pred_r, pred_i = self.pricer._cvnn(self.real_in, self.imag_in)
-        loss = nn.functional.mse_loss(pred_r, torch.real(self.targets)) + nn.functional.mse_loss(
-            pred_i, torch.imag(self.targets))
+        targets = self.targets[slot]
+        pred_r, pred_i = self.pricer._cvnn(self.real_in[slot], self.imag_in)
+        loss = nn.functional.mse_loss(pred_r, torch.real(targets)) + nn.functional.mse_loss(
+            pred_i, torch.imag(targets))
         loss.backward()
         self.loss_slot.copy_(loss.detach().reshape(1))
 
@@ -289,19 +292,22 @@ class _StepProgram:
         with torch.cuda.graph(g, stream=mc_stream):
             self.mc()
         pool = torch.cuda.graph_pool_handle()
-        if self.dp is None:
+        self.nn_graphs = []
+        upd = None
+        for slot in range(2):
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1, pool=pool, stream=nn_stream):
-                self.fwd_bwd()
-                self.update()
-            self.nn_graphs = [g1]
-        else:
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1, pool=pool, stream=nn_stream):
-                self.fwd_bwd()
-            with torch.cuda.graph(g2, pool=pool, stream=nn_stream):
-                self.update()
-            self.nn_graphs = [g1, g2]
+                self.fwd_bwd(slot)
+                if self.dp is None:
+                    self.update()
+            if self.dp is None:
+                self.nn_graphs.append([g1])
+                continue
+            if upd is None:
+                upd = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(upd, pool=pool, stream=nn_stream):
+                    self.update()
+            self.nn_graphs.append([g1, upd])
         self.mc_graph = g
 
     def run_mc(self) -> None:
@@ -310,17 +316,17 @@ class _StepProgram:
         else:
             self.mc()
 
-    def run_nn(self) -> None:
+    def run_nn(self, slot: int) -> None:
         if not self.nn_graphs:
-            self.fwd_bwd()
+            self.fwd_bwd(slot)
             self.reduce()
             self.update()
-        elif len(self.nn_graphs) == 1:
-            self.nn_graphs[0].replay()
-        else:
-            self.nn_graphs[0].replay()
+            return
+        graphs = self.nn_graphs[slot]
+        graphs[0].replay()
+        if len(graphs) == 2:
             self.reduce()
-            self.nn_graphs[1].replay()
+            graphs[1].replay()
 
 
 # ============================================================================ trainer
@@ -673,9 +679,9 @@ class TrainingSession:
             self.mc_stream = self.stream
         self.stream.wait_stream(cur)
         self.mc_stream.wait_stream(cur)
-        self._handed = torch.cuda.Event()    # MC buffers copied to the network's buffers
-        self._nn_done = torch.cuda.Event()   # network finished with its buffers
-        self._nn_started = False
+        self._handed = torch.cuda.Event()    # MC buffers copied to a network input slot
+        self._nn_done = [torch.cuda.Event(), torch.cuda.Event()]  # network finished with slot i
+        self._slot_used = [False, False]
         self._mc_pending = False             # the MC part of the next step is already enqueued
         self.mc_events: list[tuple[torch.cuda.Event, torch.cuda.Event]] | None = None
         self._closed = False
@@ -694,12 +700,13 @@ class TrainingSession:
             if self._mc_pending:  # the pending eager MC launch must finish before capture
                 self.mc_stream.synchronize()
             prog.capture(self.mc_stream, self.stream)
+        slot = self.steps % 2
         with torch.cuda.stream(self.mc_stream):
             if not self._mc_pending:
                 prog.run_mc()
-            if self._nn_started:
-                self.mc_stream.wait_event(self._nn_done)
-            prog.handoff()
+            if self._slot_used[slot]:  # the network step two back must be done with this slot
+                self.mc_stream.wait_event(self._nn_done[slot])
+            prog.handoff(slot)
             self._handed.record(self.mc_stream)
             self._mc_pending = False
             if prefetch_next and self.sobol_skip + 2 * self.global_batch <= MAX_POINTS:
@@ -714,9 +721,9 @@ class TrainingSession:
                 self._mc_pending = True
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(self._handed)
-            prog.run_nn()
-            self._nn_done.record(self.stream)
-            self._nn_started = True
+            prog.run_nn(slot)
+            self._nn_done[slot].record(self.stream)
+            self._slot_used[slot] = True
         self.steps += 1
         self.sobol_skip += self.global_batch
         self.global_step += 1

@@ -38,11 +38,20 @@ def main() -> None:
     tg = torch.empty((a.B, a.N), dtype=torch.complex64, device=dev)
     scheme = _lib.SCHEME_LOG_EULER | (_lib.MATH_HW if a.math == "hw" else 0)
     L = _lib.lib()
-    for _ in range(a.iters):
+    def launch():
         _lib.check(L.smc_train_targets(_lib.ptr(cd), a.B, a.T, a.N, a.M, 7, None, 0, scheme, 1, 0, store,
                                        _lib.ptr(paths), a.B, None, _lib.ptr(tg), None))
+
+    launch()
     torch.cuda.synchronize()
-    print("ok", float(tg.abs().mean()))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"{os.environ.get('SMC_LIB_PATH', 'default')} {a.math} {a.store}: {e0.elapsed_time(e1) / a.iters:.3f} ms/launch",
+          "checksum", float(tg.abs().double().mean()))
 
 
 if __name__ == "__main__":
