@@ -80,3 +80,12 @@ def oracle():
 
     _oracle.build()
     return _oracle
+
+
+@pytest.fixture
+def async_store(tmp_path):
+    """Offline replacement of the reference's MinIO-backed store fixture (reference
+    tests/conftest.py:174-229): a fresh local-filesystem store per test."""
+    from spectralmc_amd.storage import AsyncBlockchainModelStore
+
+    return AsyncBlockchainModelStore(tmp_path / "store")
