@@ -44,7 +44,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
-    ap.add_argument("--math", default="portable", choices=["portable", "hw"])
+    ap.add_argument("--math", default="hw", choices=["portable", "hw"])
     ap.add_argument("--kernel-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU-baseline sample")

@@ -337,9 +337,10 @@ class GbmCVNNPricer:
     warmup_steps: int = 2
     #: materialise the full [B][T][P] path matrix each step (the reference kernel's output contract)
     store_paths: bool = True
-    #: "portable": CPU-reproducible f32 transcendentals (bit-exact vs the oracle's kernel mode);
-    #: "hw": hardware transcendentals (faster, ~1 ulp, parity at the stated fp32 tolerance)
-    math_mode: str = "portable"
+    #: "hw": hardware f32 transcendentals in the path kernel (throughput mode; parity with the
+    #: CPU path at the stated fp32 tolerance); "portable": IEEE-only polynomial transcendentals,
+    #: bit-identical to the oracle's kernel mode (CPU-reproducible paths and targets)
+    math_mode: str = "hw"
     #: run step s+1's Monte-Carlo part on its own stream, concurrently with step s's network part
     overlap_mc: bool = True
 

@@ -70,10 +70,12 @@ def test_one_step_matches_oracle(oracle, dtype) -> None:
         assert rel < 1e-4, (name, rel)
 
 
-def test_hw_math_trainer_loss_within_tolerance(oracle) -> None:
+def test_portable_math_trainer_loss_within_tolerance(oracle) -> None:
+    """The CPU-reproducible math mode through the whole trainer (default is "hw")."""
     B = 32
     pricer, model = _pricer(warmup=0)
-    pricer.math_mode = "hw"
+    assert pricer.math_mode == "hw"
+    pricer.math_mode = "portable"
     res = expect_success(pricer.train(make_training_config(num_batches=1, batch_size=B, learning_rate=1e-2)))
     lo, hi = make_domain_bounds().arrays()
     contracts = oracle.sobol_contracts(7, 0, B, lo, hi)

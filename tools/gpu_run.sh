@@ -30,12 +30,13 @@ for step in "$@"; do
     gputests) run gputests 1200 python -m pytest tests -m gpu -q -rf ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py ;;
-    bench_quick) run bench_quick 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    bench_quick) run bench_quick 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --math portable ;;
     bench_hw) run bench_hw 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --math hw ;;
     bench_hw_terminal) run bench_hw_terminal 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --store terminal --math hw ;;
-    bench_terminal) run bench_terminal 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --store terminal ;;
+    bench_terminal) run bench_terminal 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --store terminal --math portable ;;
     bench_c1) run bench_c1 600 python bench.py --config c1 --steps 50 --warmup 5 --no-cpu-baseline ;;
     prof)    cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT" ;;
+    prof_default) cd /tmp && run prof_default 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_default" -o run --output-format csv -- python "$ROOT/bench.py"; cd "$ROOT" ;;
     prof_hw) cd /tmp && run prof_hw 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_hw" -o run --output-format csv -- python "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --math hw; cd "$ROOT" ;;
     pmc_hw_all)  cd /tmp && run pmc_hw_all 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_hw_all" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all; cd "$ROOT" ;;
     pmc_hw_term) cd /tmp && run pmc_hw_term 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_hw_term" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store terminal; cd "$ROOT" ;;
