@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 1
+#define SMC_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -125,6 +125,57 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
  * draws for path p, step t, laid out [t][p]). */
 int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t cols,
                     int32_t dtype, void* out_dev, void* stream);
+
+/* ---- complex-valued MLP training step --------------------------------------
+ * Replaces the network half of _torch_step (src/spectralmc/gbm_trainer.py:819-835) for
+ * ComplexSequential chains of ComplexLinear (cvnn.py:65-143) with optional modReLU
+ * (cvnn.py:168-210) or zReLU (cvnn.py:149-162) activations.  Parameters, gradients and Adam
+ * moments are flat buffers in the model's parameter order; a layer names its tensors by
+ * element offset into them (-1 = absent). */
+#define SMC_CVNN_MAX_LAYERS 8
+#define SMC_ACT_NONE     0
+#define SMC_ACT_MODRELU  1
+#define SMC_ACT_ZRELU    2
+
+typedef struct smc_cvnn_layer {
+  int32_t in_features, out_features;
+  int32_t activation;            /* SMC_ACT_* applied after this layer's affine map */
+  int32_t reserved;
+  int64_t w_re, w_im;            /* [out][in] real_weight / imag_weight offsets        */
+  int64_t b_re, b_im;            /* [out] real_bias / imag_bias offsets or -1          */
+  int64_t act_bias;              /* [out] modReLU bias offset or -1                    */
+} smc_cvnn_layer;
+
+/* torch.optim.Adam (defaults of gbm_trainer.py:1513) on flat buffers; `step` is torch's
+ * capturable f32 step counter, read before and incremented after the update. */
+typedef struct smc_adam_args {
+  void* params;
+  void* exp_avg;
+  void* exp_avg_sq;
+  float* step;
+  double lr, beta1, beta2, eps, weight_decay;
+  double* norm_partials;         /* [smc_adam_norm_partials(n_params)] scratch          */
+  void* grad_norm;               /* scalar out: ||grad||_2 (gbm_trainer.py:834)         */
+  void* loss;                    /* scalar out: grads[n_params] (the loss slot)         */
+} smc_adam_args;
+
+/* Number of per-workgroup gradient partials ([blocks][n_params + 1]) for this batch. */
+int32_t smc_cvnn_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t dtype, int64_t batch,
+                      int64_t* partial_blocks);
+/* Forward, loss = mse(Re) + mse(Im), backward: partials[g] = the gradients and loss share
+ * of workgroup g's rows.  input_im may be NULL (zeros); targets [batch][N] complex. */
+int32_t smc_cvnn_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers, int32_t dtype,
+                                  const void* params, int64_t n_params, const void* input_re,
+                                  const void* input_im, const void* targets, int64_t batch,
+                                  void* partials, int64_t partial_blocks, void* stream);
+/* grads[0..n_params] = fixed-order sum of the partials (last entry: loss).  With adam != NULL
+ * the Adam update, grad norm, loss copy and step increment follow in the same call. */
+int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t partial_blocks,
+                              int64_t n_params, void* grads, const smc_adam_args* adam, void* stream);
+/* Adam update from an already reduced (e.g. all-reduced) grads[0..n_params]. */
+int32_t smc_adam_step(int32_t dtype, int64_t n_params, const void* grads, const smc_adam_args* adam,
+                      void* stream);
+int64_t smc_adam_norm_partials(int64_t n_params);
 
 #ifdef __cplusplus
 }

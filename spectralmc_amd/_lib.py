@@ -34,7 +34,7 @@ STORE_TERMINAL = 1
 MATH_HW = 0x100
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 
@@ -57,7 +57,32 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_train_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_u64, _c_vp, _c_i64, _c_i32,
                                    _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp]),
     "smc_normals": (_c_i32, [_c_u64, _c_i64, _c_i32, _c_i64, _c_i32, _c_vp, _c_vp]),
+    "smc_cvnn_plan": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64)]),
+    "smc_cvnn_forward_backward": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64,
+                                           _c_vp, _c_i64, _c_vp]),
+    "smc_cvnn_reduce_grads": (_c_i32, [_c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
+    "smc_adam_step": (_c_i32, [_c_i32, _c_i64, _c_vp, _c_vp, _c_vp]),
+    "smc_adam_norm_partials": (_c_i64, [_c_i64]),
 }
+
+CVNN_MAX_LAYERS = 8
+ACT_NONE, ACT_MODRELU, ACT_ZRELU = 0, 1, 2
+
+
+class CvnnLayer(ctypes.Structure):
+    """smc_cvnn_layer (include/spectralmc_hip.h)."""
+
+    _fields_ = [("in_features", _c_i32), ("out_features", _c_i32), ("activation", _c_i32), ("reserved", _c_i32),
+                ("w_re", _c_i64), ("w_im", _c_i64), ("b_re", _c_i64), ("b_im", _c_i64), ("act_bias", _c_i64)]
+
+
+class AdamArgs(ctypes.Structure):
+    """smc_adam_args (include/spectralmc_hip.h)."""
+
+    _fields_ = [("params", _c_vp), ("exp_avg", _c_vp), ("exp_avg_sq", _c_vp), ("step", _c_vp),
+                ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("weight_decay", ctypes.c_double), ("norm_partials", _c_vp),
+                ("grad_norm", _c_vp), ("loss", _c_vp)]
 
 
 class HipExtensionMissing(ImportError):

@@ -1,0 +1,553 @@
+// Complex-valued MLP training step for gfx950: forward, spectral MSE, backward and Adam in
+// three launches (torch-ROCm issues ~200 small kernels for the same step).
+//
+// Reference behaviour restated (Tuee22/SpectralMC, src/spectralmc/):
+//   cvnn.py:65-143   ComplexLinear  u = A x - B y + b_re,  v = B x + A y + b_im
+//   cvnn.py:149-162  zReLU          keep z where Re z >= 0 and Im z >= 0
+//   cvnn.py:168-210  modReLU        m = sqrt(u^2 + v^2 + 1e-9),  z * relu(m + c) / m
+//   gbm_trainer.py:819-835  loss = mse(pred_re, Re y) + mse(pred_im, Im y); backward;
+//                    Adam.step (torch defaults); grad_norm = ||g||_2 after the step
+//
+// Design:
+//   * forward_backward_kernel: a workgroup takes blocks of R rows, keeps every layer's
+//     pre-activation and output for those rows in LDS, back-propagates through them and adds
+//     the rows' weight gradients into its own slot of a partial buffer [G][n_params + 1]
+//     (the last entry is the loss).  Fixed row-block assignment and fixed loop orders make
+//     the result bit-reproducible; no float atomics.
+//   * reduce_kernel: one thread per parameter sums the G partials in order (f64) -> flat
+//     gradient buffer [n_params + 1]; with SMC Adam arguments it also applies the Adam update
+//     (fused, single process) and per-block partial sums of g^2.
+//   * adam_kernel: the same update from an already reduced (all-reduced) gradient buffer.
+//   * finalize_kernel: grad norm from the block partials (fixed order), loss, step += 1.
+// Weights stay in HBM/L2 (tens of KB for the benchmark network); parameters, gradients and
+// Adam moments are single flat buffers whose layout is the model's parameter order.
+
+#include <cmath>
+
+#include "smc_internal.h"
+
+namespace smc {
+namespace {
+
+constexpr int kNetThreads = 256;
+constexpr int kMaxLayers = SMC_CVNN_MAX_LAYERS;
+constexpr int kMaxBlocks = 256;       // partial slots (workgroups) of forward_backward_kernel
+constexpr size_t kNetLdsBudget = 64 * 1024;
+
+struct NetArgs {
+  int32_t n_layers;
+  smc_cvnn_layer layer[kMaxLayers];
+  int32_t rows;             // R rows per row block
+  int64_t batch;
+  int64_t n_params;
+  int32_t out_features;     // N of the last layer
+  const void* params;
+  const void* input_re;     // [B][n_in0]
+  const void* input_im;     // [B][n_in0] or NULL (zeros)
+  const void* targets;      // [B][N] complex (interleaved re, im)
+  void* partials;           // [G][n_params + 1]
+};
+
+// LDS layout per row block (element offsets, multiplied by rows):
+//   in0_re, in0_im          n_in0 each
+//   per layer l: u, v       n_out each   (pre-activation)
+//                ar, ai     n_out each   (activation output; only if activation != none)
+//   g0_re, g0_im, g1_re, g1_im   max width each (gradient ping-pong)
+struct LdsPlan {
+  int64_t in_re, in_im;
+  int64_t u[kMaxLayers], v[kMaxLayers], ar[kMaxLayers], ai[kMaxLayers];
+  int64_t g[4];
+  int64_t per_row;
+};
+
+__host__ __device__ inline LdsPlan plan_lds(const smc_cvnn_layer* layer, int n_layers) {
+  LdsPlan p{};
+  int64_t off = 0;
+  const int n0 = layer[0].in_features;
+  p.in_re = off;
+  off += n0;
+  p.in_im = off;
+  off += n0;
+  int wmax = n0;
+  for (int l = 0; l < n_layers; ++l) {
+    const int n = layer[l].out_features;
+    wmax = n > wmax ? n : wmax;
+    p.u[l] = off;
+    off += n;
+    p.v[l] = off;
+    off += n;
+    if (layer[l].activation != SMC_ACT_NONE) {
+      p.ar[l] = off;
+      off += n;
+      p.ai[l] = off;
+      off += n;
+    } else {
+      p.ar[l] = p.u[l];
+      p.ai[l] = p.v[l];
+    }
+  }
+  for (int k = 0; k < 4; ++k) {
+    p.g[k] = off;
+    off += wmax;
+  }
+  p.per_row = off;
+  return p;
+}
+
+template <typename Real>
+__device__ __forceinline__ Real block_sum(Real x, double* red_raw) {
+  Real* red = reinterpret_cast<Real*>(red_raw);
+  // fixed-order block reduction: wave butterfly, then waves 0..3 in order
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wave] = x;
+  __syncthreads();
+  Real t = 0;
+  for (int w = 0; w < kNetThreads / 64; ++w) t += red[w];
+  return t;
+}
+
+template <typename Real>
+__global__ __launch_bounds__(kNetThreads) void forward_backward_kernel(NetArgs a) {
+  extern __shared__ double net_lds_raw[];
+  Real* lds = reinterpret_cast<Real*>(net_lds_raw);
+  const int tid = threadIdx.x;
+  const int L = a.n_layers;
+  const int R = a.rows;
+  const LdsPlan pl = plan_lds(a.layer, L);
+  __shared__ double red[kNetThreads / 64];
+  const Real* P = static_cast<const Real*>(a.params);
+  Real* part = static_cast<Real*>(a.partials) + static_cast<int64_t>(blockIdx.x) * (a.n_params + 1);
+  const Real* in_re = static_cast<const Real*>(a.input_re);
+  const Real* in_im = static_cast<const Real*>(a.input_im);
+  const Real* tgt = static_cast<const Real*>(a.targets);
+  const int n0 = a.layer[0].in_features;
+  const int N = a.out_features;
+  const Real scale = Real(2) / static_cast<Real>(static_cast<double>(a.batch) * N);  // d mean / d x
+  double loss_acc = 0.0;
+  const int64_t n_blocks = (a.batch + R - 1) / R;
+  bool first = true;
+
+  for (int64_t rb = blockIdx.x; rb < n_blocks; rb += gridDim.x, first = false) {
+    const int64_t r0 = rb * R;
+    const int rows = static_cast<int>(a.batch - r0 < R ? a.batch - r0 : R);
+    // ---- load inputs
+    for (int i = tid; i < rows * n0; i += kNetThreads) {
+      lds[pl.in_re * R + i] = in_re[r0 * n0 + i];
+      lds[pl.in_im * R + i] = in_im ? in_im[r0 * n0 + i] : Real(0);
+    }
+    __syncthreads();
+    // ---- forward
+    for (int l = 0; l < L; ++l) {
+      const smc_cvnn_layer& ly = a.layer[l];
+      const int ni = ly.in_features, no = ly.out_features;
+      const Real* x = lds + (l == 0 ? pl.in_re : pl.ar[l - 1]) * R;
+      const Real* y = lds + (l == 0 ? pl.in_im : pl.ai[l - 1]) * R;
+      Real* u = lds + pl.u[l] * R;
+      Real* v = lds + pl.v[l] * R;
+      const Real* A = P + ly.w_re;
+      const Real* Bw = P + ly.w_im;
+      for (int idx = tid; idx < rows * no; idx += kNetThreads) {
+        const int r = idx / no, j = idx - r * no;
+        Real su = ly.b_re >= 0 ? P[ly.b_re + j] : Real(0);
+        Real sv = ly.b_im >= 0 ? P[ly.b_im + j] : Real(0);
+        const Real* xr = x + r * ni;
+        const Real* yr = y + r * ni;
+        const Real* Aj = A + static_cast<int64_t>(j) * ni;
+        const Real* Bj = Bw + static_cast<int64_t>(j) * ni;
+        for (int k = 0; k < ni; ++k) {
+          su += Aj[k] * xr[k] - Bj[k] * yr[k];
+          sv += Bj[k] * xr[k] + Aj[k] * yr[k];
+        }
+        u[idx] = su;
+        v[idx] = sv;
+        if (ly.activation == SMC_ACT_MODRELU) {
+          const Real m = sqrt(su * su + sv * sv + Real(1e-9));
+          const Real t = m + P[ly.act_bias + j];
+          const Real g = (t > Real(0) ? t : Real(0)) / m;
+          lds[pl.ar[l] * R + idx] = g * su;
+          lds[pl.ai[l] * R + idx] = g * sv;
+        } else if (ly.activation == SMC_ACT_ZRELU) {
+          const bool keep = su >= Real(0) && sv >= Real(0);
+          lds[pl.ar[l] * R + idx] = keep ? su : Real(0);
+          lds[pl.ai[l] * R + idx] = keep ? sv : Real(0);
+        }
+      }
+      __syncthreads();
+    }
+    // ---- loss and d loss / d prediction
+    {
+      const Real* pr = lds + pl.ar[L - 1] * R;
+      const Real* pi = lds + pl.ai[L - 1] * R;
+      Real* gr = lds + pl.g[0] * R;
+      Real* gi = lds + pl.g[1] * R;
+      double part_loss = 0.0;
+      for (int idx = tid; idx < rows * N; idx += kNetThreads) {
+        const int r = idx / N, j = idx - r * N;
+        const int64_t t = ((r0 + r) * N + j) * 2;
+        const Real dr = pr[idx] - tgt[t];
+        const Real di = pi[idx] - tgt[t + 1];
+        part_loss += static_cast<double>(dr * dr) + static_cast<double>(di * di);
+        gr[idx] = scale * dr;
+        gi[idx] = scale * di;
+      }
+      loss_acc += block_sum<double>(part_loss, red);
+    }
+    __syncthreads();
+    // ---- backward
+    int cur = 0;  // g[cur], g[cur+1]: gradient w.r.t. the current layer's output (re, im)
+    for (int l = L - 1; l >= 0; --l) {
+      const smc_cvnn_layer& ly = a.layer[l];
+      const int ni = ly.in_features, no = ly.out_features;
+      Real* go_r = lds + pl.g[cur] * R;
+      Real* go_i = lds + pl.g[cur + 1] * R;
+      const Real* u = lds + pl.u[l] * R;
+      const Real* v = lds + pl.v[l] * R;
+      if (ly.activation == SMC_ACT_MODRELU) {
+        // d/dc first (needs the output gradient), then the output gradient -> (gu, gv) in place
+        for (int j = tid; j < no; j += kNetThreads) {
+          const Real c = P[ly.act_bias + j];
+          Real s = 0;
+          for (int r = 0; r < rows; ++r) {
+            const int idx = r * no + j;
+            const Real m = sqrt(u[idx] * u[idx] + v[idx] * v[idx] + Real(1e-9));
+            if (m + c > Real(0)) s += (go_r[idx] * u[idx] + go_i[idx] * v[idx]) / m;
+          }
+          Real* dst = static_cast<Real*>(part) + ly.act_bias + j;
+          *dst = first ? s : *dst + s;
+        }
+        __syncthreads();
+        for (int idx = tid; idx < rows * no; idx += kNetThreads) {
+          const int j = idx % no;
+          const Real c = P[ly.act_bias + j];
+          const Real uu = u[idx], vv = v[idx];
+          const Real m = sqrt(uu * uu + vv * vv + Real(1e-9));
+          if (m + c > Real(0)) {
+            const Real g = (m + c) / m;
+            const Real k = -(go_r[idx] * uu + go_i[idx] * vv) * c / (m * m * m);
+            go_r[idx] = go_r[idx] * g + k * uu;
+            go_i[idx] = go_i[idx] * g + k * vv;
+          } else {
+            go_r[idx] = Real(0);
+            go_i[idx] = Real(0);
+          }
+        }
+        __syncthreads();
+      } else if (ly.activation == SMC_ACT_ZRELU) {
+        for (int idx = tid; idx < rows * no; idx += kNetThreads) {
+          if (!(u[idx] >= Real(0) && v[idx] >= Real(0))) {
+            go_r[idx] = Real(0);
+            go_i[idx] = Real(0);
+          }
+        }
+        __syncthreads();
+      }
+      const Real* x = lds + (l == 0 ? pl.in_re : pl.ar[l - 1]) * R;
+      const Real* y = lds + (l == 0 ? pl.in_im : pl.ai[l - 1]) * R;
+      // weight gradients: dA = gu x^T + gv y^T,  dB = gv x^T - gu y^T  (summed over the rows)
+      for (int idx = tid; idx < no * ni; idx += kNetThreads) {
+        const int j = idx / ni, k = idx - j * ni;
+        Real da = 0, db = 0;
+        for (int r = 0; r < rows; ++r) {
+          const Real gu = go_r[r * no + j], gv = go_i[r * no + j];
+          const Real xk = x[r * ni + k], yk = y[r * ni + k];
+          da += gu * xk + gv * yk;
+          db += gv * xk - gu * yk;
+        }
+        Real* pa = part + ly.w_re + idx;
+        Real* pb = part + ly.w_im + idx;
+        *pa = first ? da : *pa + da;
+        *pb = first ? db : *pb + db;
+      }
+      for (int j = tid; j < no; j += kNetThreads) {
+        Real sr = 0, si = 0;
+        for (int r = 0; r < rows; ++r) {
+          sr += go_r[r * no + j];
+          si += go_i[r * no + j];
+        }
+        if (ly.b_re >= 0) part[ly.b_re + j] = first ? sr : part[ly.b_re + j] + sr;
+        if (ly.b_im >= 0) part[ly.b_im + j] = first ? si : part[ly.b_im + j] + si;
+      }
+      if (l > 0) {
+        // input gradients: gx = A^T gu + B^T gv,  gy = A^T gv - B^T gu
+        Real* gx = lds + pl.g[2 - cur] * R;
+        Real* gy = lds + pl.g[3 - cur] * R;
+        const Real* A = P + ly.w_re;
+        const Real* Bw = P + ly.w_im;
+        for (int idx = tid; idx < rows * ni; idx += kNetThreads) {
+          const int r = idx / ni, k = idx - r * ni;
+          Real sx = 0, sy = 0;
+          for (int j = 0; j < no; ++j) {
+            const Real a_ = A[static_cast<int64_t>(j) * ni + k], b_ = Bw[static_cast<int64_t>(j) * ni + k];
+            const Real gu = go_r[r * no + j], gv = go_i[r * no + j];
+            sx += a_ * gu + b_ * gv;
+            sy += a_ * gv - b_ * gu;
+          }
+          gx[idx] = sx;
+          gy[idx] = sy;
+        }
+        cur = 2 - cur;
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) part[a.n_params] = static_cast<Real>(loss_acc / (static_cast<double>(a.batch) * N));
+}
+
+struct AdamArgs {
+  void* params;
+  void* exp_avg;
+  void* exp_avg_sq;
+  const float* step;  // torch's capturable step counter before this update
+  double lr, beta1, beta2, eps, weight_decay;
+  double* norm_partials;  // [gridDim] sums of g^2
+};
+
+template <typename Real>
+__device__ __forceinline__ void adam_update(const AdamArgs& ad, int64_t p, Real g) {
+  Real* prm = static_cast<Real*>(ad.params);
+  Real* m = static_cast<Real*>(ad.exp_avg);
+  Real* v = static_cast<Real*>(ad.exp_avg_sq);
+  const Real t = static_cast<Real>(*ad.step) + Real(1);
+  const Real b1 = static_cast<Real>(ad.beta1), b2 = static_cast<Real>(ad.beta2);
+  if (ad.weight_decay != 0.0) g += static_cast<Real>(ad.weight_decay) * prm[p];
+  const Real mm = m[p] + (Real(1) - b1) * (g - m[p]);
+  const Real vv = v[p] * b2 + (Real(1) - b2) * g * g;
+  m[p] = mm;
+  v[p] = vv;
+  const Real bc1 = Real(1) - pow(b1, t);
+  const Real bc2 = Real(1) - pow(b2, t);
+  const Real step_size = static_cast<Real>(ad.lr) / bc1;
+  const Real denom = sqrt(vv) / sqrt(bc2) + static_cast<Real>(ad.eps);
+  prm[p] = prm[p] - step_size * (mm / denom);
+}
+
+template <typename Real, bool ADAM>
+__global__ __launch_bounds__(kNetThreads) void reduce_kernel(const Real* __restrict__ partials, int64_t blocks,
+                                                             int64_t n_params, Real* __restrict__ grads,
+                                                             AdamArgs ad) {
+  __shared__ double red[kNetThreads / 64];
+  const int64_t p = static_cast<int64_t>(blockIdx.x) * kNetThreads + threadIdx.x;
+  double sq = 0.0;
+  if (p <= n_params) {
+    double s = 0.0;
+    for (int64_t g = 0; g < blocks; ++g) s += static_cast<double>(partials[g * (n_params + 1) + p]);
+    const Real gr = static_cast<Real>(s);
+    grads[p] = gr;
+    if (ADAM && p < n_params) {
+      sq = static_cast<double>(gr) * static_cast<double>(gr);
+      adam_update<Real>(ad, p, gr);
+    }
+  }
+  if (ADAM) {
+    const double t = block_sum<double>(sq, red);
+    if (threadIdx.x == 0) ad.norm_partials[blockIdx.x] = t;
+  }
+}
+
+template <typename Real>
+__global__ __launch_bounds__(kNetThreads) void adam_kernel(const Real* __restrict__ grads, int64_t n_params,
+                                                           AdamArgs ad) {
+  __shared__ double red[kNetThreads / 64];
+  const int64_t p = static_cast<int64_t>(blockIdx.x) * kNetThreads + threadIdx.x;
+  double sq = 0.0;
+  if (p < n_params) {
+    const Real g = grads[p];
+    sq = static_cast<double>(g) * static_cast<double>(g);
+    adam_update<Real>(ad, p, g);
+  }
+  const double t = block_sum<double>(sq, red);
+  if (threadIdx.x == 0) ad.norm_partials[blockIdx.x] = t;
+}
+
+template <typename Real>
+__global__ __launch_bounds__(kNetThreads) void finalize_kernel(const double* __restrict__ norm_partials,
+                                                               int64_t n_partials, const Real* __restrict__ grads,
+                                                               int64_t n_params, float* step, Real* grad_norm,
+                                                               Real* loss) {
+  __shared__ double red[kNetThreads / 64];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n_partials; i += kNetThreads) s += norm_partials[i];
+  const double t = block_sum<double>(s, red);
+  if (threadIdx.x == 0) {
+    *grad_norm = static_cast<Real>(sqrt(t));
+    *loss = grads[n_params];
+    *step = *step + 1.0f;
+  }
+}
+
+bool layers_valid(const smc_cvnn_layer* layers, int32_t n_layers, int64_t n_params) {
+  if (!layers || n_layers <= 0 || n_layers > kMaxLayers) return false;
+  for (int l = 0; l < n_layers; ++l) {
+    const smc_cvnn_layer& ly = layers[l];
+    if (ly.in_features <= 0 || ly.out_features <= 0) return false;
+    if (l > 0 && ly.in_features != layers[l - 1].out_features) return false;
+    if (ly.activation < SMC_ACT_NONE || ly.activation > SMC_ACT_ZRELU) return false;
+    const int64_t w = static_cast<int64_t>(ly.in_features) * ly.out_features;
+    if (ly.w_re < 0 || ly.w_im < 0 || ly.w_re + w > n_params || ly.w_im + w > n_params) return false;
+    for (int64_t o : {ly.b_re, ly.b_im})
+      if (o >= 0 && o + ly.out_features > n_params) return false;
+    if (ly.activation == SMC_ACT_MODRELU && (ly.act_bias < 0 || ly.act_bias + ly.out_features > n_params))
+      return false;
+  }
+  return true;
+}
+
+int32_t plan_rows(const smc_cvnn_layer* layers, int32_t n_layers, int32_t dtype, int64_t batch, int32_t* rows,
+                  int64_t* blocks, size_t* lds) {
+  const LdsPlan pl = plan_lds(layers, n_layers);
+  const size_t elem = dtype == SMC_DTYPE_F64 ? 8 : 4;
+  int64_t r = static_cast<int64_t>(kNetLdsBudget / (static_cast<size_t>(pl.per_row) * elem));
+  if (r < 1) return fail(SMC_ERR_INVALID_SHAPE, "cvnn: layer widths exceed the LDS budget");
+  if (r > 16) r = 16;
+  const int64_t n_blocks = (batch + r - 1) / r;
+  *rows = static_cast<int32_t>(r);
+  *blocks = n_blocks < kMaxBlocks ? n_blocks : kMaxBlocks;
+  *lds = static_cast<size_t>(pl.per_row * r) * elem;
+  return SMC_OK;
+}
+
+}  // namespace
+}  // namespace smc
+
+using namespace smc;
+
+#pragma GCC visibility push(default)
+extern "C" {
+
+int32_t smc_cvnn_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t dtype, int64_t batch,
+                      int64_t* partial_blocks) {
+  if (!partial_blocks || batch <= 0 || (dtype != SMC_DTYPE_F32 && dtype != SMC_DTYPE_F64))
+    return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_plan: bad argument");
+  if (!layers || n_layers <= 0 || n_layers > kMaxLayers)
+    return fail(SMC_ERR_INVALID_SHAPE, "smc_cvnn_plan: 1..SMC_CVNN_MAX_LAYERS layers");
+  int32_t rows;
+  size_t lds;
+  return plan_rows(layers, n_layers, dtype, batch, &rows, partial_blocks, &lds);
+}
+
+int32_t smc_cvnn_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers, int32_t dtype, const void* params,
+                                  int64_t n_params, const void* input_re, const void* input_im,
+                                  const void* targets, int64_t batch, void* partials, int64_t partial_blocks,
+                                  void* stream) {
+  if (!params || !input_re || !targets || !partials || batch <= 0 ||
+      (dtype != SMC_DTYPE_F32 && dtype != SMC_DTYPE_F64))
+    return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_forward_backward: bad argument");
+  if (!layers_valid(layers, n_layers, n_params))
+    return fail(SMC_ERR_INVALID_SHAPE, "smc_cvnn_forward_backward: inconsistent layer table");
+  int32_t rows;
+  int64_t blocks;
+  size_t lds;
+  const int32_t rc = plan_rows(layers, n_layers, dtype, batch, &rows, &blocks, &lds);
+  if (rc != SMC_OK) return rc;
+  if (partial_blocks != blocks) return fail(SMC_ERR_INVALID_SHAPE, "smc_cvnn_forward_backward: partial_blocks != plan");
+  NetArgs a{};
+  a.n_layers = n_layers;
+  for (int l = 0; l < n_layers; ++l) a.layer[l] = layers[l];
+  a.rows = rows;
+  a.batch = batch;
+  a.n_params = n_params;
+  a.out_features = layers[n_layers - 1].out_features;
+  a.params = params;
+  a.input_re = input_re;
+  a.input_im = input_im;
+  a.targets = targets;
+  a.partials = partials;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  if (dtype == SMC_DTYPE_F32)
+    hipLaunchKernelGGL(forward_backward_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(kNetThreads), lds, s, a);
+  else
+    hipLaunchKernelGGL(forward_backward_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(kNetThreads), lds, s, a);
+  return check_launch("cvnn forward_backward_kernel");
+}
+
+static AdamArgs to_adam(const smc_adam_args* ad) {
+  AdamArgs a{};
+  a.params = ad->params;
+  a.exp_avg = ad->exp_avg;
+  a.exp_avg_sq = ad->exp_avg_sq;
+  a.step = ad->step;
+  a.lr = ad->lr;
+  a.beta1 = ad->beta1;
+  a.beta2 = ad->beta2;
+  a.eps = ad->eps;
+  a.weight_decay = ad->weight_decay;
+  a.norm_partials = ad->norm_partials;
+  return a;
+}
+
+static bool adam_valid(const smc_adam_args* ad) {
+  return ad->params && ad->exp_avg && ad->exp_avg_sq && ad->step && ad->norm_partials && ad->grad_norm &&
+         ad->loss && ad->lr > 0.0 && ad->beta1 >= 0.0 && ad->beta1 < 1.0 && ad->beta2 >= 0.0 && ad->beta2 < 1.0;
+}
+
+int64_t smc_adam_norm_partials(int64_t n_params) { return (n_params + 1 + kNetThreads - 1) / kNetThreads; }
+
+int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t partial_blocks, int64_t n_params,
+                              void* grads, const smc_adam_args* adam, void* stream) {
+  if (!partials || !grads || partial_blocks <= 0 || n_params <= 0 ||
+      (dtype != SMC_DTYPE_F32 && dtype != SMC_DTYPE_F64))
+    return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_reduce_grads: bad argument");
+  if (adam && !adam_valid(adam)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_reduce_grads: bad Adam arguments");
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned grid = static_cast<unsigned>(smc_adam_norm_partials(n_params));
+  const AdamArgs ad = adam ? to_adam(adam) : AdamArgs{};
+  if (dtype == SMC_DTYPE_F32) {
+    if (adam)
+      hipLaunchKernelGGL((reduce_kernel<float, true>), dim3(grid), dim3(kNetThreads), 0, s,
+                         static_cast<const float*>(partials), partial_blocks, n_params, static_cast<float*>(grads), ad);
+    else
+      hipLaunchKernelGGL((reduce_kernel<float, false>), dim3(grid), dim3(kNetThreads), 0, s,
+                         static_cast<const float*>(partials), partial_blocks, n_params, static_cast<float*>(grads), ad);
+  } else {
+    if (adam)
+      hipLaunchKernelGGL((reduce_kernel<double, true>), dim3(grid), dim3(kNetThreads), 0, s,
+                         static_cast<const double*>(partials), partial_blocks, n_params, static_cast<double*>(grads), ad);
+    else
+      hipLaunchKernelGGL((reduce_kernel<double, false>), dim3(grid), dim3(kNetThreads), 0, s,
+                         static_cast<const double*>(partials), partial_blocks, n_params, static_cast<double*>(grads), ad);
+  }
+  int32_t rc = check_launch("cvnn reduce_kernel");
+  if (rc != SMC_OK || !adam) return rc;
+  if (dtype == SMC_DTYPE_F32)
+    hipLaunchKernelGGL(finalize_kernel<float>, dim3(1), dim3(kNetThreads), 0, s, adam->norm_partials,
+                       static_cast<int64_t>(grid), static_cast<const float*>(grads), n_params, adam->step,
+                       static_cast<float*>(adam->grad_norm), static_cast<float*>(adam->loss));
+  else
+    hipLaunchKernelGGL(finalize_kernel<double>, dim3(1), dim3(kNetThreads), 0, s, adam->norm_partials,
+                       static_cast<int64_t>(grid), static_cast<const double*>(grads), n_params, adam->step,
+                       static_cast<double*>(adam->grad_norm), static_cast<double*>(adam->loss));
+  return check_launch("cvnn finalize_kernel");
+}
+
+int32_t smc_adam_step(int32_t dtype, int64_t n_params, const void* grads, const smc_adam_args* adam, void* stream) {
+  if (!grads || !adam || n_params <= 0 || (dtype != SMC_DTYPE_F32 && dtype != SMC_DTYPE_F64))
+    return fail(SMC_ERR_INVALID_ARGUMENT, "smc_adam_step: bad argument");
+  if (!adam_valid(adam)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_adam_step: bad Adam arguments");
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const unsigned grid = static_cast<unsigned>(smc_adam_norm_partials(n_params));
+  const AdamArgs ad = to_adam(adam);
+  if (dtype == SMC_DTYPE_F32) {
+    hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(kNetThreads), 0, s, static_cast<const float*>(grads),
+                       n_params, ad);
+    int32_t rc = check_launch("adam_kernel");
+    if (rc != SMC_OK) return rc;
+    hipLaunchKernelGGL(finalize_kernel<float>, dim3(1), dim3(kNetThreads), 0, s, adam->norm_partials,
+                       static_cast<int64_t>(grid), static_cast<const float*>(grads), n_params, adam->step,
+                       static_cast<float*>(adam->grad_norm), static_cast<float*>(adam->loss));
+  } else {
+    hipLaunchKernelGGL(adam_kernel<double>, dim3(grid), dim3(kNetThreads), 0, s, static_cast<const double*>(grads),
+                       n_params, ad);
+    int32_t rc = check_launch("adam_kernel");
+    if (rc != SMC_OK) return rc;
+    hipLaunchKernelGGL(finalize_kernel<double>, dim3(1), dim3(kNetThreads), 0, s, adam->norm_partials,
+                       static_cast<int64_t>(grid), static_cast<const double*>(grads), n_params, adam->step,
+                       static_cast<double*>(adam->grad_norm), static_cast<double*>(adam->loss));
+  }
+  return check_launch("cvnn finalize_kernel");
+}
+
+}  // extern "C"
+#pragma GCC visibility pop

@@ -251,6 +251,16 @@ class _StepProgram:
         self.targets = [torch.empty_like(eb.targets) for _ in range(2)]
         self.mc_graph: torch.cuda.CUDAGraph | None = None
         self.nn_graphs: list[list[torch.cuda.CUDAGraph]] = []  # per slot
+        # network half on the fused HIP kernels when the architecture allows (net.py)
+        self.fused = None
+        if getattr(pricer, "fused_network", False):
+            from .net import FusedNetworkStep, UnsupportedNetwork
+
+            try:
+                self.fused = FusedNetworkStep(pricer._cvnn, adam, params, self.flat, self.loss, self.grad_norm,
+                                              batch=eb.real_in.shape[0], fuse_adam=dp is None)
+            except UnsupportedNetwork:
+                self.fused = None
 
     # -- pieces -------------------------------------------------------------------------
     def mc(self) -> None:
@@ -262,6 +272,9 @@ class _StepProgram:
         self.targets[slot].copy_(eb.targets)
 
     def fwd_bwd(self, slot: int) -> None:
+        if self.fused is not None:
+            self.fused.fwd_bwd(self.real_in[slot], self.imag_in, self.targets[slot])
+            return
         self.flat.zero_()
         targets = self.targets[slot]
         pred_r, pred_i = self.pricer._cvnn(self.real_in[slot], self.imag_in)
@@ -271,6 +284,10 @@ class _StepProgram:
         self.loss_slot.copy_(loss.detach().reshape(1))
 
     def update(self) -> None:
+        if self.fused is not None:
+            if not self.fused.fuse_adam:  # data-parallel: Adam after the all-reduce
+                self.fused.adam()
+            return
         self.adam.step()
         grads = [p.grad for p in self.params]
         self.grad_norm.copy_(torch.linalg.vector_norm(torch.stack(torch._foreach_norm(grads, 2.0)), 2.0))
@@ -343,6 +360,9 @@ class GbmCVNNPricer:
     math_mode: str = "hw"
     #: run step s+1's Monte-Carlo part on its own stream, concurrently with step s's network part
     overlap_mc: bool = True
+    #: network forward/backward/Adam on the fused HIP kernels (csrc/cvnn.hip) when the CVNN is a
+    #: ComplexLinear + modReLU/zReLU chain; False (or other architectures): torch-ROCm modules
+    fused_network: bool = True
 
     @staticmethod
     def create(cfg: GbmCVNNPricerConfig) -> Result["GbmCVNNPricer", GbmPricerError]:

@@ -1,0 +1,159 @@
+"""Fused network half of the training step on the HIP kernels of csrc/cvnn.hip.
+
+``FusedNetworkStep`` replaces the torch-ROCm forward / spectral-MSE / backward / Adam of
+``_torch_step`` (reference gbm_trainer.py:819-835) with three launches when the CVNN is a
+chain of ComplexLinear layers with optional modReLU / zReLU activations — the
+architectures ``cvnn_factory`` builds without batch norm or residual blocks.  Other models
+keep the torch path.
+
+State stays where torch expects it: the model's parameters and the Adam moments become views
+into flat device buffers (the kernels' layout), the Adam state dict keeps its keys
+(``step`` is one shared capturable f32 counter), so ``state_dict()`` / snapshots / resume
+are unchanged.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch import nn
+
+from . import _lib
+from .cvnn import ComplexLinear, ComplexSequential, modReLU, zReLU
+
+
+class UnsupportedNetwork(ValueError):
+    """The model or optimiser configuration is outside what the fused kernels implement."""
+
+
+def _flatten(m: nn.Module):
+    if isinstance(m, ComplexSequential):
+        for c in m.layers:
+            yield from _flatten(c)
+    else:
+        yield m
+
+
+def lower(model: nn.Module, params: list[nn.Parameter]) -> list[_lib.CvnnLayer]:
+    """Layer table of ``model`` with element offsets into the flat ``params`` layout."""
+    offsets, off = {}, 0
+    for p in params:
+        offsets[id(p)] = off
+        off += p.numel()
+    covered: set[int] = set()
+
+    def at(p: nn.Parameter | None) -> int:
+        if p is None:
+            return -1
+        covered.add(id(p))
+        return offsets[id(p)]
+
+    mods = list(_flatten(model))
+    table: list[_lib.CvnnLayer] = []
+    i = 0
+    while i < len(mods):
+        lin = mods[i]
+        if not isinstance(lin, ComplexLinear):
+            raise UnsupportedNetwork(f"expected ComplexLinear, got {type(lin).__name__}")
+        act, act_bias = _lib.ACT_NONE, -1
+        if i + 1 < len(mods) and isinstance(mods[i + 1], (modReLU, zReLU)):
+            nxt = mods[i + 1]
+            if isinstance(nxt, modReLU):
+                act, act_bias = _lib.ACT_MODRELU, at(nxt.bias)
+            else:
+                act = _lib.ACT_ZRELU
+            i += 1
+        table.append(_lib.CvnnLayer(in_features=lin.in_features, out_features=lin.out_features, activation=act,
+                                    reserved=0, w_re=at(lin.real_weight), w_im=at(lin.imag_weight),
+                                    b_re=at(lin.real_bias), b_im=at(lin.imag_bias), act_bias=act_bias))
+        i += 1
+    if not table or len(table) > _lib.CVNN_MAX_LAYERS:
+        raise UnsupportedNetwork(f"{len(table)} layers (1..{_lib.CVNN_MAX_LAYERS} supported)")
+    if covered != {id(p) for p in params}:
+        raise UnsupportedNetwork("model has parameters outside its ComplexLinear / modReLU chain")
+    return table
+
+
+class FusedNetworkStep:
+    """Device buffers + launches of one network step; ``fwd_bwd`` then (DP) ``adam``."""
+
+    def __init__(self, model: nn.Module, adam: torch.optim.Optimizer, params: list[nn.Parameter],
+                 flat_grads: torch.Tensor, loss_out: torch.Tensor, grad_norm_out: torch.Tensor, batch: int,
+                 fuse_adam: bool) -> None:
+        if len(adam.param_groups) != 1:
+            raise UnsupportedNetwork("one Adam parameter group expected")
+        g = adam.param_groups[0]
+        if g.get("amsgrad") or g.get("maximize") or g.get("differentiable") or g.get("decoupled_weight_decay"):
+            raise UnsupportedNetwork("amsgrad / maximize / differentiable / decoupled Adam not fused")
+        if [id(p) for p in g["params"]] != [id(p) for p in params]:
+            raise UnsupportedNetwork("optimizer parameters differ from the model's")
+        dtype = params[0].dtype
+        if dtype not in (torch.float32, torch.float64) or any(p.dtype != dtype for p in params):
+            raise UnsupportedNetwork(f"parameter dtype {dtype}")
+        self.table = lower(model, params)
+        self.dtype_code = _lib.DTYPE_F32 if dtype == torch.float32 else _lib.DTYPE_F64
+        self.n = sum(p.numel() for p in params)
+        self.batch = batch
+        dev = params[0].device
+        L = _lib.lib()
+        self._layers = (_lib.CvnnLayer * len(self.table))(*self.table)
+        blocks = ctypes.c_int64()
+        _lib.check(L.smc_cvnn_plan(self._layers, len(self.table), self.dtype_code, batch, ctypes.byref(blocks)))
+        self.blocks = blocks.value
+        self.partials = torch.empty((self.blocks, self.n + 1), dtype=dtype, device=dev)
+        self.norm_partials = torch.empty(int(L.smc_adam_norm_partials(self.n)), dtype=torch.float64, device=dev)
+        self.grads = flat_grads
+        # parameters and Adam moments -> flat buffers (views keep torch's objects valid)
+        self.params_flat = torch.empty(self.n, dtype=dtype, device=dev)
+        self.exp_avg = torch.zeros(self.n, dtype=dtype, device=dev)
+        self.exp_avg_sq = torch.zeros(self.n, dtype=dtype, device=dev)
+        step0 = 0.0
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                k = p.numel()
+                st = adam.state.get(p, {})
+                self.params_flat[off:off + k].copy_(p.detach().reshape(-1))
+                if "exp_avg" in st:
+                    self.exp_avg[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                    self.exp_avg_sq[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                    step0 = float(st["step"])
+                p.data = self.params_flat[off:off + k].view_as(p)
+                off += k
+        self.step = torch.tensor(step0, dtype=torch.float32, device=dev)
+        off = 0
+        for p in params:
+            k = p.numel()
+            adam.state[p] = {"step": self.step, "exp_avg": self.exp_avg[off:off + k].view_as(p),
+                             "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p)}
+            off += k
+        b1, b2 = g["betas"]
+        self.adam_args = _lib.AdamArgs(params=_lib.ptr(self.params_flat), exp_avg=_lib.ptr(self.exp_avg),
+                                       exp_avg_sq=_lib.ptr(self.exp_avg_sq), step=_lib.ptr(self.step),
+                                       lr=float(g["lr"]), beta1=float(b1), beta2=float(b2), eps=float(g["eps"]),
+                                       weight_decay=float(g["weight_decay"]),
+                                       norm_partials=_lib.ptr(self.norm_partials), grad_norm=_lib.ptr(grad_norm_out),
+                                       loss=_lib.ptr(loss_out))
+        self.fuse_adam = fuse_adam
+
+    def fwd_bwd(self, real_in: torch.Tensor, imag_in: torch.Tensor | None, targets: torch.Tensor) -> None:
+        """Gradients + loss into the flat buffer (and, fused, the Adam step) on the current stream."""
+        L = _lib.lib()
+        stream = _lib.stream_handle()
+        _lib.check(L.smc_cvnn_forward_backward(self._layers, len(self.table), self.dtype_code,
+                                               _lib.ptr(self.params_flat), self.n, _lib.ptr(real_in),
+                                               _lib.ptr(imag_in) if imag_in is not None else None,
+                                               _lib.ptr(targets), self.batch, _lib.ptr(self.partials), self.blocks,
+                                               stream))
+        _lib.check(L.smc_cvnn_reduce_grads(self.dtype_code, _lib.ptr(self.partials), self.blocks, self.n,
+                                           _lib.ptr(self.grads),
+                                           ctypes.byref(self.adam_args) if self.fuse_adam else None, stream))
+
+    def adam(self) -> None:
+        """Adam + grad norm + loss copy from the (all-reduced) flat buffer."""
+        _lib.check(_lib.lib().smc_adam_step(self.dtype_code, self.n, _lib.ptr(self.grads),
+                                            ctypes.byref(self.adam_args), _lib.stream_handle()))
+
+
+__all__ = ["FusedNetworkStep", "UnsupportedNetwork", "lower"]

@@ -224,3 +224,37 @@ def test_session_step_without_prefetch_then_close() -> None:
     st = sess.close()
     assert st.global_step == 3 and st.sobol_skip == 48
     assert max_param_diff(m, m_r) == 0.0
+
+
+def test_fused_network_matches_torch_modules() -> None:
+    """HIP network step (csrc/cvnn.hip) vs the torch-ROCm modules + torch Adam, 3 steps."""
+    fused, m_f = _pricer()
+    ref, m_r = _pricer()
+    ref.fused_network = False
+    cfg = make_training_config(num_batches=3, batch_size=32)
+    r_f = expect_success(fused.train(cfg))
+    r_r = expect_success(ref.train(cfg))
+    assert r_f.final_loss == pytest.approx(r_r.final_loss, rel=1e-4)
+    assert r_f.final_grad_norm == pytest.approx(r_r.final_grad_norm, rel=1e-3)
+    assert max_param_diff(m_f, m_r) < 3 * 1e-2 * 1e-2  # well inside one Adam step (lr = 1e-2)
+    st_f = r_f.updated_config.optimizer_state
+    st_r = r_r.updated_config.optimizer_state
+    assert st_f.param_states.keys() == st_r.param_states.keys()
+    for pid in st_f.param_states:
+        a = expect_success(st_f.param_states[pid].exp_avg.to_torch())
+        b = expect_success(st_r.param_states[pid].exp_avg.to_torch())
+        assert st_f.param_states[pid].step == st_r.param_states[pid].step == 3
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3 * float(b.abs().max()) + 1e-12)
+
+
+def test_fused_network_is_used_and_deterministic() -> None:
+    a, ma = _pricer()
+    b, mb = _pricer()
+    cfg = make_training_config(num_batches=4, batch_size=40)  # ragged last row block
+    sess = expect_success(a.open_session(cfg))
+    assert sess.program.fused is not None and sess.program.fused.blocks >= 1
+    for i in range(4):
+        expect_success(sess.step(prefetch_next=i < 3))
+    sess.close()
+    expect_success(b.train(cfg))
+    assert max_param_diff(ma, mb) == 0.0
