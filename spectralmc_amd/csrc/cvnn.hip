@@ -32,7 +32,7 @@ namespace {
 constexpr int kNetThreads = 256;
 constexpr int kMaxLayers = SMC_CVNN_MAX_LAYERS;
 constexpr int kMaxBlocks = 256;       // partial slots (workgroups) of forward_backward_kernel
-constexpr size_t kNetLdsBudget = 64 * 1024;
+constexpr size_t kNetLdsBudget = 96 * 1024;  // leaves room for two contract_kernel workgroups per CU
 
 struct NetArgs {
   int32_t n_layers;
@@ -57,11 +57,12 @@ struct LdsPlan {
   int64_t in_re, in_im;
   int64_t u[kMaxLayers], v[kMaxLayers], ar[kMaxLayers], ai[kMaxLayers];
   int64_t g[4];
+  int64_t scratch;          // input-gradient partials: 2 * max(kNetThreads, widest input)
   int64_t per_row;
 };
 
-__host__ __device__ inline LdsPlan plan_lds(const smc_cvnn_layer* layer, int n_layers) {
-  LdsPlan p{};
+__host__ __device__ inline void plan_lds_into(const smc_cvnn_layer* layer, int n_layers, LdsPlan* out) {
+  LdsPlan& p = *out;
   int64_t off = 0;
   const int n0 = layer[0].in_features;
   p.in_re = off;
@@ -90,7 +91,14 @@ __host__ __device__ inline LdsPlan plan_lds(const smc_cvnn_layer* layer, int n_l
     p.g[k] = off;
     off += wmax;
   }
+  p.scratch = off;
+  off += 2 * (wmax > kNetThreads ? wmax : kNetThreads);
   p.per_row = off;
+}
+
+inline LdsPlan plan_lds(const smc_cvnn_layer* layer, int n_layers) {
+  LdsPlan p{};
+  plan_lds_into(layer, n_layers, &p);
   return p;
 }
 
@@ -109,21 +117,33 @@ __device__ __forceinline__ Real block_sum(Real x, double* red_raw) {
   return t;
 }
 
-template <typename Real>
+// Forward + backward of R-row blocks.  Register blocking over the R rows: each weight is
+// loaded once per row block (forward: thread per output feature; input gradients: thread per
+// (input feature, j-group) with a fixed-order LDS reduction over the groups).
+template <typename Real, int R>
 __global__ __launch_bounds__(kNetThreads) void forward_backward_kernel(NetArgs a) {
   extern __shared__ double net_lds_raw[];
   Real* lds = reinterpret_cast<Real*>(net_lds_raw);
   const int tid = threadIdx.x;
   const int L = a.n_layers;
-  const int R = a.rows;
-  const LdsPlan pl = plan_lds(a.layer, L);
+  // layer table and LDS plan in LDS: indexed by the runtime layer number, they would otherwise
+  // be copied to scratch memory
+  __shared__ smc_cvnn_layer layer[kMaxLayers];
+  __shared__ LdsPlan pl;
   __shared__ double red[kNetThreads / 64];
+  if (tid == 0) {
+#pragma unroll
+    for (int i = 0; i < kMaxLayers; ++i) layer[i] = a.layer[i];  // compile-time indices: no scratch copy
+  }
+  __syncthreads();
+  if (tid == 0) plan_lds_into(layer, L, &pl);
+  __syncthreads();
   const Real* P = static_cast<const Real*>(a.params);
   Real* part = static_cast<Real*>(a.partials) + static_cast<int64_t>(blockIdx.x) * (a.n_params + 1);
   const Real* in_re = static_cast<const Real*>(a.input_re);
   const Real* in_im = static_cast<const Real*>(a.input_im);
   const Real* tgt = static_cast<const Real*>(a.targets);
-  const int n0 = a.layer[0].in_features;
+  const int n0 = layer[0].in_features;
   const int N = a.out_features;
   const Real scale = Real(2) / static_cast<Real>(static_cast<double>(a.batch) * N);  // d mean / d x
   double loss_acc = 0.0;
@@ -133,65 +153,83 @@ __global__ __launch_bounds__(kNetThreads) void forward_backward_kernel(NetArgs a
   for (int64_t rb = blockIdx.x; rb < n_blocks; rb += gridDim.x, first = false) {
     const int64_t r0 = rb * R;
     const int rows = static_cast<int>(a.batch - r0 < R ? a.batch - r0 : R);
-    // ---- load inputs
-    for (int i = tid; i < rows * n0; i += kNetThreads) {
-      lds[pl.in_re * R + i] = in_re[r0 * n0 + i];
-      lds[pl.in_im * R + i] = in_im ? in_im[r0 * n0 + i] : Real(0);
+    // ---- load inputs (rows >= `rows` are zero-filled so unused lanes of the blocking stay finite)
+    for (int i = tid; i < R * n0; i += kNetThreads) {
+      const bool ok = i < rows * n0;
+      lds[pl.in_re * R + i] = ok ? in_re[r0 * n0 + i] : Real(0);
+      lds[pl.in_im * R + i] = ok && in_im ? in_im[r0 * n0 + i] : Real(0);
     }
     __syncthreads();
     // ---- forward
     for (int l = 0; l < L; ++l) {
-      const smc_cvnn_layer& ly = a.layer[l];
+      const smc_cvnn_layer& ly = layer[l];
       const int ni = ly.in_features, no = ly.out_features;
       const Real* x = lds + (l == 0 ? pl.in_re : pl.ar[l - 1]) * R;
       const Real* y = lds + (l == 0 ? pl.in_im : pl.ai[l - 1]) * R;
       Real* u = lds + pl.u[l] * R;
       Real* v = lds + pl.v[l] * R;
-      const Real* A = P + ly.w_re;
-      const Real* Bw = P + ly.w_im;
-      for (int idx = tid; idx < rows * no; idx += kNetThreads) {
-        const int r = idx / no, j = idx - r * no;
-        Real su = ly.b_re >= 0 ? P[ly.b_re + j] : Real(0);
-        Real sv = ly.b_im >= 0 ? P[ly.b_im + j] : Real(0);
-        const Real* xr = x + r * ni;
-        const Real* yr = y + r * ni;
-        const Real* Aj = A + static_cast<int64_t>(j) * ni;
-        const Real* Bj = Bw + static_cast<int64_t>(j) * ni;
-        for (int k = 0; k < ni; ++k) {
-          su += Aj[k] * xr[k] - Bj[k] * yr[k];
-          sv += Bj[k] * xr[k] + Aj[k] * yr[k];
+      for (int j = tid; j < no; j += kNetThreads) {
+        Real au[R], av[R];
+        const Real br = ly.b_re >= 0 ? P[ly.b_re + j] : Real(0);
+        const Real bi = ly.b_im >= 0 ? P[ly.b_im + j] : Real(0);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          au[r] = br;
+          av[r] = bi;
         }
-        u[idx] = su;
-        v[idx] = sv;
-        if (ly.activation == SMC_ACT_MODRELU) {
-          const Real m = sqrt(su * su + sv * sv + Real(1e-9));
-          const Real t = m + P[ly.act_bias + j];
-          const Real g = (t > Real(0) ? t : Real(0)) / m;
-          lds[pl.ar[l] * R + idx] = g * su;
-          lds[pl.ai[l] * R + idx] = g * sv;
-        } else if (ly.activation == SMC_ACT_ZRELU) {
-          const bool keep = su >= Real(0) && sv >= Real(0);
-          lds[pl.ar[l] * R + idx] = keep ? su : Real(0);
-          lds[pl.ai[l] * R + idx] = keep ? sv : Real(0);
+        const Real* Aj = P + ly.w_re + static_cast<int64_t>(j) * ni;
+        const Real* Bj = P + ly.w_im + static_cast<int64_t>(j) * ni;
+        for (int k = 0; k < ni; ++k) {
+          const Real wa = Aj[k], wb = Bj[k];
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const Real xr = x[r * ni + k], yr = y[r * ni + k];
+            au[r] += wa * xr - wb * yr;
+            av[r] += wb * xr + wa * yr;
+          }
+        }
+        const Real c = ly.activation == SMC_ACT_MODRELU ? P[ly.act_bias + j] : Real(0);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int idx = r * no + j;
+          const Real su = au[r], sv = av[r];
+          u[idx] = su;
+          v[idx] = sv;
+          if (ly.activation == SMC_ACT_MODRELU) {
+            const Real m = sqrt(su * su + sv * sv + Real(1e-9));
+            const Real t = m + c;
+            const Real g = (t > Real(0) ? t : Real(0)) / m;
+            lds[pl.ar[l] * R + idx] = g * su;
+            lds[pl.ai[l] * R + idx] = g * sv;
+          } else if (ly.activation == SMC_ACT_ZRELU) {
+            const bool keep = su >= Real(0) && sv >= Real(0);
+            lds[pl.ar[l] * R + idx] = keep ? su : Real(0);
+            lds[pl.ai[l] * R + idx] = keep ? sv : Real(0);
+          }
         }
       }
       __syncthreads();
     }
-    // ---- loss and d loss / d prediction
+    // ---- loss and d loss / d prediction (rows >= `rows` get zero gradient)
     {
       const Real* pr = lds + pl.ar[L - 1] * R;
       const Real* pi = lds + pl.ai[L - 1] * R;
       Real* gr = lds + pl.g[0] * R;
       Real* gi = lds + pl.g[1] * R;
       double part_loss = 0.0;
-      for (int idx = tid; idx < rows * N; idx += kNetThreads) {
+      for (int idx = tid; idx < R * N; idx += kNetThreads) {
         const int r = idx / N, j = idx - r * N;
-        const int64_t t = ((r0 + r) * N + j) * 2;
-        const Real dr = pr[idx] - tgt[t];
-        const Real di = pi[idx] - tgt[t + 1];
-        part_loss += static_cast<double>(dr * dr) + static_cast<double>(di * di);
-        gr[idx] = scale * dr;
-        gi[idx] = scale * di;
+        if (r < rows) {
+          const int64_t t = ((r0 + r) * N + j) * 2;
+          const Real dr = pr[idx] - tgt[t];
+          const Real di = pi[idx] - tgt[t + 1];
+          part_loss += static_cast<double>(dr * dr) + static_cast<double>(di * di);
+          gr[idx] = scale * dr;
+          gi[idx] = scale * di;
+        } else {
+          gr[idx] = Real(0);
+          gi[idx] = Real(0);
+        }
       }
       loss_acc += block_sum<double>(part_loss, red);
     }
@@ -199,7 +237,7 @@ __global__ __launch_bounds__(kNetThreads) void forward_backward_kernel(NetArgs a
     // ---- backward
     int cur = 0;  // g[cur], g[cur+1]: gradient w.r.t. the current layer's output (re, im)
     for (int l = L - 1; l >= 0; --l) {
-      const smc_cvnn_layer& ly = a.layer[l];
+      const smc_cvnn_layer& ly = layer[l];
       const int ni = ly.in_features, no = ly.out_features;
       Real* go_r = lds + pl.g[cur] * R;
       Real* go_i = lds + pl.g[cur + 1] * R;
@@ -215,11 +253,11 @@ __global__ __launch_bounds__(kNetThreads) void forward_backward_kernel(NetArgs a
             const Real m = sqrt(u[idx] * u[idx] + v[idx] * v[idx] + Real(1e-9));
             if (m + c > Real(0)) s += (go_r[idx] * u[idx] + go_i[idx] * v[idx]) / m;
           }
-          Real* dst = static_cast<Real*>(part) + ly.act_bias + j;
+          Real* dst = part + ly.act_bias + j;
           *dst = first ? s : *dst + s;
         }
         __syncthreads();
-        for (int idx = tid; idx < rows * no; idx += kNetThreads) {
+        for (int idx = tid; idx < R * no; idx += kNetThreads) {
           const int j = idx % no;
           const Real c = P[ly.act_bias + j];
           const Real uu = u[idx], vv = v[idx];
@@ -236,7 +274,7 @@ __global__ __launch_bounds__(kNetThreads) void forward_backward_kernel(NetArgs a
         }
         __syncthreads();
       } else if (ly.activation == SMC_ACT_ZRELU) {
-        for (int idx = tid; idx < rows * no; idx += kNetThreads) {
+        for (int idx = tid; idx < R * no; idx += kNetThreads) {
           if (!(u[idx] >= Real(0) && v[idx] >= Real(0))) {
             go_r[idx] = Real(0);
             go_i[idx] = Real(0);
@@ -250,7 +288,8 @@ __global__ __launch_bounds__(kNetThreads) void forward_backward_kernel(NetArgs a
       for (int idx = tid; idx < no * ni; idx += kNetThreads) {
         const int j = idx / ni, k = idx - j * ni;
         Real da = 0, db = 0;
-        for (int r = 0; r < rows; ++r) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
           const Real gu = go_r[r * no + j], gv = go_i[r * no + j];
           const Real xk = x[r * ni + k], yk = y[r * ni + k];
           da += gu * xk + gv * yk;
@@ -263,7 +302,8 @@ __global__ __launch_bounds__(kNetThreads) void forward_backward_kernel(NetArgs a
       }
       for (int j = tid; j < no; j += kNetThreads) {
         Real sr = 0, si = 0;
-        for (int r = 0; r < rows; ++r) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
           sr += go_r[r * no + j];
           si += go_i[r * no + j];
         }
@@ -271,19 +311,44 @@ __global__ __launch_bounds__(kNetThreads) void forward_backward_kernel(NetArgs a
         if (ly.b_im >= 0) part[ly.b_im + j] = first ? si : part[ly.b_im + j] + si;
       }
       if (l > 0) {
-        // input gradients: gx = A^T gu + B^T gv,  gy = A^T gv - B^T gu
+        // input gradients gx = A^T gu + B^T gv, gy = A^T gv - B^T gu: thread (g, k) sums the
+        // j = g, g+G, ... terms for all R rows; the G partials are added in order after a barrier
         Real* gx = lds + pl.g[2 - cur] * R;
         Real* gy = lds + pl.g[3 - cur] * R;
+        Real* scr = lds + pl.scratch * R;
+        const int G = ni >= kNetThreads ? 1 : kNetThreads / ni;
         const Real* A = P + ly.w_re;
         const Real* Bw = P + ly.w_im;
-        for (int idx = tid; idx < rows * ni; idx += kNetThreads) {
+        for (int t = tid; t < G * ni; t += kNetThreads) {
+          const int g = t / ni, k = t - g * ni;
+          Real sx[R], sy[R];
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            sx[r] = Real(0);
+            sy[r] = Real(0);
+          }
+          for (int j = g; j < no; j += G) {
+            const Real wa = A[static_cast<int64_t>(j) * ni + k], wb = Bw[static_cast<int64_t>(j) * ni + k];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const Real gu = go_r[r * no + j], gv = go_i[r * no + j];
+              sx[r] += wa * gu + wb * gv;
+              sy[r] += wa * gv - wb * gu;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            scr[(static_cast<int64_t>(r) * G + g) * ni + k] = sx[r];
+            scr[(static_cast<int64_t>(R + r) * G + g) * ni + k] = sy[r];
+          }
+        }
+        __syncthreads();
+        for (int idx = tid; idx < R * ni; idx += kNetThreads) {
           const int r = idx / ni, k = idx - r * ni;
           Real sx = 0, sy = 0;
-          for (int j = 0; j < no; ++j) {
-            const Real a_ = A[static_cast<int64_t>(j) * ni + k], b_ = Bw[static_cast<int64_t>(j) * ni + k];
-            const Real gu = go_r[r * no + j], gv = go_i[r * no + j];
-            sx += a_ * gu + b_ * gv;
-            sy += a_ * gv - b_ * gu;
+          for (int g = 0; g < G; ++g) {
+            sx += scr[(static_cast<int64_t>(r) * G + g) * ni + k];
+            sy += scr[(static_cast<int64_t>(R + r) * G + g) * ni + k];
           }
           gx[idx] = sx;
           gy[idx] = sy;
@@ -324,16 +389,35 @@ __device__ __forceinline__ void adam_update(const AdamArgs& ad, int64_t p, Real 
   prm[p] = prm[p] - step_size * (mm / denom);
 }
 
+// One block = 64 consecutive gradient entries x 4 slices of the G partials (a wave per slice,
+// so every load instruction reads 64 consecutive entries); slices are added in order.
+constexpr int kReduceCols = 64;
+constexpr int kReduceSlices = kNetThreads / kReduceCols;
+
 template <typename Real, bool ADAM>
 __global__ __launch_bounds__(kNetThreads) void reduce_kernel(const Real* __restrict__ partials, int64_t blocks,
                                                              int64_t n_params, Real* __restrict__ grads,
                                                              AdamArgs ad) {
   __shared__ double red[kNetThreads / 64];
-  const int64_t p = static_cast<int64_t>(blockIdx.x) * kNetThreads + threadIdx.x;
-  double sq = 0.0;
+  __shared__ double slice_sum[kReduceSlices][kReduceCols];
+  const int col = threadIdx.x % kReduceCols, slice = threadIdx.x / kReduceCols;
+  const int64_t p = static_cast<int64_t>(blockIdx.x) * kReduceCols + col;
+  const int64_t stride = n_params + 1;
+  double s0 = 0.0, s1 = 0.0;
   if (p <= n_params) {
+    int64_t g = slice;
+    for (; g + kReduceSlices < blocks; g += 2 * kReduceSlices) {
+      s0 += static_cast<double>(partials[g * stride + p]);
+      s1 += static_cast<double>(partials[(g + kReduceSlices) * stride + p]);
+    }
+    for (; g < blocks; g += kReduceSlices) s0 += static_cast<double>(partials[g * stride + p]);
+  }
+  slice_sum[slice][col] = s0 + s1;
+  __syncthreads();
+  double sq = 0.0;
+  if (slice == 0 && p <= n_params) {
     double s = 0.0;
-    for (int64_t g = 0; g < blocks; ++g) s += static_cast<double>(partials[g * (n_params + 1) + p]);
+    for (int k = 0; k < kReduceSlices; ++k) s += slice_sum[k][col];
     const Real gr = static_cast<Real>(s);
     grads[p] = gr;
     if (ADAM && p < n_params) {
@@ -399,14 +483,39 @@ int32_t plan_rows(const smc_cvnn_layer* layers, int32_t n_layers, int32_t dtype,
                   int64_t* blocks, size_t* lds) {
   const LdsPlan pl = plan_lds(layers, n_layers);
   const size_t elem = dtype == SMC_DTYPE_F64 ? 8 : 4;
-  int64_t r = static_cast<int64_t>(kNetLdsBudget / (static_cast<size_t>(pl.per_row) * elem));
-  if (r < 1) return fail(SMC_ERR_INVALID_SHAPE, "cvnn: layer widths exceed the LDS budget");
-  if (r > 16) r = 16;
+  int r = 16;
+  while (r > 1 && static_cast<size_t>(pl.per_row) * r * elem > kNetLdsBudget) r >>= 1;
+  if (static_cast<size_t>(pl.per_row) * r * elem > kNetLdsBudget)
+    return fail(SMC_ERR_INVALID_SHAPE, "cvnn: layer widths exceed the LDS budget");
   const int64_t n_blocks = (batch + r - 1) / r;
-  *rows = static_cast<int32_t>(r);
+  *rows = r;
   *blocks = n_blocks < kMaxBlocks ? n_blocks : kMaxBlocks;
-  *lds = static_cast<size_t>(pl.per_row * r) * elem;
+  *lds = static_cast<size_t>(pl.per_row) * r * elem;
   return SMC_OK;
+}
+
+template <typename Real, int R>
+int32_t launch_fwd_bwd_r(const NetArgs& a, unsigned grid, size_t lds, hipStream_t s) {
+  auto kernel = forward_backward_kernel<Real, R>;
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "cvnn forward_backward_kernel: cannot raise the dynamic LDS limit");
+  }
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kNetThreads), lds, s, a);
+  return SMC_OK;
+}
+
+template <typename Real>
+int32_t launch_fwd_bwd(const NetArgs& a, unsigned grid, size_t lds, hipStream_t s) {
+  switch (a.rows) {
+    case 16: return launch_fwd_bwd_r<Real, 16>(a, grid, lds, s);
+    case 8: return launch_fwd_bwd_r<Real, 8>(a, grid, lds, s);
+    case 4: return launch_fwd_bwd_r<Real, 4>(a, grid, lds, s);
+    case 2: return launch_fwd_bwd_r<Real, 2>(a, grid, lds, s);
+    default: return launch_fwd_bwd_r<Real, 1>(a, grid, lds, s);
+  }
 }
 
 }  // namespace
@@ -456,10 +565,9 @@ int32_t smc_cvnn_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers
   a.targets = targets;
   a.partials = partials;
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  if (dtype == SMC_DTYPE_F32)
-    hipLaunchKernelGGL(forward_backward_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(kNetThreads), lds, s, a);
-  else
-    hipLaunchKernelGGL(forward_backward_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(kNetThreads), lds, s, a);
+  const int32_t lrc = dtype == SMC_DTYPE_F32 ? launch_fwd_bwd<float>(a, static_cast<unsigned>(blocks), lds, s)
+                                             : launch_fwd_bwd<double>(a, static_cast<unsigned>(blocks), lds, s);
+  if (lrc != SMC_OK) return lrc;
   return check_launch("cvnn forward_backward_kernel");
 }
 
@@ -483,7 +591,7 @@ static bool adam_valid(const smc_adam_args* ad) {
          ad->loss && ad->lr > 0.0 && ad->beta1 >= 0.0 && ad->beta1 < 1.0 && ad->beta2 >= 0.0 && ad->beta2 < 1.0;
 }
 
-int64_t smc_adam_norm_partials(int64_t n_params) { return (n_params + 1 + kNetThreads - 1) / kNetThreads; }
+int64_t smc_adam_norm_partials(int64_t n_params) { return (n_params + 1 + kReduceCols - 1) / kReduceCols; }
 
 int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t partial_blocks, int64_t n_params,
                               void* grads, const smc_adam_args* adam, void* stream) {
@@ -492,7 +600,7 @@ int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t parti
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_reduce_grads: bad argument");
   if (adam && !adam_valid(adam)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_reduce_grads: bad Adam arguments");
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  const unsigned grid = static_cast<unsigned>(smc_adam_norm_partials(n_params));
+  const unsigned grid = static_cast<unsigned>(smc_adam_norm_partials(n_params));  // 64 entries per block
   const AdamArgs ad = adam ? to_adam(adam) : AdamArgs{};
   if (dtype == SMC_DTYPE_F32) {
     if (adam)
@@ -527,7 +635,7 @@ int32_t smc_adam_step(int32_t dtype, int64_t n_params, const void* grads, const 
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_adam_step: bad argument");
   if (!adam_valid(adam)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_adam_step: bad Adam arguments");
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  const unsigned grid = static_cast<unsigned>(smc_adam_norm_partials(n_params));
+  const unsigned grid = static_cast<unsigned>((n_params + kNetThreads - 1) / kNetThreads);
   const AdamArgs ad = to_adam(adam);
   if (dtype == SMC_DTYPE_F32) {
     hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(kNetThreads), 0, s, static_cast<const float*>(grads),
