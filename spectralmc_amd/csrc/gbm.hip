@@ -138,6 +138,19 @@ struct Stepper {
 
 constexpr int kRowBlock = 16;  // rows accumulated in registers per pass over the paths
 
+// x[j] *= 2^y[j] for the lane's 4 paths, two v_pk_mul_f32 (f32 HW log-Euler)
+template <typename Real>
+__device__ __forceinline__ void advance_packed(Real (&x)[4], const Real (&y)[4]) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int j = 0; j < 4; j += 2) {
+    const f2 e = {__builtin_amdgcn_exp2f(y[j]), __builtin_amdgcn_exp2f(y[j + 1])};
+    const f2 v = f2{x[j], x[j + 1]} * e;
+    x[j] = v.x;
+    x[j + 1] = v.y;
+  }
+}
+
 // The 4 paths p0..p0+3 of one lane: steps [0, t0) are replayed without output (only when
 // T > kRowBlock), rows [t0, t0 + nrows) are stored and added to acc[].  MASKED handles the
 // ragged last chunk (nvalid < 4) and P % 4 != 0 with scalar stores; otherwise one dwordx4
@@ -152,14 +165,22 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   const bool store_all = a.store == SMC_STORE_ALL;
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));  // the lane's group stream
+  // f32 HW log-Euler: the RNG hands back the step exponents directly (packed path pairs)
+  constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
   Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
 #pragma unroll
   for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
   for (int t = 0; t < t0; t += 2) {  // t0 is a multiple of kRowBlock (even)
+    if constexpr (kPacked) {
+      s.hw_log_increments4(step.b, step.a, zl, zh);
+      advance_packed(x, zl);
+      advance_packed(x, zh);
+    } else {
 #pragma unroll
-    for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
+      for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
 #pragma unroll
-    for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(step(x[j], zl[j]), zh[j]);
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(step(x[j], zl[j]), zh[j]);
+    }
   }
   // wave-uniform row base (SGPR pair) + 32-bit per-lane byte offset
   const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(Real)) * threadIdx.x;
@@ -168,12 +189,17 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   for (int i = 0; i < kRowBlock; ++i) {
     if (FULLBLOCK || i < nrows) {
       const int t = t0 + i;
-      if ((i & 1) == 0) {
+      if constexpr (kPacked) {
+        if ((i & 1) == 0) s.hw_log_increments4(step.b, step.a, zl, zh);
+        advance_packed(x, (i & 1) ? zh : zl);
+      } else {
+        if ((i & 1) == 0) {
 #pragma unroll
-        for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
+          for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (i & 1) ? zh[j] : zl[j]);
       }
-#pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (i & 1) ? zh[j] : zl[j]);
       if (store_all || t == T - 1) {
         char* row = reinterpret_cast<char*>(chunk_base + (store_all ? static_cast<int64_t>(t) * P : 0));
         if constexpr (!MASKED) {
@@ -286,14 +312,26 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
   double* cs = avg + N;                                // [N]
   double* sn = cs + N;                                 // [N]
 
+  constexpr int kBatch = 16;  // loads in flight per thread; the sum keeps the m order
   for (int item = tid; item < items; item += kThreads) {
     const int n = item % N, g = item / N;
     double sum = 0.0;
-    for (int m = g; m < M; m += G) {
-      const Real xs = row[static_cast<int64_t>(m) * N + n] * s;  // sims *= scale (rounded to Real)
-      const Real diff = K - xs;
-      const Real pay = df * (diff > Real(0) ? diff : Real(0));
-      sum += static_cast<double>(pay);
+    for (int m0 = g; m0 < M; m0 += G * kBatch) {
+      Real v[kBatch];
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        const int m = m0 + u * G < M ? m0 + u * G : M - 1;  // clamped: loads stay unconditional
+        v[u] = row[static_cast<int64_t>(m) * N + n];
+      }
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        if (m0 + u * G < M) {
+          const Real xs = v[u] * s;  // sims *= scale (rounded to Real)
+          const Real diff = K - xs;
+          const Real pay = df * (diff > Real(0) ? diff : Real(0));
+          sum += static_cast<double>(pay);
+        }
+      }
     }
     part[item] = sum;
   }

@@ -91,6 +91,16 @@ struct PathStream {
   //   2 alignbit + 1 sub + 4 transcendentals + 2 mul per pair.
   template <bool HW>
   __device__ __forceinline__ void normal_pair(float& z0, float& z1) {
+#if defined(SMC_EXPERIMENT_ZERO_NORMALS)  // tools/micro decomposition builds only
+    z0 = 0.0f;
+    z1 = 0.0f;
+    return;
+#elif defined(SMC_EXPERIMENT_NO_TRANSCENDENTALS)
+    const uint32_t ea = next(), eb = next();
+    z0 = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ea, 9)) - 1.5f;
+    z1 = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, eb, 9)) - 1.5f;
+    return;
+#endif
     const uint32_t a = next(), b = next();
     const float u1 = 2.0f - __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, a, 9));
     if constexpr (HW) {
@@ -104,6 +114,34 @@ struct PathStream {
       math::sincos2pi_u24((b >> 9) << 1, sn, cs);
       z0 = r * cs;
       z1 = r * sn;
+    }
+  }
+
+  // HW log-Euler fast path: exponents y = a + b z of the next two steps for the lane's 4 paths
+  // (ylo: step t, yhi: step t+1), same draws as normal_pair<true>, with b folded into the
+  // Box-Muller radius (one fma per normal) and path pairs packed into v_pk_* ops.
+  __device__ __forceinline__ void hw_log_increments4(float b, float a, float (&ylo)[4], float (&yhi)[4]) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    float r[4], c[4], sn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t ua = next(), ub = next();
+      const float u1 = 2.0f - __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ua, 9));
+      r[j] = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u1));
+      const float w = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ub, 9));
+      c[j] = __builtin_amdgcn_cosf(w);
+      sn[j] = __builtin_amdgcn_sinf(w);
+    }
+    const f2 bb = {b, b}, aa = {a, a};
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+      const f2 br = f2{r[j], r[j + 1]} * bb;
+      const f2 lo = __builtin_elementwise_fma(br, f2{c[j], c[j + 1]}, aa);
+      const f2 hi = __builtin_elementwise_fma(br, f2{sn[j], sn[j + 1]}, aa);
+      ylo[j] = lo.x;
+      ylo[j + 1] = lo.y;
+      yhi[j] = hi.x;
+      yhi[j + 1] = hi.y;
     }
   }
 
