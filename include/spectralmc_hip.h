@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 2
+#define SMC_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -113,14 +113,19 @@ int32_t smc_cf_targets(const double* contracts_dev, int64_t n_contracts, int32_t
                        void* targets_dev, void* stream);
 /* Fused training targets: simulate + (store) + normalise + payoff + M-mean + DFT for
  * B contracts.  store_mode SMC_STORE_ALL writes the full matrix into paths_dev, which
- * holds `chunk_contracts` contracts ([chunk][T][P]) and is reused chunk by chunk;
- * SMC_STORE_TERMINAL needs paths_dev of [chunk][P].  targets_dev: [B][N] complex. */
+ * holds `chunk_contracts` contracts ([chunk][T][pitch]) and is reused chunk by chunk;
+ * SMC_STORE_TERMINAL needs paths_dev of [chunk][pitch].  path_pitch: elements between
+ * consecutive path rows (0 = P, contiguous; else a multiple of 4 >= P, e.g. smc_path_pitch).
+ * targets_dev: [B][N] complex. */
 int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int32_t timesteps,
                           int32_t network_size, int32_t batches_per_mc_run, uint64_t mc_seed,
                           const int64_t* ordinal_dev, int64_t ordinal0, int32_t scheme,
                           int32_t normalization, int32_t dtype, int32_t store_mode,
-                          void* paths_dev, int64_t chunk_contracts, double* rowsum_dev,
-                          void* targets_dev, void* stream);
+                          void* paths_dev, int64_t path_pitch, int64_t chunk_contracts,
+                          double* rowsum_dev, void* targets_dev, void* stream);
+/* Recommended row pitch (elements) for a path scratch buffer of n_paths columns: the row
+ * stride becomes an odd multiple of 4 KiB (power-of-two strides alias in HBM). */
+int64_t smc_path_pitch(int64_t n_paths, int32_t dtype);
 /* The [rows][cols] N(0,1) matrix of contract ordinal m (the values smc_gbm_simulate
  * draws for path p, step t, laid out [t][p]). */
 int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t cols,

@@ -66,6 +66,7 @@ struct EngineArgs {
   void* paths;
   double* rowsum;             // [B][T] or NULL
   void* targets;              // [B][N] complex or NULL
+  int64_t pitch;              // elements between consecutive path rows (0: P, contiguous)
 };
 
 template <typename Real>
@@ -162,6 +163,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   using V4 = typename Vec4T<Real>::type;
   const int T = a.T;
   const int64_t P = a.P;
+  const int64_t pitch = a.pitch ? a.pitch : P;
   const bool store_all = a.store == SMC_STORE_ALL;
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));  // the lane's group stream
@@ -201,7 +203,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
         for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (i & 1) ? zh[j] : zl[j]);
       }
       if (store_all || t == T - 1) {
-        char* row = reinterpret_cast<char*>(chunk_base + (store_all ? static_cast<int64_t>(t) * P : 0));
+        char* row = reinterpret_cast<char*>(chunk_base + (store_all ? static_cast<int64_t>(t) * pitch : 0));
         if constexpr (!MASKED) {
           V4 v4;
           v4.x = x[0];
@@ -237,7 +239,8 @@ __device__ void simulate_contract(const EngineArgs& a, const Contract& c, uint64
   const int T = a.T;
   const int64_t P = a.P;
   const bool store_all = a.store == SMC_STORE_ALL;
-  Real* base = static_cast<Real*>(a.paths) + (store_all ? b * T * P : b * P);
+  const int64_t pitch = a.pitch ? a.pitch : P;
+  Real* base = static_cast<Real*>(a.paths) + (store_all ? b * T * pitch : b * pitch);
   const bool vec_ok = (P % kPathsPerLane) == 0;
   const int64_t full_end = vec_ok ? (P / kChunk) * kChunk : 0;
   const Stepper<Real, LOG_EULER, HW> step(c, T);
@@ -290,7 +293,8 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
   const int T = a.T, N = a.N, M = a.M;
   const int64_t P = a.P;
   const bool store_all = a.store == SMC_STORE_ALL;
-  const Real* row = static_cast<const Real*>(a.paths) + (store_all ? (b * T + (T - 1)) * P : b * P);
+  const int64_t pitch = a.pitch ? a.pitch : P;
+  const Real* row = static_cast<const Real*>(a.paths) + (store_all ? (b * T + (T - 1)) * pitch : b * pitch);
 
   // Reference scalar semantics: gbm.py:429-431 evaluate times/forwards/df in the sim dtype.
   Real F, df;
@@ -383,7 +387,11 @@ __global__ __launch_bounds__(kThreads) void contract_kernel(EngineArgs a) {
     terminal_sum = a.rowsum[b * T + (T - 1)];
   }
   if (!ALLROWS && a.rowsum && threadIdx.x == 0 && a.simulate) a.rowsum[b * T + (T - 1)] = terminal_sum;
+#if defined(SMC_EXPERIMENT_NO_CF)  // tools/micro decomposition builds only
+  if (false) {
+#else
   if (a.targets) {
+#endif
     __syncthreads();  // workgroup-scope fence: phase-1 stores of the terminal row are visible
     cf_targets_contract<Real>(a, c, b, terminal_sum, lds_work);
   }
@@ -559,7 +567,8 @@ int32_t smc_cf_targets(const double* contracts_dev, int64_t n_contracts, int32_t
 int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int32_t timesteps, int32_t network_size,
                           int32_t batches_per_mc_run, uint64_t mc_seed, const int64_t* ordinal_dev, int64_t ordinal0,
                           int32_t scheme, int32_t normalization, int32_t dtype, int32_t store_mode, void* paths_dev,
-                          int64_t chunk_contracts, double* rowsum_dev, void* targets_dev, void* stream) {
+                          int64_t path_pitch, int64_t chunk_contracts, double* rowsum_dev, void* targets_dev,
+                          void* stream) {
   const int64_t P = static_cast<int64_t>(network_size) * batches_per_mc_run;
   if (network_size <= 0 || batches_per_mc_run <= 0)
     return fail(SMC_ERR_INVALID_SHAPE, "smc_train_targets: network_size and batches_per_mc_run must be > 0");
@@ -569,6 +578,8 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_targets: bad store_mode");
   if (!valid_scheme(scheme)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_targets: bad scheme");
   if (chunk_contracts <= 0) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_targets: chunk_contracts <= 0");
+  if (path_pitch != 0 && (path_pitch < P || (path_pitch != P && path_pitch % kPathsPerLane != 0)))
+    return fail(SMC_ERR_INVALID_SHAPE, "smc_train_targets: path_pitch must be 0, P, or a multiple of 4 >= P");
   const size_t esz = dtype == SMC_DTYPE_F32 ? sizeof(float) : sizeof(double);
   const size_t csz = dtype == SMC_DTYPE_F32 ? 2 * sizeof(float) : 2 * sizeof(double);
   for (int64_t off = 0; off < n_contracts; off += chunk_contracts) {
@@ -577,11 +588,23 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
                  ordinal_dev, ordinal0 + off, scheme, normalization != SMC_NORM_RAW, store_mode, 1,
                  rowsum_dev ? 1 : 0, paths_dev,
                  rowsum_dev ? rowsum_dev + off * timesteps : nullptr,
-                 static_cast<char*>(targets_dev) + static_cast<size_t>(off) * network_size * csz};
+                 static_cast<char*>(targets_dev) + static_cast<size_t>(off) * network_size * csz, path_pitch};
     (void)esz;
     if (int32_t st = dispatch_engine(a, dtype, as_stream(stream))) return st;
   }
   return SMC_OK;
+}
+
+int64_t smc_path_pitch(int64_t n_paths, int32_t dtype) {
+  // rows at a power-of-two stride alias in the memory system (a 13 % slower store stream at
+  // C2, tools/micro/pitchbench.hip): round the row up to 4 KiB, then make the stride an odd
+  // multiple of 4 KiB
+  if (n_paths <= 0) return 0;
+  const int64_t esz = (dtype & 0xff) == SMC_DTYPE_F64 ? 8 : 4;
+  const int64_t unit = 4096 / esz;
+  int64_t units = (n_paths + unit - 1) / unit;
+  if (units % 2 == 0) ++units;
+  return units * unit;
 }
 
 int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t cols, int32_t dtype, void* out_dev,

@@ -31,7 +31,8 @@ from .gbm import BlackScholesConfig, dtype_code, normalization_code, scheme_code
 from .models.numerical import Precision
 from .sobol_sampler import SobolSampler, draw_device
 
-DEFAULT_PATH_BUFFER_BYTES = int(float(os.environ.get("SMC_PATH_BUFFER_GB", "16")) * (1 << 30))
+# path scratch budget: 288 GB of HBM per MI355X; C2 needs 17.4 GB, C3 is cut into equal launches
+DEFAULT_PATH_BUFFER_BYTES = int(float(os.environ.get("SMC_PATH_BUFFER_GB", "40")) * (1 << 30))
 
 
 @dataclass(frozen=True)
@@ -87,11 +88,16 @@ class TrainingEngine:
         self.buffers = StepBuffers(contracts=contracts, real_in=real_in,
                                    imag_in=torch.zeros_like(real_in),
                                    targets=torch.empty((B, self.N), dtype=cplx, device=device))
-        per_contract = (self.T * self.P if store_paths else self.P) * torch.finfo(sim_torch).bits // 8
+        # scratch rows at a padded pitch: a power-of-two row stride aliases in HBM
+        self.pitch = int(_lib.lib().smc_path_pitch(self.P, self._dtype_code))
+        per_contract = (self.T * self.pitch if store_paths else self.pitch) * torch.finfo(sim_torch).bits // 8
         budget = path_buffer_bytes if path_buffer_bytes is not None else DEFAULT_PATH_BUFFER_BYTES
-        self.chunk = max(1, min(B, budget // per_contract))
-        shape = (self.chunk, self.T, self.P) if store_paths else (self.chunk, self.P)
-        self.paths = torch.empty(shape, dtype=sim_torch, device=device)
+        max_chunk = max(1, min(B, budget // per_contract))
+        launches = -(-B // max_chunk)
+        self.chunk = -(-B // launches)  # equal launches: no small trailing launch
+        shape = (self.chunk, self.T, self.pitch) if store_paths else (self.chunk, self.pitch)
+        self._paths_buf = torch.empty(shape, dtype=sim_torch, device=device)
+        self.paths = self._paths_buf[..., :self.P]  # (chunk, T, P) / (chunk, P) strided view
         self._f32_in = model_dtype == torch.float32
 
     @property
@@ -114,7 +120,8 @@ class TrainingEngine:
             b.real_in.copy_(b.contracts)
         _lib.check(L.smc_train_targets(
             _lib.ptr(b.contracts), self.B, self.T, self.N, self.M, self.seed, _lib.ptr(self.cursor[1:2]), offset,
-            self._scheme, self._norm, self._dtype_code, self.store_mode, _lib.ptr(self.paths), self.chunk,
+            self._scheme, self._norm, self._dtype_code, self.store_mode, _lib.ptr(self._paths_buf), self.pitch,
+            self.chunk,
             None, _lib.ptr(b.targets), stream))  # training needs only the terminal row sum (kept on chip)
         self.cursor.add_(self.global_batch)
         return b

@@ -77,12 +77,17 @@ def test_engine_argument_errors_do_not_launch() -> None:
     assert L.smc_gbm_simulate(p, 1, 0, 1024, 7, None, 0, 0, 0, p, None, None) == _lib.SMC_ERR_INVALID_SHAPE
     assert L.smc_gbm_simulate(p, 1, 16, 1024, 7, None, 0, 5, 0, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
     assert L.smc_gbm_simulate(p, 1, 16, 1024, 7, None, 0, 0, 9, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
-    assert L.smc_train_targets(p, 4, 16, 0, 4, 7, None, 0, 0, 1, 0, 2, p, 4, None, p, None) == \
+    assert L.smc_train_targets(p, 4, 16, 0, 4, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, None) == \
         _lib.SMC_ERR_INVALID_SHAPE
-    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 3, p, 4, None, p, None) == \
+    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 3, p, 0, 4, None, p, None) == \
         _lib.SMC_ERR_INVALID_ARGUMENT
     # an N too large for the LDS budget is a shape error, reported before launching
-    assert L.smc_train_targets(p, 4, 16, 1 << 14, 1, 7, None, 0, 0, 1, 0, 2, p, 4, None, p, None) == \
+    assert L.smc_train_targets(p, 4, 16, 1 << 14, 1, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, None) == \
+        _lib.SMC_ERR_INVALID_SHAPE
+    # a row pitch below P, or not a multiple of 4, is a shape error
+    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 31, 4, None, p, None) == \
+        _lib.SMC_ERR_INVALID_SHAPE
+    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 34, 4, None, p, None) == \
         _lib.SMC_ERR_INVALID_SHAPE
     assert L.smc_normals(7, 0, 0, 10, 0, p, None) == _lib.SMC_ERR_INVALID_SHAPE
     assert L.smc_sobol_draw(None, 6, None, 0, 4, p, p, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
@@ -92,4 +97,15 @@ def test_zero_contracts_is_a_noop() -> None:
     L = _lib.lib()
     dummy = ctypes.c_double(0.0)
     p = ctypes.addressof(dummy)
-    assert L.smc_train_targets(p, 0, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 4, None, p, None) == _lib.SMC_OK
+    assert L.smc_train_targets(p, 0, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, None) == _lib.SMC_OK
+
+
+def test_path_pitch_is_an_odd_multiple_of_4k() -> None:
+    L = _lib.lib()
+    assert L.smc_path_pitch(65536, _lib.DTYPE_F32) == 65536 + 1024
+    assert L.smc_path_pitch(1024, _lib.DTYPE_F32) == 1024
+    assert L.smc_path_pitch(1000, _lib.DTYPE_F32) == 1024
+    assert L.smc_path_pitch(65536, _lib.DTYPE_F64) == 65536 + 512
+    for P in (4, 100, 4096, 262144, 1 << 20):
+        q = L.smc_path_pitch(P, _lib.DTYPE_F32)
+        assert q >= P and (q * 4) % 4096 == 0 and ((q * 4) // 4096) % 2 == 1

@@ -143,22 +143,24 @@ TARGET_CASES = [
 
 
 def _run_targets(c: np.ndarray, T: int, N: int, M: int, scheme: int, normalize: int, dtype: str, store: int,
-                 chunk: int | None = None, ordinal0: int = 0, with_rowsum: bool = True, flags: int = 0):
+                 chunk: int | None = None, ordinal0: int = 0, with_rowsum: bool = True, flags: int = 0,
+                 pitch: int | None = None):
     B = c.shape[0]
     P = N * M
     tdt = torch.float32 if dtype == "float32" else torch.float64
     cdt = torch.complex64 if dtype == "float32" else torch.complex128
     cd = torch.from_numpy(c).to(DEV)
     chunk = chunk or B
-    shape = (chunk, T, P) if store == _lib.STORE_ALL else (chunk, P)
+    pitch = pitch or P
+    shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
     paths = torch.empty(shape, dtype=tdt, device=DEV)
     rowsum = torch.empty((B, T), dtype=torch.float64, device=DEV)
     tg = torch.empty((B, N), dtype=cdt, device=DEV)
     _lib.check(_L().smc_train_targets(_lib.ptr(cd), B, T, N, M, 7, None, ordinal0, scheme | flags, normalize,
-                                      0 if dtype == "float32" else 1, store, _lib.ptr(paths), chunk,
+                                      0 if dtype == "float32" else 1, store, _lib.ptr(paths), pitch, chunk,
                                       _lib.ptr(rowsum) if with_rowsum else None, _lib.ptr(tg), None))
     torch.cuda.synchronize()
-    return tg.cpu().numpy(), rowsum.cpu().numpy(), paths
+    return tg.cpu().numpy(), rowsum.cpu().numpy(), paths[..., :P]
 
 
 @pytest.mark.parametrize("B,T,N,M,scheme,normalize,dtype", TARGET_CASES)
@@ -189,6 +191,20 @@ def test_store_modes_and_chunking_bit_identical(oracle, golden) -> None:
     # run-to-run determinism (fixed-order reductions, no atomics)
     e, _, _ = _run_targets(c, 16, 64, 8, 0, 1, "float32", _lib.STORE_ALL)
     np.testing.assert_array_equal(a, e)
+
+
+@pytest.mark.parametrize("store", [_lib.STORE_ALL, _lib.STORE_TERMINAL])
+def test_padded_row_pitch_bit_identical(oracle, golden, store) -> None:
+    """A padded scratch pitch (smc_path_pitch, or any multiple of 4 >= P) changes nothing."""
+    c = _contracts(oracle, golden, 9, seed=7)
+    P = 64 * 8
+    a, rs_a, pa = _run_targets(c, 20, 64, 8, 0, 1, "float32", store)
+    for pitch in (int(_L().smc_path_pitch(P, 0)), P + 4, P + 1024):
+        b, rs_b, pb = _run_targets(c, 20, 64, 8, 0, 1, "float32", store, chunk=4, pitch=pitch)
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(rs_a, rs_b)
+        if store == _lib.STORE_ALL:  # last chunk of 4 holds contracts 8.. of 9 in slot 0
+            torch.testing.assert_close(pb[0], pa[8], rtol=0, atol=0)
 
 
 def test_cf_targets_from_stored_paths_equal_fused(oracle, golden) -> None:

@@ -139,8 +139,14 @@ def test_multi_chunk_equals_single_chunk(monkeypatch) -> None:
 
     a, ma = _pricer(warmup=0)
     expect_success(a.train(make_training_config(num_batches=2, batch_size=20)))
-    monkeypatch.setattr(eng, "DEFAULT_PATH_BUFFER_BYTES", 3 * T * N * M * 4)  # 3 contracts per launch
+    from spectralmc_amd import _lib
+
+    pitch = int(_lib.lib().smc_path_pitch(N * M, _lib.DTYPE_F32))
+    monkeypatch.setattr(eng, "DEFAULT_PATH_BUFFER_BYTES", 3 * T * pitch * 4)  # 3 contracts per launch
     b, mb = _pricer(warmup=0)
+    sess = expect_success(b.open_session(make_training_config(num_batches=2, batch_size=20)))
+    assert sess.engine.chunk == 3  # 7 equal launches of <= 3 contracts
+    sess.close()
     expect_success(b.train(make_training_config(num_batches=2, batch_size=20)))
     assert max_param_diff(ma, mb) == 0.0
 

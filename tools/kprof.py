@@ -26,6 +26,7 @@ def main() -> None:
     ap.add_argument("--math", default="hw", choices=["hw", "portable"])
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--pitch", type=int, default=-1, help="row pitch (-1: smc_path_pitch, 0: P)")
     a = ap.parse_args()
     lo = np.array([0.001, 0.001, 0.0, -0.2, -0.2, 0.0])
     hi = np.array([1e4, 2e4, 10.0, 0.2, 0.2, 2.0])
@@ -34,13 +35,14 @@ def main() -> None:
     cd = torch.from_numpy(c).to(dev)
     P = a.N * a.M
     store = _lib.STORE_ALL if a.store == "all" else _lib.STORE_TERMINAL
-    paths = torch.empty((a.B, a.T, P) if store == _lib.STORE_ALL else (a.B, P), dtype=torch.float32, device=dev)
+    pitch = int(_lib.lib().smc_path_pitch(P, 0)) if a.pitch < 0 else (a.pitch or P)
+    paths = torch.empty((a.B, a.T, pitch) if store == _lib.STORE_ALL else (a.B, pitch), dtype=torch.float32, device=dev)
     tg = torch.empty((a.B, a.N), dtype=torch.complex64, device=dev)
     scheme = _lib.SCHEME_LOG_EULER | (_lib.MATH_HW if a.math == "hw" else 0)
     L = _lib.lib()
     def launch():
         _lib.check(L.smc_train_targets(_lib.ptr(cd), a.B, a.T, a.N, a.M, 7, None, 0, scheme, 1, 0, store,
-                                       _lib.ptr(paths), a.B, None, _lib.ptr(tg), None))
+                                       _lib.ptr(paths), pitch, a.B, None, _lib.ptr(tg), None))
 
     launch()
     torch.cuda.synchronize()
@@ -50,7 +52,8 @@ def main() -> None:
         launch()
     e1.record()
     torch.cuda.synchronize()
-    print(f"{os.environ.get('SMC_LIB_PATH', 'default')} {a.math} {a.store}: {e0.elapsed_time(e1) / a.iters:.3f} ms/launch",
+    print(f"{os.environ.get('SMC_LIB_PATH', 'default')} {a.math} {a.store} pitch={pitch}: "
+          f"{e0.elapsed_time(e1) / a.iters:.3f} ms/launch",
           "checksum", float(tg.abs().double().mean()))
 
 
