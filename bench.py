@@ -34,6 +34,10 @@ CONFIGS = {
     "c1": (64, 16, 256, 4, [32], "C1: 64 contracts x 1024 paths (N=256 x M=4), T=16, 2-layer CVNN 6->32->256 fp32"),
     "c2": (4096, 16, 256, 256, [32, 32],
            "C2: 4096 contracts x 65536 paths (N=256 x M=256), T=16, 3-layer CVNN 6->32->32->256 fp32"),
+    # BASELINE configs[2] shapes; the CVNN stays fp32 (the reference accepts full precision only,
+    # gbm_trainer.py:679-682); 275 GB of paths per step run as equal launches through the scratch
+    "c3": (16384, 16, 1024, 256, [32, 32],
+           "C3: 16384 contracts x 262144 paths (N=1024 x M=256), T=16, 3-layer CVNN 6->32->32->1024 fp32"),
 }
 
 

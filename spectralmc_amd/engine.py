@@ -93,6 +93,11 @@ class TrainingEngine:
         per_contract = (self.T * self.pitch if store_paths else self.pitch) * torch.finfo(sim_torch).bits // 8
         budget = path_buffer_bytes if path_buffer_bytes is not None else DEFAULT_PATH_BUFFER_BYTES
         max_chunk = max(1, min(B, budget // per_contract))
+        if max_chunk < B:
+            # several launches: whole rounds of resident contract workgroups (2 per CU)
+            slots = 2 * torch.cuda.get_device_properties(device).multi_processor_count
+            if max_chunk >= slots:
+                max_chunk -= max_chunk % slots
         launches = -(-B // max_chunk)
         self.chunk = -(-B // launches)  # equal launches: no small trailing launch
         shape = (self.chunk, self.T, self.pitch) if store_paths else (self.chunk, self.pitch)
