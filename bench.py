@@ -209,6 +209,32 @@ def main() -> None:
     live_ms = (sum(live) / len(live) / launches_per_call) if live else kernel_ms
     achieved = bytes_launch / (live_ms * 1e-3) / 1e9
 
+    # ---- network part alone (fused HIP kernels), HIP events on its own stream ------------
+    network = None
+    fused = session.program.fused
+    if fused is not None:
+        prog = session.program
+        widths_all = [6] + list(widths) + [N]
+        macs = sum(4 * a_ * b_ for a_, b_ in zip(widths_all[:-1], widths_all[1:]))  # complex = 4 real MACs
+        macs_bwd = macs + sum(4 * a_ * b_ for a_, b_ in zip(widths_all[1:-1], widths_all[2:]))
+        flops = 2.0 * (macs + macs_bwd) * B  # forward + weight grads + input grads (not layer 0)
+        with torch.cuda.stream(stream):
+            fused.fwd_bwd(prog.real_in[0], prog.imag_in, prog.targets[0])
+            n0, n1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            n0.record(stream)
+            for _ in range(args.kernel_iters):
+                fused.fwd_bwd(prog.real_in[0], prog.imag_in, prog.targets[0])
+                if not fused.fuse_adam:
+                    fused.adam()
+            n1.record(stream)
+        n1.synchronize()
+        net_ms = n0.elapsed_time(n1) / args.kernel_iters
+        network = {"kernels": "forward_backward + reduce/Adam + finalize (csrc/cvnn.hip), VALU f32",
+                   "flops_per_step": flops, "ms": net_ms, "achieved": flops / (net_ms * 1e-3) / 1e12,
+                   "peak": 157.3, "unit": "TFLOP/s", "frac": flops / (net_ms * 1e-3) / 1e12 / 157.3,
+                   "note": "latency-bound small complex GEMMs; runs on its own stream beside the next "
+                           "step's contract kernel, so it adds ~0 to ms_per_step"}
+
     # ---- measured HBM ceilings on this device (STREAM-style, 8 GiB buffers) --------------
     stream_gbs = {}
     if rank == 0:
@@ -267,6 +293,7 @@ def main() -> None:
                      "contracts_per_launch": contracts_per_launch,
                      "measured_stream_gbs": stream_gbs,
                      "frac_of_measured_write": (achieved / stream_gbs["write"]) if "write" in stream_gbs else None},
+        "network": network,
         "final_loss": final.loss,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

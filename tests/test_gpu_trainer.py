@@ -264,3 +264,25 @@ def test_fused_network_is_used_and_deterministic() -> None:
     sess.close()
     expect_success(b.train(cfg))
     assert max_param_diff(ma, mb) == 0.0
+
+
+def test_fused_network_wide_output_matches_torch_modules() -> None:
+    """N = 1024 outputs (C3 width): 2-row blocks, ragged last block, vs the torch modules."""
+    def make(fused: bool):
+        sp = make_simulation_params(timesteps=4, network_size=1024, batches_per_mc_run=2, mc_seed=3,
+                                    buffer_size=1, dtype=Precision.float32)
+        m = make_test_cvnn(n_inputs=6, n_outputs=1024, seed=17, dtype=torch.float32, hidden_layers=2)
+        cfg = make_gbm_cvnn_config(m, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                                   domain_bounds=make_domain_bounds())
+        p = expect_success(GbmCVNNPricer.create(cfg))
+        p.fused_network = fused
+        return p, m
+
+    a, ma = make(True)
+    b, mb = make(False)
+    cfg = make_training_config(num_batches=2, batch_size=21)
+    ra = expect_success(a.train(cfg))
+    rb = expect_success(b.train(cfg))
+    assert ra.final_loss == pytest.approx(rb.final_loss, rel=1e-4)
+    assert ra.final_grad_norm == pytest.approx(rb.final_grad_norm, rel=1e-3)
+    assert max_param_diff(ma, mb) < 3e-4
