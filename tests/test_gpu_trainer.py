@@ -286,3 +286,37 @@ def test_fused_network_wide_output_matches_torch_modules() -> None:
     assert ra.final_loss == pytest.approx(rb.final_loss, rel=1e-4)
     assert ra.final_grad_norm == pytest.approx(rb.final_grad_norm, rel=1e-3)
     assert max_param_diff(ma, mb) < 3e-4
+
+
+def test_batchnorm_residual_model_trains_on_torch_path(oracle) -> None:
+    """Architectures outside the fused kernels (batch norm, residual) keep the torch-ROCm
+    network path and still match the oracle's torch-cpu step."""
+    from spectralmc_amd.cvnn_factory import (ActivationCfg, ActivationKind, CovBNCfg, ExplicitWidth, LinearCfg,
+                                             ResidualCfg, SequentialCfg, build_cvnn_config, build_model)
+    from spectralmc_amd.models.torch import FullPrecisionDType
+
+    layers = [LinearCfg(width=ExplicitWidth(value=16), activation=ActivationCfg(kind=ActivationKind.MOD_RELU)),
+              CovBNCfg(),
+              ResidualCfg(body=SequentialCfg(layers=[LinearCfg(width=ExplicitWidth(value=16),
+                                                               activation=ActivationCfg(kind=ActivationKind.Z_RELU))])),
+              LinearCfg(width=ExplicitWidth(value=N))]
+    cfg = expect_success(build_cvnn_config(dtype=FullPrecisionDType.float32, layers=layers, seed=5))
+    model = expect_success(build_model(n_inputs=6, n_outputs=N, cfg=cfg))
+    cpu_model = copy.deepcopy(model)
+    model = model.to("cuda")
+    sp = _sim()
+    pcfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                                domain_bounds=make_domain_bounds())
+    pricer = expect_success(GbmCVNNPricer.create(pcfg))
+    pricer.warmup_steps = 0
+    sess = expect_success(pricer.open_session(make_training_config(num_batches=1, batch_size=16)))
+    assert sess.program.fused is None
+    sess.close()
+    res = expect_success(pricer.train(make_training_config(num_batches=1, batch_size=16, learning_rate=1e-2)))
+    lo, hi = make_domain_bounds().arrays()
+    contracts = oracle.sobol_contracts(7, 0, 16, lo, hi)
+    targets = oracle.training_targets(contracts, T, N, M, seed=7)
+    x = torch.tensor(contracts, dtype=torch.float32)
+    ref = oracle.torch_step(cpu_model, x, torch.zeros_like(x), torch.from_numpy(targets),
+                            torch.optim.Adam(cpu_model.parameters(), lr=1e-2))
+    assert res.final_loss == pytest.approx(ref.loss, rel=1e-4)
