@@ -187,10 +187,7 @@ def main() -> None:
         b = eng.buffers
 
         def run_kernel() -> None:
-            _lib.check(L.smc_train_targets(_lib.ptr(b.contracts), eng.B, eng.T, eng.N, eng.M, eng.seed, None, 0,
-                                           eng._scheme, eng._norm, eng._dtype_code, eng.store_mode,
-                                           _lib.ptr(eng._paths_buf), eng.pitch, eng.chunk, None,
-                                           _lib.ptr(b.targets), _lib.stream_handle(stream)))
+            eng.launch_targets(_lib.stream_handle(stream), None, 0)
 
         run_kernel()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

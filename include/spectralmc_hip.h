@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 3
+#define SMC_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -116,13 +116,23 @@ int32_t smc_cf_targets(const double* contracts_dev, int64_t n_contracts, int32_t
  * holds `chunk_contracts` contracts ([chunk][T][pitch]) and is reused chunk by chunk;
  * SMC_STORE_TERMINAL needs paths_dev of [chunk][pitch].  path_pitch: elements between
  * consecutive path rows (0 = P, contiguous; else a multiple of 4 >= P, e.g. smc_path_pitch).
- * targets_dev: [B][N] complex. */
+ * targets_dev: [B][N] complex.
+ * workspace_dev (may be NULL): smc_engine_workspace_bytes(chunk, T, P, rowsum_dev != NULL)
+ * bytes, zero-filled once before first use (the kernel leaves it zeroed).  With a workspace
+ * each contract is simulated by several workgroups (slices of 8192 paths) and the last one
+ * to finish runs the payoff/DFT phase; without it one workgroup runs the whole contract.
+ * Results are bit-identical run to run either way; the two differ only in the f64 row-sum
+ * association (oracle/gbm_oracle.c restates both). */
 int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int32_t timesteps,
                           int32_t network_size, int32_t batches_per_mc_run, uint64_t mc_seed,
                           const int64_t* ordinal_dev, int64_t ordinal0, int32_t scheme,
                           int32_t normalization, int32_t dtype, int32_t store_mode,
                           void* paths_dev, int64_t path_pitch, int64_t chunk_contracts,
-                          double* rowsum_dev, void* targets_dev, void* stream);
+                          double* rowsum_dev, void* targets_dev, void* workspace_dev,
+                          int64_t workspace_bytes, void* stream);
+/* Workspace bytes smc_train_targets needs for sliced contracts (0: P too small to slice). */
+int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, int64_t n_paths,
+                                   int32_t all_rows);
 /* Recommended row pitch (elements) for a path scratch buffer of n_paths columns: the row
  * stride becomes an odd multiple of 4 KiB (power-of-two strides alias in HBM). */
 int64_t smc_path_pitch(int64_t n_paths, int32_t dtype);

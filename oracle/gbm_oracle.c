@@ -343,9 +343,12 @@ int32_t oracle_num_threads(void) {
 #define K_CHUNK (K_THREADS * K_PPL)
 #define K_WAVES (K_THREADS / 64)
 
-/* paths: [B][T][P] (optional), terminal [B][P] (optional), rowsum [B][T] (required) */
+/* paths: [B][T][P] (optional), terminal [B][P] (optional), rowsum [B][T] (required).
+ * slice_paths: 0 = one workgroup per contract; else the contract's paths are cut into slices of
+ * that many paths (gbm.hip kSliceChunks * kChunk = 8192 when smc_train_targets gets a workspace),
+ * each reduced like a whole contract, and the slice sums are added in slice order from 0.0. */
 void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t P, uint64_t seed, int64_t ordinal0,
-                         int32_t scheme, float* paths, float* terminal, double* rowsum) {
+                         int32_t scheme, int64_t slice_paths, float* paths, float* terminal, double* rowsum) {
   const double kLog2e = 1.4426950408889634;
   float* X = (float*)malloc(sizeof(float) * (size_t)T * (size_t)P);
   double* lane_acc = (double*)malloc(sizeof(double) * (size_t)K_THREADS * (size_t)T);
@@ -389,29 +392,36 @@ void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t 
     }
     if (paths) memcpy(paths + b * (int64_t)T * P, X, sizeof(float) * (size_t)T * (size_t)P);
     if (terminal) memcpy(terminal + b * P, X + (int64_t)(T - 1) * P, sizeof(float) * (size_t)P);
-    /* per lane: sequential over chunks of f32 4-path partial sums, accumulated in f64 */
-    memset(lane_acc, 0, sizeof(double) * (size_t)K_THREADS * (size_t)T);
-    for (int64_t chunk = 0; chunk < P; chunk += K_CHUNK)
-      for (int lane = 0; lane < K_THREADS; ++lane) {
-        const int64_t p0 = chunk + (int64_t)K_PPL * lane;
-        for (int t = 0; t < T; ++t) {
-          float part = 0.0f;
-          for (int j = 0; j < K_PPL; ++j) part += (p0 + j < P) ? X[(int64_t)t * P + p0 + j] : 0.0f;
-          lane_acc[(size_t)lane * T + t] += (double)part;
+    const int64_t span = slice_paths > 0 && slice_paths < P ? slice_paths : P;
+    const int sliced = span < P;
+    for (int t = 0; t < T; ++t) rowsum[b * T + t] = 0.0;
+    for (int64_t p_begin = 0; p_begin < P; p_begin += span) {
+      const int64_t p_end = p_begin + span < P ? p_begin + span : P;
+      /* per lane: sequential over the slice's chunks of f32 4-path partial sums, in f64 */
+      memset(lane_acc, 0, sizeof(double) * (size_t)K_THREADS * (size_t)T);
+      for (int64_t chunk = p_begin; chunk < p_end; chunk += K_CHUNK)
+        for (int lane = 0; lane < K_THREADS; ++lane) {
+          const int64_t p0 = chunk + (int64_t)K_PPL * lane;
+          for (int t = 0; t < T; ++t) {
+            float part = 0.0f;
+            for (int j = 0; j < K_PPL; ++j) part += (p0 + j < p_end) ? X[(int64_t)t * P + p0 + j] : 0.0f;
+            lane_acc[(size_t)lane * T + t] += (double)part;
+          }
         }
-      }
-    for (int t = 0; t < T; ++t) {
-      double tot = 0.0;
-      for (int w = 0; w < K_WAVES; ++w) {
-        double v[64], nv[64];
-        for (int l = 0; l < 64; ++l) v[l] = lane_acc[(size_t)(64 * w + l) * T + t];
-        for (int off = 32; off >= 1; off >>= 1) {
-          for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
-          memcpy(v, nv, sizeof(v));
+      for (int t = 0; t < T; ++t) {
+        double tot = 0.0;
+        for (int w = 0; w < K_WAVES; ++w) {
+          double v[64], nv[64];
+          for (int l = 0; l < 64; ++l) v[l] = lane_acc[(size_t)(64 * w + l) * T + t];
+          for (int off = 32; off >= 1; off >>= 1) {
+            for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+            memcpy(v, nv, sizeof(v));
+          }
+          tot += v[0];
         }
-        tot += v[0];
+        if (sliced) rowsum[b * T + t] += tot; /* last arriver: slices 0..W-1 in order from 0.0 */
+        else rowsum[b * T + t] = tot;
       }
-      rowsum[b * T + t] = tot;
     }
   }
   free(lane_acc);
@@ -422,7 +432,10 @@ void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t 
 void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, int32_t normalize,
                       const float* terminal, const double* terminal_sum, float* targets) {
   const int64_t P = (int64_t)N * M;
-  const int G = N <= K_THREADS ? K_THREADS / N : 1;
+  /* gbm.hip cf_targets_contract: with N % 4 == 0 a thread owns 4 adjacent columns (16-B loads),
+   * so the m-groups per column are counted over N/4 column quads */
+  const int cols = (N % 4 == 0 && P < ((int64_t)1 << 29)) ? N / 4 : N;
+  const int G = cols <= K_THREADS ? K_THREADS / cols : 1;
   const int items = N * G;
   double* part = (double*)malloc(sizeof(double) * (size_t)items);
   double* avg = (double*)malloc(sizeof(double) * (size_t)N);

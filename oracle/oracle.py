@@ -60,8 +60,8 @@ def lib() -> ctypes.CDLL:
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
         L.oracle_num_threads.restype = ctypes.c_int32
         L.oracle_kernel_paths.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
-                                          ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
-                                          ctypes.c_void_p, ctypes.c_void_p]
+                                          ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_kernel_cf.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_log_pos.argtypes = [ctypes.c_float]
@@ -184,16 +184,22 @@ def training_targets(contracts: np.ndarray, timesteps: int, network_size: int, b
 
 
 # --------------------------------------------------------------------------- kernel mode
+# paths per workgroup slice when smc_train_targets gets a workspace (gbm.hip kSliceChunks * kChunk)
+SLICE_PATHS = 8192
+
+
 def kernel_paths(contracts: np.ndarray, timesteps: int, n_paths: int, seed: int, ordinal0: int = 0,
-                 scheme: int = 0, want_paths: bool = False) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
-    """f32 KERNEL mode: exact restatement of the HIP engine (paths, terminal, rowsum in its order)."""
+                 scheme: int = 0, want_paths: bool = False,
+                 sliced: bool = False) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
+    """f32 KERNEL mode: exact restatement of the HIP engine (paths, terminal, rowsum in its order).
+    sliced: row sums in the sliced-contract order (engine with a workspace)."""
     contracts = np.ascontiguousarray(contracts, dtype=np.float64)
     B = contracts.shape[0]
     paths = np.empty((B, timesteps, n_paths), dtype=np.float32) if want_paths else None
     terminal = np.empty((B, n_paths), dtype=np.float32)
     rowsum = np.empty((B, timesteps), dtype=np.float64)
-    lib().oracle_kernel_paths(_ptr(contracts), B, timesteps, n_paths, seed, ordinal0, scheme, _ptr(paths),
-                              _ptr(terminal), _ptr(rowsum))
+    lib().oracle_kernel_paths(_ptr(contracts), B, timesteps, n_paths, seed, ordinal0, scheme,
+                              SLICE_PATHS if sliced else 0, _ptr(paths), _ptr(terminal), _ptr(rowsum))
     return paths, terminal, rowsum
 
 
@@ -209,9 +215,11 @@ def kernel_cf(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndar
 
 
 def kernel_targets(contracts: np.ndarray, timesteps: int, network_size: int, batches: int, seed: int,
-                   ordinal0: int = 0, scheme: int = 0, normalize: bool = True) -> tuple[np.ndarray, np.ndarray]:
+                   ordinal0: int = 0, scheme: int = 0, normalize: bool = True,
+                   sliced: bool = False) -> tuple[np.ndarray, np.ndarray]:
     """(targets [B,N] complex64, rowsum [B,T]) exactly as the f32 HIP engine computes them."""
-    _, terminal, rowsum = kernel_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme)
+    _, terminal, rowsum = kernel_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme,
+                                       sliced=sliced)
     return kernel_cf(contracts, terminal, rowsum[:, -1], network_size, batches, normalize), rowsum
 
 

@@ -34,7 +34,7 @@ STORE_TERMINAL = 1
 MATH_HW = 0x100
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 
@@ -55,7 +55,9 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_cf_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_vp, _c_vp, _c_vp,
                                 _c_vp]),
     "smc_train_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_u64, _c_vp, _c_i64, _c_i32,
-                                   _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
+                                   _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64,
+                                   _c_vp]),
+    "smc_engine_workspace_bytes": (_c_i64, [_c_i64, _c_i32, _c_i64, _c_i32]),
     "smc_path_pitch": (_c_i64, [_c_i64, _c_i32]),
     "smc_normals": (_c_i32, [_c_u64, _c_i64, _c_i32, _c_i64, _c_i32, _c_vp, _c_vp]),
     "smc_cvnn_plan": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64)]),

@@ -38,6 +38,9 @@ namespace {
 #ifndef SMC_MIN_LDS
 #define SMC_MIN_LDS 0
 #endif
+#ifndef SMC_MIN_BLOCKS
+#define SMC_MIN_BLOCKS 1
+#endif
 constexpr int kThreads = SMC_WG_THREADS;
 constexpr int kWaves = kThreads / 64;
 constexpr int kPathsPerLane = 4;
@@ -67,7 +70,48 @@ struct EngineArgs {
   double* rowsum;             // [B][T] or NULL
   void* targets;              // [B][N] complex or NULL
   int64_t pitch;              // elements between consecutive path rows (0: P, contiguous)
+  int32_t slices;             // workgroups per contract (>= 1); > 1 needs the workspace below
+  double* partials;           // [B][slices][all_rows ? T : 1] slice row sums (slices > 1)
+  uint32_t* arrivals;         // [B] arrival counters, zero between launches (slices > 1)
+  uint32_t* queues;           // [16] queue_kernel work counters, zero between launches (slices > 1)
 };
+
+#ifndef SMC_SLICE_CHUNKS
+#define SMC_SLICE_CHUNKS 4
+#endif
+constexpr int kSliceChunks = SMC_SLICE_CHUNKS;  // chunks (of kChunk paths) per workgroup when sliced
+
+
+// Stores / loads of bytes handed from one workgroup to another (possibly on another XCD):
+// write-through (sc1) 16-B stores drained before the arrival add, sc1 loads after it
+// (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms).
+// 16-B write-through stores through a buffer descriptor on the wave-uniform row base: the
+// compiler counts them in vmcnt and pads their data hazards.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row_base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row_base), static_cast<short>(0), 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ void store_wt(const void* row_base, uint32_t off, float4 v) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, row_rsrc(row_base), off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ void store_wt(const void* row_base, uint32_t off, double4 v) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  const v2d lo = {v.x, v.y}, hi = {v.z, v.w};
+  const __amdgpu_buffer_rsrc_t r = row_rsrc(row_base);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, lo), r, off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, hi), r, off + 16, 0, 16);
+}
+template <typename U>
+__device__ __forceinline__ void put_sc1(U* p, U v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename U>
+__device__ __forceinline__ U get_sc1(const U* p) {
+  return __hip_atomic_load(const_cast<U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 template <typename Real>
 struct Vec4T;
@@ -204,18 +248,25 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
       }
       if (store_all || t == T - 1) {
         char* row = reinterpret_cast<char*>(chunk_base + (store_all ? static_cast<int64_t>(t) * pitch : 0));
+        // the terminal row is read back by the CF phase (maybe another workgroup's): write-through
+        const bool handoff = t == T - 1 && a.targets != nullptr;
         if constexpr (!MASKED) {
           V4 v4;
           v4.x = x[0];
           v4.y = x[1];
           v4.z = x[2];
           v4.w = x[3];
-          *reinterpret_cast<V4*>(row + lane_off) = v4;
+          if (handoff) store_wt(row, lane_off, v4);
+          else *reinterpret_cast<V4*>(row + lane_off) = v4;
         } else {
           Real* r = reinterpret_cast<Real*>(row + lane_off);
 #pragma unroll
-          for (int j = 0; j < kPathsPerLane; ++j)
-            if (j < nvalid) r[j] = x[j];
+          for (int j = 0; j < kPathsPerLane; ++j) {
+            if (j < nvalid) {
+              if (handoff) put_sc1(r + j, x[j]);
+              else r[j] = x[j];
+            }
+          }
         }
       }
       if (ALLROWS || t == T - 1) {
@@ -234,7 +285,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
 // waves 0..7.  Training needs only the terminal row's sum (its normalisation scale).
 template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
 __device__ void simulate_contract(const EngineArgs& a, const Contract& c, uint64_t ordinal, int64_t b,
-                                  double* lds_acc, double* lds_tot) {
+                                  int64_t p_begin, int64_t p_end, double* lds_acc, double* lds_tot) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = a.T;
   const int64_t P = a.P;
@@ -242,7 +293,7 @@ __device__ void simulate_contract(const EngineArgs& a, const Contract& c, uint64
   const int64_t pitch = a.pitch ? a.pitch : P;
   Real* base = static_cast<Real*>(a.paths) + (store_all ? b * T * pitch : b * pitch);
   const bool vec_ok = (P % kPathsPerLane) == 0;
-  const int64_t full_end = vec_ok ? (P / kChunk) * kChunk : 0;
+  const int64_t full_end = vec_ok ? p_begin + ((p_end - p_begin) / kChunk) * kChunk : p_begin;
   const Stepper<Real, LOG_EULER, HW> step(c, T);
   const Real x0 = static_cast<Real>(c.X0);
   constexpr int kAcc = ALLROWS ? kRowBlock : 1;
@@ -252,15 +303,15 @@ __device__ void simulate_contract(const EngineArgs& a, const Contract& c, uint64
     double acc[kAcc];
 #pragma unroll
     for (int i = 0; i < kAcc; ++i) acc[i] = 0.0;
-    int64_t chunk = 0;
+    int64_t chunk = p_begin;
     if (nrows == kRowBlock) {  // branch-free fast path: whole 16-row block, whole 2048-path chunks
       for (; chunk < full_end; chunk += kChunk)
         lane_paths<Real, LOG_EULER, HW, ALLROWS, false, true>(a, step, x0, ordinal, chunk, kPathsPerLane, t0, nrows,
                                                               base, acc);
     }
-    for (; chunk < P; chunk += kChunk) {  // everything else: ragged rows / paths, scalar stores
+    for (; chunk < p_end; chunk += kChunk) {  // everything else: ragged rows / paths, scalar stores
       const int64_t p0 = chunk + kPathsPerLane * tid;
-      const int nvalid = static_cast<int>(p0 >= P ? 0 : (P - p0 >= kPathsPerLane ? kPathsPerLane : P - p0));
+      const int nvalid = static_cast<int>(p0 >= p_end ? 0 : (p_end - p0 >= kPathsPerLane ? kPathsPerLane : p_end - p0));
       lane_paths<Real, LOG_EULER, HW, ALLROWS, true, false>(a, step, x0, ordinal, chunk, nvalid, t0, nrows, base,
                                                             acc);
     }
@@ -285,70 +336,39 @@ __device__ void simulate_contract(const EngineArgs& a, const Contract& c, uint64
 }
 
 // ---- phases 2+3: normalised put payoff, mean over M batches, real-input DFT ------------
+// Reference scalar semantics: gbm.py:429-431 evaluate times/forwards/df in the sim dtype;
+// the put is df * max(K - x * scale, 0) with x * scale rounded to the sim dtype (gbm.py:437, 473).
 template <typename Real>
-__device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int64_t b,
-                                    double terminal_sum, double* lds) {
-  using C2 = typename Complex2<Real>::type;
-  const int tid = threadIdx.x;
-  const int T = a.T, N = a.N, M = a.M;
-  const int64_t P = a.P;
-  const bool store_all = a.store == SMC_STORE_ALL;
-  const int64_t pitch = a.pitch ? a.pitch : P;
-  const Real* row = static_cast<const Real*>(a.paths) + (store_all ? (b * T + (T - 1)) * pitch : b * pitch);
-
-  // Reference scalar semantics: gbm.py:429-431 evaluate times/forwards/df in the sim dtype.
-  Real F, df;
-  const Real Tm = static_cast<Real>(c.T);
-  if constexpr (sizeof(Real) == 4) {
-    F = static_cast<float>(c.X0) * math::exp_any(static_cast<float>(c.r - c.d) * Tm);
-    df = math::exp_any(static_cast<float>(-c.r) * Tm);
-  } else {
-    F = c.X0 * exp((c.r - c.d) * Tm);
-    df = exp(-c.r * Tm);
-  }
-  const Real s = a.normalize ? F / static_cast<Real>(terminal_sum / static_cast<double>(P)) : Real(1);
-  const Real K = static_cast<Real>(c.K);
-
-  const int G = N <= kThreads ? kThreads / N : 1;
-  const int items = N * G;
-  double* part = lds;                                  // [max(kThreads, N)]
-  double* avg = part + (N > kThreads ? N : kThreads);  // [N]
-  double* cs = avg + N;                                // [N]
-  double* sn = cs + N;                                 // [N]
-
-  constexpr int kBatch = 16;  // loads in flight per thread; the sum keeps the m order
-  for (int item = tid; item < items; item += kThreads) {
-    const int n = item % N, g = item / N;
-    double sum = 0.0;
-    for (int m0 = g; m0 < M; m0 += G * kBatch) {
-      Real v[kBatch];
-#pragma unroll
-      for (int u = 0; u < kBatch; ++u) {
-        const int m = m0 + u * G < M ? m0 + u * G : M - 1;  // clamped: loads stay unconditional
-        v[u] = row[static_cast<int64_t>(m) * N + n];
-      }
-#pragma unroll
-      for (int u = 0; u < kBatch; ++u) {
-        if (m0 + u * G < M) {
-          const Real xs = v[u] * s;  // sims *= scale (rounded to Real)
-          const Real diff = K - xs;
-          const Real pay = df * (diff > Real(0) ? diff : Real(0));
-          sum += static_cast<double>(pay);
-        }
-      }
+struct Payoff {
+  Real s, K, df;
+  Payoff() = default;
+  __device__ Payoff(const EngineArgs& a, const Contract& c, double terminal_sum) {
+    Real F;
+    const Real Tm = static_cast<Real>(c.T);
+    if constexpr (sizeof(Real) == 4) {
+      F = static_cast<float>(c.X0) * math::exp_any(static_cast<float>(c.r - c.d) * Tm);
+      df = math::exp_any(static_cast<float>(-c.r) * Tm);
+    } else {
+      F = c.X0 * exp((c.r - c.d) * Tm);
+      df = exp(-c.r * Tm);
     }
-    part[item] = sum;
+    s = a.normalize ? F / static_cast<Real>(terminal_sum / static_cast<double>(a.P)) : Real(1);
+    K = static_cast<Real>(c.K);
   }
-  for (int j = tid; j < N; j += kThreads) math::twiddle(j, N, sn[j], cs[j]);
-  __syncthreads();
-  for (int n = tid; n < N; n += kThreads) {
-    double tot = 0.0;
-    for (int g = 0; g < G; ++g) tot += part[g * N + n];
-    avg[n] = tot / static_cast<double>(M);
+  __device__ __forceinline__ Real operator()(Real x) const {
+    const Real xs = x * s;  // sims *= scale (rounded to Real)
+    const Real diff = K - xs;
+    return df * (diff > Real(0) ? diff : Real(0));
   }
-  __syncthreads();
-  C2* out = static_cast<C2*>(a.targets) + b * N;
-  for (int k = tid; k <= N / 2; k += kThreads) {
+};
+
+// Real-input N-point DFT of avg[0..N) from the twiddle table -> targets row (bins 0..N/2 and
+// their Hermitian mirror); fixed summation order.
+template <typename Real>
+__device__ void dft_row(const double* avg, const double* cs, const double* sn, int N,
+                        typename Complex2<Real>::type* out) {
+  using C2 = typename Complex2<Real>::type;
+  for (int k = threadIdx.x; k <= N / 2; k += kThreads) {
     double re = 0.0, im = 0.0;
     int idx = 0;
     for (int n = 0; n < N; ++n) {
@@ -368,10 +388,98 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
   }
 }
 
+template <typename Real>
+__device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int64_t b,
+                                    double terminal_sum, double* lds) {
+  using C2 = typename Complex2<Real>::type;
+  const int tid = threadIdx.x;
+  const int T = a.T, N = a.N, M = a.M;
+  const int64_t P = a.P;
+  const bool store_all = a.store == SMC_STORE_ALL;
+  const int64_t pitch = a.pitch ? a.pitch : P;
+  const Real* row = static_cast<const Real*>(a.paths) + (store_all ? (b * T + (T - 1)) * pitch : b * pitch);
+  const Payoff<Real> pay(a, c, terminal_sum);
+
+  // f32 rows of N % 4 == 0 columns: each thread sums 4 adjacent columns from 16-B loads
+  // (256 B in flight per lane, 128 KiB per workgroup); otherwise one column per thread.
+  // Column n's batches m = g, g + G, ... are summed by one thread (group g), then the G
+  // group sums in g order.
+  const bool quad = sizeof(Real) == 4 && (N % 4) == 0 && (pitch % 4) == 0 && P < (int64_t{1} << 29);
+  const int cols = quad ? N / 4 : N;
+  const int G = cols <= kThreads ? kThreads / cols : 1;
+  const int items = cols * G;
+  double* part = lds;                                            // [max(4 kThreads, N)]
+  double* avg = part + (N > 4 * kThreads ? N : 4 * kThreads);    // [N]
+  double* cs = avg + N;                                          // [N]
+  double* sn = cs + N;                                           // [N]
+
+  constexpr int kBatch = 16;  // loads in flight per thread; the sum keeps the m order
+  if constexpr (sizeof(Real) == 4) {
+    if (quad) {
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      // sc1 (L1-bypassing) 16-B loads: the row was written by this contract's slices (sc1 stores)
+      const __amdgpu_buffer_rsrc_t rsrc =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<Real*>(row), static_cast<short>(0), 0x7fffffff, 0x00020000);
+      for (int item = tid; item < items; item += kThreads) {
+        const int q = item % cols, g = item / cols;
+        double sum[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int m0 = g; m0 < M; m0 += G * kBatch) {
+          v4f v[kBatch];
+#pragma unroll
+          for (int u = 0; u < kBatch; ++u) {
+            const int m = m0 + u * G < M ? m0 + u * G : M - 1;  // clamped: loads stay unconditional
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (m * N + 4 * q) * 4, 0, 16 /* sc1 */);
+          }
+#pragma unroll
+          for (int u = 0; u < kBatch; ++u) {
+            if (m0 + u * G < M) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) sum[e] += static_cast<double>(pay(v[u][e]));
+            }
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) part[g * N + 4 * q + e] = sum[e];
+      }
+    }
+  }
+  for (int item = tid; item < items && !quad; item += kThreads) {
+    const int n = item % N, g = item / N;
+    double sum = 0.0;
+    for (int m0 = g; m0 < M; m0 += G * kBatch) {
+      Real v[kBatch];
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        const int m = m0 + u * G < M ? m0 + u * G : M - 1;  // clamped: loads stay unconditional
+        v[u] = get_sc1(row + static_cast<int64_t>(m) * N + n);  // written by the slices' sc1 stores
+      }
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u)
+        if (m0 + u * G < M) sum += static_cast<double>(pay(v[u]));
+    }
+    part[item] = sum;
+  }
+  for (int j = tid; j < N; j += kThreads) math::twiddle(j, N, sn[j], cs[j]);
+  __syncthreads();
+  for (int n = tid; n < N; n += kThreads) {
+    double tot = 0.0;
+    for (int g = 0; g < G; ++g) tot += part[g * N + n];
+    avg[n] = tot / static_cast<double>(M);
+  }
+  __syncthreads();
+  dft_row<Real>(avg, cs, sn, N, static_cast<C2*>(a.targets) + b * N);
+}
+
+// Slice k of contract b (paths [k S, (k+1) S), S = kSliceChunks * kChunk; the whole contract
+// when slices == 1), then — for the workgroup that completes the contract — the CF phase.
+// With slices > 1 every slice publishes its row sums (write-through) and arrives on the
+// contract's counter; the last arriver sums the W slice sums in slice order 0..W-1 (a fixed
+// order: bit-reproducible, oracle "sliced" mode) and runs the CF phase on the terminal row,
+// which the slices wrote moments ago (write-through stores drained before arriving, L1-bypassing
+// loads after: MI355X_MICROARCH.md, inter-workgroup visibility, valid forms).
 template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
-__global__ __launch_bounds__(kThreads) void contract_kernel(EngineArgs a) {
-  extern __shared__ double lds[];
-  const int64_t b = blockIdx.x;
+__device__ void run_slice(const EngineArgs& a, int64_t b, int k, double* lds, int* lds_flag) {
+  const int W = a.slices;
   const Contract c = load_contract(a.contracts + b * 6);
   const int T = a.T;
   double* lds_tot = lds;               // [T]
@@ -379,7 +487,32 @@ __global__ __launch_bounds__(kThreads) void contract_kernel(EngineArgs a) {
   double terminal_sum;
   if (a.simulate) {
     const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
-    simulate_contract<Real, LOG_EULER, HW, ALLROWS>(a, c, ordinal, b, lds_work, lds_tot);
+    const int64_t span = W == 1 ? a.P : static_cast<int64_t>(kSliceChunks) * kChunk;
+    const int64_t p_begin = k * span;
+    const int64_t p_end = p_begin + span < a.P ? p_begin + span : a.P;
+    simulate_contract<Real, LOG_EULER, HW, ALLROWS>(a, c, ordinal, b, p_begin, p_end, lds_work, lds_tot);
+    if (W > 1) {
+      // publish this slice's row sums, drain every wave's write-through stores, then arrive
+      const int rows = ALLROWS ? T : 1;
+      double* mine = a.partials + (b * W + k) * rows;
+      for (int t = threadIdx.x; t < rows; t += kThreads) put_sc1(mine + t, lds_tot[ALLROWS ? t : T - 1]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint32_t before = __hip_atomic_fetch_add(a.arrivals + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lds_flag = before == static_cast<uint32_t>(W - 1);
+        if (*lds_flag) __hip_atomic_store(a.arrivals + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (!*lds_flag) return;
+      const double* all = a.partials + b * W * rows;
+      for (int t = threadIdx.x; t < rows; t += kThreads) {
+        double tot = 0.0;
+        for (int j = 0; j < W; ++j) tot += get_sc1(all + j * rows + t);
+        lds_tot[ALLROWS ? t : T - 1] = tot;
+      }
+      __syncthreads();
+    }
     if (ALLROWS && a.rowsum)
       for (int t = threadIdx.x; t < T; t += kThreads) a.rowsum[b * T + t] = lds_tot[t];
     terminal_sum = lds_tot[T - 1];
@@ -392,8 +525,171 @@ __global__ __launch_bounds__(kThreads) void contract_kernel(EngineArgs a) {
 #else
   if (a.targets) {
 #endif
-    __syncthreads();  // workgroup-scope fence: phase-1 stores of the terminal row are visible
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's own terminal-row stores
+    __syncthreads();
     cf_targets_contract<Real>(a, c, b, terminal_sum, lds_work);
+  }
+  __syncthreads();  // LDS is reused by the workgroup's next item
+}
+
+// One workgroup per contract (slices == 1).
+template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
+__global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void contract_kernel(EngineArgs a) {
+  extern __shared__ double lds[];
+  __shared__ int flag;
+  run_slice<Real, LOG_EULER, HW, ALLROWS>(a, blockIdx.x, 0, lds, &flag);
+}
+
+// Sliced contracts on persistent workgroups.  Contract b belongs to queue b mod 8; a workgroup
+// takes items (slice k of a contract) from the queue of the XCD it runs on (s_getreg XCC_ID), so
+// the slices of a contract run side by side on one XCD, finish within a few tens of microseconds
+// of each other, and the last one's CF re-read finds the terminal row still on chip.  Placement
+// is for speed only: the hand-off protocol is cross-XCD safe, and the last workgroup to leave
+// runs whatever is left in any queue (an XCD without workgroups) before resetting the counters.
+// queues[0..7]: next item per queue, queues[8]: workgroups done; all zero between launches.
+template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
+__global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void queue_kernel(EngineArgs a) {
+  extern __shared__ double lds[];
+  __shared__ int flag;
+  __shared__ int64_t next_item;
+  const int W = a.slices;
+  uint32_t* queues = a.queues;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  auto queue_items = [&](int x) -> int64_t { return x < a.B ? ((a.B - 1 - x) / 8 + 1) * W : 0; };
+  auto drain_queue = [&](int x) {
+    const int64_t n = queue_items(x);
+    for (;;) {
+      if (threadIdx.x == 0)
+        next_item = __hip_atomic_fetch_add(queues + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int64_t j = next_item;
+      __syncthreads();
+      if (j >= n) break;
+      run_slice<Real, LOG_EULER, HW, ALLROWS>(a, x + 8 * (j / W), static_cast<int>(j % W), lds, &flag);
+    }
+  };
+  drain_queue(static_cast<int>(xcc & 7));
+  if (threadIdx.x == 0)
+    flag = __hip_atomic_fetch_add(queues + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (flag) {  // every other workgroup has left: finish orphaned queues, reset for the next launch
+    for (int x = 0; x < 8; ++x) drain_queue(x);
+    if (threadIdx.x < 9) __hip_atomic_store(queues + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---- training fast path: persistent workgroups, CF phase pipelined into the next contract ----
+// Conditions (pipelined_ok): f32, T <= kRowBlock, P a multiple of kChunk, N a power of two
+// dividing kChunk (N >= 4), terminal-row sums only, targets requested, no slices.
+// Each of the gridDim.x resident workgroups runs contracts b = blockIdx.x, + gridDim.x, ...
+// While it simulates contract b, chunk by chunk, every thread re-reads its OWN 16-B terminal
+// store of the same chunk of the previous contract (same thread, same address: program order,
+// no fence) and adds the put payoffs to 4 column sums; the loads are issued before the chunk's
+// compute and consumed after it, so their latency (long behind the write stream) is hidden
+// and no workgroup ever drains its stores.  Thread tid owns columns 4q..4q+3 (q = tid mod N/4)
+// and batches m = g, g + G, ... (g = tid div N/4, G = kChunk / N) — exactly the quad order of
+// cf_targets_contract, so targets are bit-identical to the unpipelined kernel.
+__device__ __forceinline__ void lds_barrier() {  // LDS-only: no vmcnt drain of the path stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <bool LOG_EULER, bool HW>
+__global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void pipelined_kernel(EngineArgs a) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = a.T, N = a.N, M = a.M;
+  const int64_t P = a.P;
+  const bool store_all = a.store == SMC_STORE_ALL;
+  const int64_t pitch = a.pitch ? a.pitch : P;
+  const int G = kChunk / N;  // batches per chunk
+  const int Q = N / 4;
+  const int q = tid % Q, g = tid / Q;
+  double* lds_acc = lds;                // [kWaves]
+  double* part = lds + kWaves;          // [G][N] = [4 kThreads]
+  double* avg = part + 4 * kThreads;    // [N]
+  double* cs = avg + N;                 // [N]
+  double* sn = cs + N;                  // [N]
+  for (int j = tid; j < N; j += kThreads) math::twiddle(j, N, sn[j], cs[j]);  // once per workgroup
+
+  // the pending CF phase (previous contract of this workgroup)
+  int64_t prev = -1;
+  const float* prev_row = nullptr;
+  Payoff<float> prev_pay{};
+  double colsum[4];
+
+  auto finish_cf = [&](int64_t pb) {  // column sums -> batch mean -> DFT -> targets row pb
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[g * N + 4 * q + e] = colsum[e];
+    lds_barrier();
+    for (int n = tid; n < N; n += kThreads) {
+      double tot = 0.0;
+      for (int gg = 0; gg < G; ++gg) tot += part[gg * N + n];
+      avg[n] = tot / static_cast<double>(M);
+    }
+    lds_barrier();
+    dft_row<float>(avg, cs, sn, N, static_cast<float2*>(a.targets) + pb * N);
+    lds_barrier();  // part / avg are reused by the next contract
+  };
+
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    const Contract c = load_contract(a.contracts + b * 6);
+    const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
+    const Stepper<float, LOG_EULER, HW> step(c, T);
+    const float x0 = static_cast<float>(c.X0);
+    float* base = static_cast<float*>(a.paths) + (store_all ? b * T * pitch : b * pitch);
+    double acc[1] = {0.0};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) colsum[e] = 0.0;
+    for (int64_t chunk = 0; chunk < P; chunk += kChunk) {
+      v4f pv = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (prev >= 0) pv = *reinterpret_cast<const v4f*>(prev_row + chunk + 4 * tid);
+      if (T == kRowBlock)
+        lane_paths<float, LOG_EULER, HW, false, false, true>(a, step, x0, ordinal, chunk, kPathsPerLane, 0, T,
+                                                             base, acc);
+      else
+        lane_paths<float, LOG_EULER, HW, false, false, false>(a, step, x0, ordinal, chunk, kPathsPerLane, 0, T,
+                                                              base, acc);
+      if (prev >= 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) colsum[e] += static_cast<double>(prev_pay(pv[e]));
+      }
+    }
+    // terminal-row sum of contract b: lane over chunks, wave butterfly, waves 0..7
+    const double w = wave_sum(acc[0]);
+    if (lane == 0) lds_acc[wave] = w;
+    lds_barrier();
+    double tot = 0.0;
+    for (int ww = 0; ww < kWaves; ++ww) tot += lds_acc[ww];
+    lds_barrier();
+    if (prev >= 0) finish_cf(prev);
+    prev = b;
+    prev_row = base + (store_all ? static_cast<int64_t>(T - 1) * pitch : 0);
+    prev_pay = Payoff<float>(a, c, tot);
+  }
+  if (prev >= 0) {  // the last contract: its own re-read, 16 loads in flight per thread
+    constexpr int kBatch = 16;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) colsum[e] = 0.0;
+    for (int64_t c0 = 0; c0 < P; c0 += kBatch * kChunk) {
+      v4f v[kBatch];
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        const int64_t chunk = c0 + u * kChunk < P ? c0 + u * kChunk : P - kChunk;
+        v[u] = *reinterpret_cast<const v4f*>(prev_row + chunk + 4 * tid);
+      }
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        if (c0 + u * kChunk < P) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) colsum[e] += static_cast<double>(prev_pay(v[u][e]));
+        }
+      }
+    }
+    finish_cf(prev);
   }
 }
 
@@ -447,15 +743,58 @@ size_t lds_bytes(int T, int N, bool cf) {
   size_t doubles = static_cast<size_t>(T);                       // lds_tot
   size_t work = static_cast<size_t>(kWaves) * kRowBlock;         // per-wave row partials
   if (cf) {
-    const size_t cfw = static_cast<size_t>(N > kThreads ? N : kThreads) + 3 * static_cast<size_t>(N);
+    const size_t cfw = static_cast<size_t>(N > 4 * kThreads ? N : 4 * kThreads) + 3 * static_cast<size_t>(N);
     if (cfw > work) work = cfw;
   }
   const size_t bytes = (doubles + work) * sizeof(double);
   return bytes < SMC_MIN_LDS ? SMC_MIN_LDS : bytes;
 }
 
+// Resident workgroups of a persistent kernel on the current device (occupancy x CUs, cached
+// per (device, kernel)); grid = min(work items, that).
+int32_t resident_grid(const void* kernel, size_t lds, int64_t items, unsigned* grid) {
+  struct Entry {
+    int dev;
+    const void* kernel;
+    size_t lds;
+    unsigned slots;
+  };
+  static Entry cache[32];
+  static int used = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(SMC_ERR_HIP, "engine: hipGetDevice failed");
+  unsigned slots = 0;
+  for (int i = 0; i < used; ++i)
+    if (cache[i].dev == dev && cache[i].kernel == kernel && cache[i].lds == lds) slots = cache[i].slots;
+  if (slots == 0) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, lds) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(SMC_ERR_HIP, "engine: occupancy query failed");
+    }
+    slots = static_cast<unsigned>((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1));
+    if (used < 32) cache[used++] = Entry{dev, kernel, lds, slots};
+  }
+  *grid = static_cast<unsigned>(items < slots ? items : slots);
+  return SMC_OK;
+}
+
 template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
 int32_t launch_engine_k(const EngineArgs& a, size_t lds, hipStream_t stream) {
+  if (a.slices > 1) {
+    auto kernel = queue_kernel<Real, LOG_EULER, HW, ALLROWS>;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(lds)) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(SMC_ERR_HIP, "queue_kernel: cannot raise the dynamic LDS limit");
+    }
+    unsigned grid = 0;
+    if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), lds, a.B * a.slices, &grid)) return st;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), lds, stream, a);
+    return check_launch("queue_kernel");
+  }
   auto kernel = contract_kernel<Real, LOG_EULER, HW, ALLROWS>;
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -468,9 +807,64 @@ int32_t launch_engine_k(const EngineArgs& a, size_t lds, hipStream_t stream) {
   return check_launch("contract_kernel");
 }
 
+// Workgroups per contract: slices of kSliceChunks chunks when a workspace is given.
+int32_t slices_for(int64_t P, bool sliced) {
+  if (!sliced) return 1;
+  const int64_t chunks = (P + kChunk - 1) / kChunk;
+  return static_cast<int32_t>((chunks + kSliceChunks - 1) / kSliceChunks);
+}
+
+size_t workspace_bytes(int64_t B, int32_t T, int64_t P, bool all_rows) {
+  const int64_t W = slices_for(P, true);
+  if (W <= 1) return 0;
+  return static_cast<size_t>(B) * W * (all_rows ? T : 1) * sizeof(double) + static_cast<size_t>(B + 16) * sizeof(uint32_t);
+}
+
+bool pipelined_ok(const EngineArgs& a, bool f32) {
+  const bool pow2 = a.N >= 4 && (a.N & (a.N - 1)) == 0 && a.N <= kChunk;
+  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T <= kRowBlock && pow2 &&
+         a.P % kChunk == 0 && (a.pitch == 0 || a.pitch % 4 == 0);
+}
+
+size_t pipelined_lds_bytes(int N) {
+  return (static_cast<size_t>(kWaves) + 4 * static_cast<size_t>(kThreads) + 3 * static_cast<size_t>(N)) *
+         sizeof(double);
+}
+
+template <bool LOG_EULER, bool HW>
+int32_t launch_pipelined_k(const EngineArgs& a, hipStream_t stream) {
+  auto kernel = pipelined_kernel<LOG_EULER, HW>;
+  const size_t lds = pipelined_lds_bytes(a.N);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "pipelined_kernel: cannot raise the dynamic LDS limit");
+  }
+  unsigned grid = 0;
+  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), lds, a.B, &grid)) return st;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), lds, stream, a);
+  return check_launch("pipelined_kernel");
+}
+
 template <typename Real>
-int32_t launch_engine(const EngineArgs& a, hipStream_t stream) {
+int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   if (a.B == 0) return SMC_OK;
+#if !defined(SMC_NO_PIPELINE)
+  if (pipelined_ok(a, sizeof(Real) == 4)) {
+    const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+    const bool hw = (a.scheme & SMC_MATH_HW) != 0;
+    if (log_euler && hw) return launch_pipelined_k<true, true>(a, stream);
+    if (log_euler) return launch_pipelined_k<true, false>(a, stream);
+    if (hw) return launch_pipelined_k<false, true>(a, stream);
+    return launch_pipelined_k<false, false>(a, stream);
+  }
+#endif
+  if (a.slices < 1 || !a.simulate) a.slices = 1;
+  if (a.slices > 1 && (!a.partials || !a.arrivals || !a.queues))
+    return fail(SMC_ERR_INVALID_ARGUMENT, "engine: sliced contracts need a workspace");
+  if (static_cast<int64_t>(a.B) * a.slices > 0x7fffffffLL)
+    return fail(SMC_ERR_INVALID_SHAPE, "engine: more than 2^31-1 workgroups in one launch");
   const bool cf = a.targets != nullptr;
   const size_t lds = lds_bytes(a.T, a.N, cf);
   if (lds > kMaxLds) return fail(SMC_ERR_INVALID_SHAPE, "engine: timesteps/network_size exceed the LDS budget");
@@ -568,7 +962,7 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
                           int32_t batches_per_mc_run, uint64_t mc_seed, const int64_t* ordinal_dev, int64_t ordinal0,
                           int32_t scheme, int32_t normalization, int32_t dtype, int32_t store_mode, void* paths_dev,
                           int64_t path_pitch, int64_t chunk_contracts, double* rowsum_dev, void* targets_dev,
-                          void* stream) {
+                          void* workspace_dev, int64_t workspace_size, void* stream) {
   const int64_t P = static_cast<int64_t>(network_size) * batches_per_mc_run;
   if (network_size <= 0 || batches_per_mc_run <= 0)
     return fail(SMC_ERR_INVALID_SHAPE, "smc_train_targets: network_size and batches_per_mc_run must be > 0");
@@ -580,19 +974,36 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
   if (chunk_contracts <= 0) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_targets: chunk_contracts <= 0");
   if (path_pitch != 0 && (path_pitch < P || (path_pitch != P && path_pitch % kPathsPerLane != 0)))
     return fail(SMC_ERR_INVALID_SHAPE, "smc_train_targets: path_pitch must be 0, P, or a multiple of 4 >= P");
-  const size_t esz = dtype == SMC_DTYPE_F32 ? sizeof(float) : sizeof(double);
   const size_t csz = dtype == SMC_DTYPE_F32 ? 2 * sizeof(float) : 2 * sizeof(double);
+  const int64_t chunk = chunk_contracts < n_contracts ? chunk_contracts : n_contracts;
+  const bool all_rows = rowsum_dev != nullptr;
+  const int32_t W = slices_for(P, workspace_dev != nullptr);
+  double* partials = nullptr;
+  uint32_t* arrivals = nullptr;
+  uint32_t* queues = nullptr;
+  if (W > 1) {
+    if (workspace_size < static_cast<int64_t>(workspace_bytes(chunk, timesteps, P, all_rows)))
+      return fail(SMC_ERR_INVALID_SHAPE, "smc_train_targets: workspace smaller than smc_engine_workspace_bytes");
+    partials = static_cast<double*>(workspace_dev);
+    arrivals = reinterpret_cast<uint32_t*>(partials + chunk * W * (all_rows ? timesteps : 1));
+    queues = arrivals + chunk;
+  }
   for (int64_t off = 0; off < n_contracts; off += chunk_contracts) {
     const int64_t nb = n_contracts - off < chunk_contracts ? n_contracts - off : chunk_contracts;
     EngineArgs a{contracts_dev + off * 6, nb, timesteps, P, network_size, batches_per_mc_run, mc_seed,
                  ordinal_dev, ordinal0 + off, scheme, normalization != SMC_NORM_RAW, store_mode, 1,
-                 rowsum_dev ? 1 : 0, paths_dev,
+                 all_rows ? 1 : 0, paths_dev,
                  rowsum_dev ? rowsum_dev + off * timesteps : nullptr,
-                 static_cast<char*>(targets_dev) + static_cast<size_t>(off) * network_size * csz, path_pitch};
-    (void)esz;
+                 static_cast<char*>(targets_dev) + static_cast<size_t>(off) * network_size * csz, path_pitch,
+                 W, partials, arrivals, queues};
     if (int32_t st = dispatch_engine(a, dtype, as_stream(stream))) return st;
   }
   return SMC_OK;
+}
+
+int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, int64_t n_paths, int32_t all_rows) {
+  if (chunk_contracts <= 0 || timesteps <= 0 || n_paths <= 0) return 0;
+  return static_cast<int64_t>(workspace_bytes(chunk_contracts, timesteps, n_paths, all_rows != 0));
 }
 
 int64_t smc_path_pitch(int64_t n_paths, int32_t dtype) {

@@ -125,12 +125,27 @@ struct PathStream {
     float r[4], c[4], sn[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+#if defined(SMC_EXPERIMENT_ZERO_NORMALS)  // tools/micro decomposition builds only
+      r[j] = 0.0f;
+      c[j] = sn[j] = 1.0f;
+#elif defined(SMC_EXPERIMENT_NO_TRANSCENDENTALS)
+      const uint32_t ea = next(), eb = next();
+      r[j] = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ea, 9)) - 1.5f;
+      c[j] = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, eb, 9)) - 1.5f;
+      sn[j] = c[j] * 0.5f;
+#else
+#if defined(SMC_EXPERIMENT_NO_RNG)
+      s0 += 0x9E3779B9u;
+      const uint32_t ua = s0, ub = s0 ^ s1;
+#else
       const uint32_t ua = next(), ub = next();
+#endif
       const float u1 = 2.0f - __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ua, 9));
       r[j] = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u1));
       const float w = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ub, 9));
       c[j] = __builtin_amdgcn_cosf(w);
       sn[j] = __builtin_amdgcn_sinf(w);
+#endif
     }
     const f2 bb = {b, b}, aa = {a, a};
 #pragma unroll

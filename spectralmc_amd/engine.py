@@ -103,6 +103,10 @@ class TrainingEngine:
         shape = (self.chunk, self.T, self.pitch) if store_paths else (self.chunk, self.pitch)
         self._paths_buf = torch.empty(shape, dtype=sim_torch, device=device)
         self.paths = self._paths_buf[..., :self.P]  # (chunk, T, P) / (chunk, P) strided view
+        # slice row sums + arrival counters: contracts run as several workgroups
+        ws = int(_lib.lib().smc_engine_workspace_bytes(self.chunk, self.T, self.P, 0))
+        self._workspace = torch.zeros(max(ws, 8), dtype=torch.uint8, device=device) if ws else None
+        self._workspace_bytes = ws
         self._f32_in = model_dtype == torch.float32
 
     @property
@@ -115,7 +119,6 @@ class TrainingEngine:
 
     def enqueue_step(self) -> StepBuffers:
         """Launch contracts + targets of the next step on the current stream, advance the cursor."""
-        L = _lib.lib()
         stream = _lib.stream_handle()
         b = self.buffers
         offset = self.rank * self.B
@@ -123,13 +126,18 @@ class TrainingEngine:
                     b.real_in if self._f32_in else None)
         if not self._f32_in:
             b.real_in.copy_(b.contracts)
-        _lib.check(L.smc_train_targets(
-            _lib.ptr(b.contracts), self.B, self.T, self.N, self.M, self.seed, _lib.ptr(self.cursor[1:2]), offset,
-            self._scheme, self._norm, self._dtype_code, self.store_mode, _lib.ptr(self._paths_buf), self.pitch,
-            self.chunk,
-            None, _lib.ptr(b.targets), stream))  # training needs only the terminal row sum (kept on chip)
+        self.launch_targets(stream, _lib.ptr(self.cursor[1:2]), offset)
         self.cursor.add_(self.global_batch)
         return b
+
+    def launch_targets(self, stream: int | None, ordinal_ptr: int | None, ordinal0: int) -> None:
+        """The fused path/CF kernel(s) for the current contracts (training needs only the
+        terminal row sum, so no rowsum buffer)."""
+        b = self.buffers
+        _lib.check(_lib.lib().smc_train_targets(
+            _lib.ptr(b.contracts), self.B, self.T, self.N, self.M, self.seed, ordinal_ptr, ordinal0,
+            self._scheme, self._norm, self._dtype_code, self.store_mode, _lib.ptr(self._paths_buf), self.pitch,
+            self.chunk, None, _lib.ptr(b.targets), _lib.ptr(self._workspace), self._workspace_bytes, stream))
 
 
 __all__ = ["TrainingEngine", "StepBuffers", "DEFAULT_PATH_BUFFER_BYTES"]

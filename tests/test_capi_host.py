@@ -77,17 +77,17 @@ def test_engine_argument_errors_do_not_launch() -> None:
     assert L.smc_gbm_simulate(p, 1, 0, 1024, 7, None, 0, 0, 0, p, None, None) == _lib.SMC_ERR_INVALID_SHAPE
     assert L.smc_gbm_simulate(p, 1, 16, 1024, 7, None, 0, 5, 0, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
     assert L.smc_gbm_simulate(p, 1, 16, 1024, 7, None, 0, 0, 9, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
-    assert L.smc_train_targets(p, 4, 16, 0, 4, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, None) == \
+    assert L.smc_train_targets(p, 4, 16, 0, 4, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, None, 0, None) == \
         _lib.SMC_ERR_INVALID_SHAPE
-    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 3, p, 0, 4, None, p, None) == \
+    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 3, p, 0, 4, None, p, None, 0, None) == \
         _lib.SMC_ERR_INVALID_ARGUMENT
     # an N too large for the LDS budget is a shape error, reported before launching
-    assert L.smc_train_targets(p, 4, 16, 1 << 14, 1, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, None) == \
+    assert L.smc_train_targets(p, 4, 16, 1 << 14, 1, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, None, 0, None) == \
         _lib.SMC_ERR_INVALID_SHAPE
     # a row pitch below P, or not a multiple of 4, is a shape error
-    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 31, 4, None, p, None) == \
+    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 31, 4, None, p, None, 0, None) == \
         _lib.SMC_ERR_INVALID_SHAPE
-    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 34, 4, None, p, None) == \
+    assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 34, 4, None, p, None, 0, None) == \
         _lib.SMC_ERR_INVALID_SHAPE
     assert L.smc_normals(7, 0, 0, 10, 0, p, None) == _lib.SMC_ERR_INVALID_SHAPE
     assert L.smc_sobol_draw(None, 6, None, 0, 4, p, p, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
@@ -97,7 +97,7 @@ def test_zero_contracts_is_a_noop() -> None:
     L = _lib.lib()
     dummy = ctypes.c_double(0.0)
     p = ctypes.addressof(dummy)
-    assert L.smc_train_targets(p, 0, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, None) == _lib.SMC_OK
+    assert L.smc_train_targets(p, 0, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, None, 0, None) == _lib.SMC_OK
 
 
 def test_path_pitch_is_an_odd_multiple_of_4k() -> None:
@@ -109,3 +109,17 @@ def test_path_pitch_is_an_odd_multiple_of_4k() -> None:
     for P in (4, 100, 4096, 262144, 1 << 20):
         q = L.smc_path_pitch(P, _lib.DTYPE_F32)
         assert q >= P and (q * 4) % 4096 == 0 and ((q * 4) // 4096) % 2 == 1
+
+
+def test_engine_workspace_size_and_check() -> None:
+    """Sliced contracts (8192-path workgroup slices): f64 slice sums + a u32 arrival counter
+    per contract; too small a workspace is a shape error raised before any launch."""
+    L = _lib.lib()
+    assert L.smc_engine_workspace_bytes(4096, 16, 8192, 0) == 0          # one slice: no workspace
+    assert L.smc_engine_workspace_bytes(4096, 16, 65536, 0) == 4096 * 8 * 8 + (4096 + 16) * 4
+    assert L.smc_engine_workspace_bytes(10, 16, 65536, 1) == 10 * 8 * 16 * 8 + (10 + 16) * 4
+    assert L.smc_engine_workspace_bytes(3, 20, 25000, 0) == 3 * 4 * 8 + (3 + 16) * 4   # 13 chunks -> 4 slices
+    dummy = ctypes.c_double(0.0)
+    p = ctypes.addressof(dummy)
+    assert L.smc_train_targets(p, 4, 16, 256, 64, 7, None, 0, 0, 1, 0, 2, p, 0, 4, None, p, p, 8, None) == \
+        _lib.SMC_ERR_INVALID_SHAPE

@@ -144,7 +144,7 @@ TARGET_CASES = [
 
 def _run_targets(c: np.ndarray, T: int, N: int, M: int, scheme: int, normalize: int, dtype: str, store: int,
                  chunk: int | None = None, ordinal0: int = 0, with_rowsum: bool = True, flags: int = 0,
-                 pitch: int | None = None):
+                 pitch: int | None = None, sliced: bool = False, workspace: torch.Tensor | None = None):
     B = c.shape[0]
     P = N * M
     tdt = torch.float32 if dtype == "float32" else torch.float64
@@ -156,9 +156,13 @@ def _run_targets(c: np.ndarray, T: int, N: int, M: int, scheme: int, normalize: 
     paths = torch.empty(shape, dtype=tdt, device=DEV)
     rowsum = torch.empty((B, T), dtype=torch.float64, device=DEV)
     tg = torch.empty((B, N), dtype=cdt, device=DEV)
+    wsb = int(_L().smc_engine_workspace_bytes(chunk, T, P, int(with_rowsum))) if sliced else 0
+    if sliced and workspace is None:
+        workspace = torch.zeros(max(wsb, 8), dtype=torch.uint8, device=DEV)
     _lib.check(_L().smc_train_targets(_lib.ptr(cd), B, T, N, M, 7, None, ordinal0, scheme | flags, normalize,
                                       0 if dtype == "float32" else 1, store, _lib.ptr(paths), pitch, chunk,
-                                      _lib.ptr(rowsum) if with_rowsum else None, _lib.ptr(tg), None))
+                                      _lib.ptr(rowsum) if with_rowsum else None, _lib.ptr(tg),
+                                      _lib.ptr(workspace) if sliced else None, wsb, None))
     torch.cuda.synchronize()
     return tg.cpu().numpy(), rowsum.cpu().numpy(), paths[..., :P]
 
@@ -177,6 +181,78 @@ def test_targets_match_oracle(oracle, golden, B, T, N, M, scheme, normalize, dty
                                    dtype=dtype)
     tol = 1e-5 if dtype == "float32" else 1e-10
     assert _norm_rel(got, want) < tol
+
+
+SLICED_CASES = [
+    # (B, T, N, M, scheme, normalize, dtype): P > 8192, so a contract runs as several workgroups
+    (3, 16, 256, 64, 0, 1, "float32"),    # 2 whole slices
+    (3, 20, 100, 250, 0, 1, "float32"),   # 4 slices, ragged last chunk, T > 16 (row-block replay)
+    (2, 4, 99, 101, 1, 1, "float32"),     # P % 4 != 0: every chunk masked; simple Euler
+    (2, 16, 1024, 24, 0, 0, "float32"),   # N > workgroup, RAW, 3 slices
+]
+
+
+@pytest.mark.parametrize("B,T,N,M,scheme,normalize,dtype", SLICED_CASES)
+@pytest.mark.parametrize("with_rowsum", [True, False])
+def test_sliced_contracts_match_oracle(oracle, golden, B, T, N, M, scheme, normalize, dtype, with_rowsum) -> None:
+    """Several workgroups per contract + last-arriver CF phase: bit-identical to the oracle's
+    sliced reduction order, run-to-run identical, counters left at zero."""
+    c = _contracts(oracle, golden, B, seed=42)
+    P = N * M
+    wsb = int(_L().smc_engine_workspace_bytes(B, T, P, int(with_rowsum)))
+    assert wsb > 0
+    ws = torch.zeros(wsb, dtype=torch.uint8, device=DEV)
+    got, rowsum, _ = _run_targets(c, T, N, M, scheme, normalize, dtype, _lib.STORE_ALL, ordinal0=5,
+                                  with_rowsum=with_rowsum, sliced=True, workspace=ws)
+    kt, krs = oracle.kernel_targets(c, T, N, M, seed=7, ordinal0=5, scheme=scheme, normalize=bool(normalize),
+                                    sliced=True)
+    np.testing.assert_array_equal(got, kt)
+    if with_rowsum:
+        np.testing.assert_array_equal(rowsum, krs)
+    assert int(ws[-4 * (B + 16):].view(torch.int32).abs().sum()) == 0  # arrival + queue counters reset
+    again, _, _ = _run_targets(c, T, N, M, scheme, normalize, dtype, _lib.STORE_TERMINAL, ordinal0=5,
+                               with_rowsum=with_rowsum, sliced=True, workspace=ws)
+    np.testing.assert_array_equal(again, got)
+    # unsliced: same paths, row sums associated differently -> targets within f32 rounding
+    flat, _, _ = _run_targets(c, T, N, M, scheme, normalize, dtype, _lib.STORE_ALL, ordinal0=5,
+                              with_rowsum=with_rowsum)
+    assert _norm_rel(got, flat) < 1e-6
+
+
+def test_sliced_f64_and_chunked_launches(oracle, golden) -> None:
+    """f64 sliced engine within the reference tolerance; several launches share one workspace."""
+    c = _contracts(oracle, golden, 5, seed=7)
+    got, _, _ = _run_targets(c, 16, 128, 80, 0, 1, "float64", _lib.STORE_ALL, sliced=True)
+    want = oracle.training_targets(c, 16, 128, 80, seed=7, dtype="float64")
+    assert _norm_rel(got, want) < 1e-10
+    a, _, _ = _run_targets(c, 16, 256, 40, 0, 1, "float32", _lib.STORE_ALL, sliced=True)
+    b, _, _ = _run_targets(c, 16, 256, 40, 0, 1, "float32", _lib.STORE_ALL, sliced=True, chunk=2)
+    np.testing.assert_array_equal(a, b)
+
+
+PIPELINED_CASES = [
+    # (B, T, N, M, scheme, normalize): terminal-only training shapes that take the persistent
+    # pipelined kernel (P % 2048 == 0, N a power of two, T <= 16); B > the resident grid (512 on
+    # MI355X), so workgroups run several contracts and pipeline the previous one's CF phase
+    (600, 16, 128, 16, 0, 1),
+    (1100, 5, 256, 8, 1, 1),     # T < 16, simple Euler, 2-3 contracts per workgroup
+    (520, 16, 2048, 2, 0, 0),    # N = kChunk, RAW
+    (513, 16, 4, 1024, 0, 1),    # N = 4
+]
+
+
+@pytest.mark.parametrize("B,T,N,M,scheme,normalize", PIPELINED_CASES)
+@pytest.mark.parametrize("store", [_lib.STORE_ALL, _lib.STORE_TERMINAL])
+def test_pipelined_kernel_matches_oracle(oracle, golden, B, T, N, M, scheme, normalize, store) -> None:
+    c = _contracts(oracle, golden, B, seed=7, skip=3)
+    got, _, _ = _run_targets(c, T, N, M, scheme, normalize, "float32", store, ordinal0=9, with_rowsum=False)
+    kt, _ = oracle.kernel_targets(c, T, N, M, seed=7, ordinal0=9, scheme=scheme, normalize=bool(normalize))
+    np.testing.assert_array_equal(got, kt)
+    # padded pitch and chunked launches: same bits
+    pitch = int(_L().smc_path_pitch(N * M, 0))
+    again, _, _ = _run_targets(c, T, N, M, scheme, normalize, "float32", store, ordinal0=9, with_rowsum=False,
+                               pitch=pitch, chunk=B // 2 + 1)
+    np.testing.assert_array_equal(again, kt)
 
 
 def test_store_modes_and_chunking_bit_identical(oracle, golden) -> None:

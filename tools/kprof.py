@@ -27,6 +27,8 @@ def main() -> None:
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--pitch", type=int, default=-1, help="row pitch (-1: smc_path_pitch, 0: P)")
+    ap.add_argument("--unsliced", action="store_true", help="one workgroup per contract (no workspace)")
+    ap.add_argument("--trace", default="", help="save per-workgroup timestamps (SMC_EXPERIMENT_TRACE builds)")
     a = ap.parse_args()
     lo = np.array([0.001, 0.001, 0.0, -0.2, -0.2, 0.0])
     hi = np.array([1e4, 2e4, 10.0, 0.2, 0.2, 2.0])
@@ -40,9 +42,12 @@ def main() -> None:
     tg = torch.empty((a.B, a.N), dtype=torch.complex64, device=dev)
     scheme = _lib.SCHEME_LOG_EULER | (_lib.MATH_HW if a.math == "hw" else 0)
     L = _lib.lib()
+    wsb = 0 if a.unsliced else int(L.smc_engine_workspace_bytes(a.B, a.T, P, 0))
+    ws = torch.zeros(max(wsb, 8), dtype=torch.uint8, device=dev) if wsb else None
+
     def launch():
         _lib.check(L.smc_train_targets(_lib.ptr(cd), a.B, a.T, a.N, a.M, 7, None, 0, scheme, 1, 0, store,
-                                       _lib.ptr(paths), pitch, a.B, None, _lib.ptr(tg), None))
+                                       _lib.ptr(paths), pitch, a.B, None, _lib.ptr(tg), _lib.ptr(ws), wsb, None))
 
     launch()
     torch.cuda.synchronize()
@@ -52,7 +57,16 @@ def main() -> None:
         launch()
     e1.record()
     torch.cuda.synchronize()
-    print(f"{os.environ.get('SMC_LIB_PATH', 'default')} {a.math} {a.store} pitch={pitch}: "
+    if a.trace:
+        import ctypes
+        n = a.B * 16
+        buf = np.zeros((n, 5), dtype=np.uint64)
+        fn = getattr(L, "smc_debug_trace")
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        torch.cuda.synchronize()
+        assert fn(buf.ctypes.data, n) == 0
+        np.save(a.trace, buf)
+    print(f"{os.environ.get('SMC_LIB_PATH', 'default')} {a.math} {a.store} pitch={pitch} sliced={not a.unsliced}: "
           f"{e0.elapsed_time(e1) / a.iters:.3f} ms/launch",
           "checksum", float(tg.abs().double().mean()))
 
