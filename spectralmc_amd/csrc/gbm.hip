@@ -596,15 +596,60 @@ __device__ __forceinline__ void lds_barrier() {  // LDS-only: no vmcnt drain of 
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <bool LOG_EULER, bool HW>
+#ifndef SMC_ROW_POLICY
+#define SMC_ROW_POLICY 0  // tools/micro experiment: 1 = non-temporal stores for the non-terminal rows
+#endif
+
+// One 2048-path chunk of a kRowBlock-step contract: the lane's 4 paths through all steps in
+// straight-line code — no control flow between the caller's prefetch load and its use, so the
+// compiler waits for that load with a counted vmcnt instead of draining the chunk's row stores.
+// Returns the lane's f32 sum of its 4 terminal values (lane_paths' order).
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
+__device__ __forceinline__ float chunk16(const Stepper<float, LOG_EULER, HW>& step, float x0, PathStream& s,
+                                         char* chunk_base, uint32_t lane_off, int64_t pitch_bytes) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  constexpr bool kPacked = HW && LOG_EULER;
+  float x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
+#pragma unroll
+  for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
+#pragma unroll
+  for (int i = 0; i < kRowBlock; ++i) {
+    if constexpr (kPacked) {
+      if ((i & 1) == 0) s.hw_log_increments4(step.b, step.a, zl, zh);
+      advance_packed(x, (i & 1) ? zh : zl);
+    } else {
+      if ((i & 1) == 0) {
+#pragma unroll
+        for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (i & 1) ? zh[j] : zl[j]);
+    }
+    if (STORE_ALL || i == kRowBlock - 1) {
+      const v4f v = {x[0], x[1], x[2], x[3]};
+      v4f* dst = reinterpret_cast<v4f*>(chunk_base + (STORE_ALL ? i * pitch_bytes : 0) + lane_off);
+      if (SMC_ROW_POLICY == 1 && i < kRowBlock - 1) __builtin_nontemporal_store(v, dst);
+      else *dst = v;
+    }
+  }
+  float part = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kPathsPerLane; ++j) part += x[j];
+  return part;
+}
+
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
 __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void pipelined_kernel(EngineArgs a) {
   typedef float v4f __attribute__((ext_vector_type(4)));
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int T = a.T, N = a.N, M = a.M;
+  constexpr int T = kRowBlock;
+  const int N = a.N, M = a.M;
   const int64_t P = a.P;
-  const bool store_all = a.store == SMC_STORE_ALL;
+  constexpr bool store_all = STORE_ALL;
   const int64_t pitch = a.pitch ? a.pitch : P;
+  const int64_t pitch_bytes = pitch * static_cast<int64_t>(sizeof(float));
+  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(float)) * tid;
   const int G = kChunk / N;  // batches per chunk
   const int Q = N / 4;
   const int q = tid % Q, g = tid / Q;
@@ -641,25 +686,27 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void pipelined_kernel(Eng
     const Stepper<float, LOG_EULER, HW> step(c, T);
     const float x0 = static_cast<float>(c.X0);
     float* base = static_cast<float*>(a.paths) + (store_all ? b * T * pitch : b * pitch);
-    double acc[1] = {0.0};
+    const float* term = base + (store_all ? static_cast<int64_t>(T - 1) * pitch : 0);
+    // unconditional prefetch (no branch around the load): the workgroup's first contract reads
+    // its own, not yet written terminal row and discards it
+    const bool have_prev = prev >= 0;
+    const float* src = have_prev ? prev_row : term;
+    double acc = 0.0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) colsum[e] = 0.0;
     for (int64_t chunk = 0; chunk < P; chunk += kChunk) {
-      v4f pv = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (prev >= 0) pv = *reinterpret_cast<const v4f*>(prev_row + chunk + 4 * tid);
-      if (T == kRowBlock)
-        lane_paths<float, LOG_EULER, HW, false, false, true>(a, step, x0, ordinal, chunk, kPathsPerLane, 0, T,
-                                                             base, acc);
-      else
-        lane_paths<float, LOG_EULER, HW, false, false, false>(a, step, x0, ordinal, chunk, kPathsPerLane, 0, T,
-                                                              base, acc);
-      if (prev >= 0) {
+      const v4f pv = *reinterpret_cast<const v4f*>(src + chunk + 4 * tid);
+      PathStream s(a.seed, ordinal, static_cast<uint64_t>(chunk / kPathsPerLane + tid));
+      acc += static_cast<double>(chunk16<LOG_EULER, HW, STORE_ALL>(step, x0, s, reinterpret_cast<char*>(base + chunk),
+                                                                   lane_off, pitch_bytes));
 #pragma unroll
-        for (int e = 0; e < 4; ++e) colsum[e] += static_cast<double>(prev_pay(pv[e]));
+      for (int e = 0; e < 4; ++e) {
+        const double pay = static_cast<double>(prev_pay(pv[e]));
+        colsum[e] += have_prev ? pay : 0.0;
       }
     }
     // terminal-row sum of contract b: lane over chunks, wave butterfly, waves 0..7
-    const double w = wave_sum(acc[0]);
+    const double w = wave_sum(acc);
     if (lane == 0) lds_acc[wave] = w;
     lds_barrier();
     double tot = 0.0;
@@ -667,7 +714,7 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void pipelined_kernel(Eng
     lds_barrier();
     if (prev >= 0) finish_cf(prev);
     prev = b;
-    prev_row = base + (store_all ? static_cast<int64_t>(T - 1) * pitch : 0);
+    prev_row = term;
     prev_pay = Payoff<float>(a, c, tot);
   }
   if (prev >= 0) {  // the last contract: its own re-read, 16 loads in flight per thread
@@ -822,7 +869,7 @@ size_t workspace_bytes(int64_t B, int32_t T, int64_t P, bool all_rows) {
 
 bool pipelined_ok(const EngineArgs& a, bool f32) {
   const bool pow2 = a.N >= 4 && (a.N & (a.N - 1)) == 0 && a.N <= kChunk;
-  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T <= kRowBlock && pow2 &&
+  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T == kRowBlock && pow2 &&
          a.P % kChunk == 0 && (a.pitch == 0 || a.pitch % 4 == 0);
 }
 
@@ -831,9 +878,9 @@ size_t pipelined_lds_bytes(int N) {
          sizeof(double);
 }
 
-template <bool LOG_EULER, bool HW>
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
 int32_t launch_pipelined_k(const EngineArgs& a, hipStream_t stream) {
-  auto kernel = pipelined_kernel<LOG_EULER, HW>;
+  auto kernel = pipelined_kernel<LOG_EULER, HW, STORE_ALL>;
   const size_t lds = pipelined_lds_bytes(a.N);
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -854,10 +901,18 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   if (pipelined_ok(a, sizeof(Real) == 4)) {
     const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
     const bool hw = (a.scheme & SMC_MATH_HW) != 0;
-    if (log_euler && hw) return launch_pipelined_k<true, true>(a, stream);
-    if (log_euler) return launch_pipelined_k<true, false>(a, stream);
-    if (hw) return launch_pipelined_k<false, true>(a, stream);
-    return launch_pipelined_k<false, false>(a, stream);
+    const bool sa = a.store == SMC_STORE_ALL;
+#define SMC_PIPE(LE, HWM, SA) \
+  if (log_euler == LE && hw == HWM && sa == SA) return launch_pipelined_k<LE, HWM, SA>(a, stream);
+    SMC_PIPE(true, true, true)
+    SMC_PIPE(true, true, false)
+    SMC_PIPE(true, false, true)
+    SMC_PIPE(true, false, false)
+    SMC_PIPE(false, true, true)
+    SMC_PIPE(false, true, false)
+    SMC_PIPE(false, false, true)
+    SMC_PIPE(false, false, false)
+#undef SMC_PIPE
   }
 #endif
   if (a.slices < 1 || !a.simulate) a.slices = 1;

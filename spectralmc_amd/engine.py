@@ -48,7 +48,8 @@ class TrainingEngine:
 
     def __init__(self, cfg: BlackScholesConfig, sampler: SobolSampler, batch_size: int, *, model_dtype: torch.dtype,
                  device: torch.device, rank: int = 0, world_size: int = 1, store_paths: bool = True,
-                 path_buffer_bytes: int | None = None, math: str = "portable") -> None:
+                 path_buffer_bytes: int | None = None, math: str = "portable",
+                 sliced: bool = False) -> None:
         _lib.require_device()
         sp = cfg.sim_params
         self.cfg = cfg
@@ -103,8 +104,10 @@ class TrainingEngine:
         shape = (self.chunk, self.T, self.pitch) if store_paths else (self.chunk, self.pitch)
         self._paths_buf = torch.empty(shape, dtype=sim_torch, device=device)
         self.paths = self._paths_buf[..., :self.P]  # (chunk, T, P) / (chunk, P) strided view
-        # slice row sums + arrival counters: contracts run as several workgroups
-        ws = int(_lib.lib().smc_engine_workspace_bytes(self.chunk, self.T, self.P, 0))
+        # sliced=True: each contract runs as several workgroups (slice row sums + arrival counters
+        # in a workspace); the default one-workgroup-per-contract launch takes the
+        # pipelined kernel where it applies and is the faster one on MI355X
+        ws = int(_lib.lib().smc_engine_workspace_bytes(self.chunk, self.T, self.P, 0)) if sliced else 0
         self._workspace = torch.zeros(max(ws, 8), dtype=torch.uint8, device=device) if ws else None
         self._workspace_bytes = ws
         self._f32_in = model_dtype == torch.float32
