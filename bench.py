@@ -11,7 +11,7 @@ M-batch mean + N-point DFT -> targets, CVNN forward/backward, Adam, grad norm.  
 every rank processes B contracts per step (contract-sharded data parallel, one RCCL all-reduce).
 
 Rank 0 prints ONE JSON line.  `value` = contracts x paths per second over the whole job.
-The roofline object is for the dominant kernel (contract_kernel, the fused path/CF kernel),
+The roofline object is for the dominant kernel (the fused path/CF kernel, pipelined_kernel at C2/C3),
 timed with HIP events on its own stream after the timed region; `cpu_baseline` is the
 oracle (CPU restatement: C/OpenMP paths + numpy.fft + torch-cpu CVNN) on a bounded sample.
 """
@@ -201,7 +201,7 @@ def main() -> None:
     bytes_launch = algorithmic_bytes_per_contract(T, N, M, pricer.store_paths) * contracts_per_launch + \
         48 * contracts_per_launch
     # live: HIP events on the MC stream around each MC-part launch inside the timed region
-    # (Sobol draw + contract_kernel + cursor update; the contract kernel is >99 % of it)
+    # (Sobol draw + path/CF kernel + cursor update; the path/CF kernel is >99 % of it)
     live = [a.elapsed_time(b_) for a, b_ in (session.mc_events or [])]
     live_ms = (sum(live) / len(live) / launches_per_call) if live else kernel_ms
     achieved = bytes_launch / (live_ms * 1e-3) / 1e9
@@ -283,7 +283,7 @@ def main() -> None:
         "config": {"workload": desc, "contracts_per_gpu": B, "global_contracts": world * B, "paths": P,
                    "timesteps": T, "network_size": N, "batches_per_mc_run": M,
                    "path_store": args.store, "math": args.math, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": "contract_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": eng.kernel_name, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": live_ms, "kernel_ms_isolated": kernel_ms, "live_launches": len(live),
                      "algorithmic_bytes_per_launch": bytes_launch,

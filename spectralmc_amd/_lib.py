@@ -58,6 +58,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
                                    _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64,
                                    _c_vp]),
     "smc_engine_workspace_bytes": (_c_i64, [_c_i64, _c_i32, _c_i64, _c_i32]),
+    "smc_train_targets_kernel": (ctypes.c_char_p, [_c_i32, _c_i32, _c_i64, _c_i32, _c_i64, _c_i32]),
     "smc_path_pitch": (_c_i64, [_c_i64, _c_i32]),
     "smc_normals": (_c_i32, [_c_u64, _c_i64, _c_i32, _c_i64, _c_i32, _c_vp, _c_vp]),
     "smc_cvnn_plan": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64)]),

@@ -1061,6 +1061,22 @@ int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, i
   return static_cast<int64_t>(workspace_bytes(chunk_contracts, timesteps, n_paths, all_rows != 0));
 }
 
+const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, int64_t n_paths, int32_t dtype,
+                                     int64_t path_pitch, int32_t sliced) {
+  EngineArgs a{};
+  a.T = timesteps;
+  a.N = network_size;
+  a.P = n_paths;
+  a.simulate = 1;
+  a.targets = &a;  // any non-null: the training call always writes targets
+  a.pitch = path_pitch;
+  a.slices = slices_for(n_paths, sliced != 0);
+#if !defined(SMC_NO_PIPELINE)
+  if (pipelined_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "pipelined_kernel";
+#endif
+  return a.slices > 1 ? "queue_kernel" : "contract_kernel";
+}
+
 int64_t smc_path_pitch(int64_t n_paths, int32_t dtype) {
   // rows at a power-of-two stride alias in the memory system (a 13 % slower store stream at
   // C2, tools/micro/pitchbench.hip): round the row up to 4 KiB, then make the stride an odd

@@ -111,6 +111,9 @@ class TrainingEngine:
         self._workspace = torch.zeros(max(ws, 8), dtype=torch.uint8, device=device) if ws else None
         self._workspace_bytes = ws
         self._f32_in = model_dtype == torch.float32
+        # the path/CF kernel launch_targets runs for this shape (bench labels, rocprof cross-check)
+        self.kernel_name = _lib.lib().smc_train_targets_kernel(
+            self.T, self.N, self.P, self._dtype_code, self.pitch, 1 if ws else 0).decode()
 
     @property
     def global_batch(self) -> int:

@@ -111,6 +111,19 @@ def test_path_pitch_is_an_odd_multiple_of_4k() -> None:
         assert q >= P and (q * 4) % 4096 == 0 and ((q * 4) // 4096) % 2 == 1
 
 
+def test_train_targets_kernel_choice() -> None:
+    """Which path/CF kernel smc_train_targets runs: the pipelined one for 16-step f32 training
+    shapes, the sliced queue kernel with a workspace, the per-contract kernel otherwise."""
+    L = _lib.lib()
+    assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 0) == b"pipelined_kernel"
+    assert L.smc_train_targets_kernel(16, 1024, 262144, 0, 0, 0) == b"pipelined_kernel"
+    assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 1) == b"queue_kernel"
+    assert L.smc_train_targets_kernel(17, 256, 65536, 0, 0, 0) == b"contract_kernel"
+    assert L.smc_train_targets_kernel(16, 256, 65536, 1, 0, 0) == b"contract_kernel"   # f64
+    assert L.smc_train_targets_kernel(16, 256, 1024, 0, 0, 0) == b"contract_kernel"    # P % 2048
+    assert L.smc_train_targets_kernel(16, 6, 6144, 0, 0, 0) == b"contract_kernel"      # N not 2^k
+
+
 def test_engine_workspace_size_and_check() -> None:
     """Sliced contracts (8192-path workgroup slices): f64 slice sums + a u32 arrival counter
     per contract; too small a workspace is a shape error raised before any launch."""
