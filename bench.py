@@ -38,7 +38,12 @@ CONFIGS = {
     # gbm_trainer.py:679-682); 275 GB of paths per step run as equal launches through the scratch
     "c3": (16384, 16, 1024, 256, [32, 32],
            "C3: 16384 contracts x 262144 paths (N=1024 x M=256), T=16, 3-layer CVNN 6->32->32->1024 fp32"),
+    # BASELINE configs[4] (per GPU): 4 correlated assets (Cholesky in LDS), equal-weight basket put
+    "c5": (8192, 16, 256, 512, [32, 32],
+           "C5: 8192 contracts x 131072 paths (N=256 x M=512), 4 correlated assets, T=16, basket put, "
+           "3-layer CVNN 16->32->32->256 fp32"),
 }
+BASKET_ASSETS = {"c5": 4}
 
 
 def parse() -> argparse.Namespace:
@@ -61,7 +66,7 @@ def algorithmic_bytes_per_contract(T: int, N: int, M: int, store_all: bool) -> i
     return (T * P * 4 if store_all else P * 4) + P * 4 + N * 8
 
 
-def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: float) -> dict:
+def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: float, n_assets: int = 0) -> dict:
     """Oracle step on the host cores: MC for a time-boxed sample of the B contracts
     (extrapolated to B) + one full-size CVNN/Adam step on torch-cpu."""
     import numpy as np
@@ -73,7 +78,12 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
     oracle.build()
     threads = oracle.num_threads()
     torch.set_num_threads(threads)
-    lo, hi = make_domain_bounds().arrays()
+    if n_assets:
+        from spectralmc_amd.basket import BasketConfig
+
+        lo, hi = BasketConfig(n_assets=n_assets, timesteps=T, network_size=N, batches_per_mc_run=M).arrays()
+    else:
+        lo, hi = make_domain_bounds().arrays()
     contracts = oracle.sobol_contracts(7, 0, B, lo, hi)
     done, t_mc = 0, 0.0
     chunk = max(1, threads)
@@ -81,11 +91,14 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
     while done < B and t_mc < budget_s * 0.8:
         n = min(chunk, B - done)
         t0 = time.perf_counter()
-        targets.append(oracle.training_targets(contracts[done:done + n], T, N, M, seed=7, ordinal0=done))
+        if n_assets:  # kernel-mode basket restatement (the basket has no reference-mode CPU path)
+            targets.append(oracle.basket_kernel(contracts[done:done + n], n_assets, T, N, M, 7, ordinal0=done)[2])
+        else:
+            targets.append(oracle.training_targets(contracts[done:done + n], T, N, M, seed=7, ordinal0=done))
         t_mc += time.perf_counter() - t0
         done += n
     mc_per_contract = t_mc / done
-    model = make_test_cvnn(n_inputs=6, n_outputs=N, seed=123, dtype=torch.float32, device="cpu",
+    model = make_test_cvnn(n_inputs=contracts.shape[1], n_outputs=N, seed=123, dtype=torch.float32, device="cpu",
                            hidden_layers=len(widths))
     adam = torch.optim.Adam(model.parameters(), lr=1e-2)
     x = torch.tensor(contracts, dtype=torch.float32)
@@ -110,7 +123,8 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
         "steps_per_sec": 1.0 / step_s,
         "cores": threads,
         "kind": "port",
-        "sample": (f"oracle MC (f64 path recursion, OpenMP {threads} threads) on {done}/{B} contracts "
+        "sample": (f"oracle MC ({'f32 basket kernel-mode' if n_assets else 'f64 path recursion'}, OpenMP "
+                   f"{threads} threads) on {done}/{B} contracts "
                    f"x {N * M} paths x T={T} ({t_mc:.1f}s), extrapolated x{B / done:.1f}, "
                    f"+ full B={B} CVNN/Adam step on torch-cpu ({t_nn * 1e3:.1f} ms)"),
         "cpu_model": cpu_model,
@@ -146,7 +160,9 @@ def main() -> None:
     P = N * M
     sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=M, threads_per_block=256,
                                 mc_seed=7, buffer_size=512, dtype=Precision.float32)
-    model = make_test_cvnn(n_inputs=6, n_outputs=N, seed=123, dtype=torch.float32, device=dev,
+    n_assets = BASKET_ASSETS.get(args.config, 0)
+    n_inputs = 3 * n_assets + 4 if n_assets else 6
+    model = make_test_cvnn(n_inputs=n_inputs, n_outputs=N, seed=123, dtype=torch.float32, device=dev,
                            hidden_layers=len(widths))
     cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
                                domain_bounds=make_domain_bounds())
@@ -154,6 +170,11 @@ def main() -> None:
     pricer.store_paths = args.store == "all"
     pricer.math_mode = args.math
     pricer.warmup_steps = max(1, min(2, args.warmup))
+    if n_assets:
+        from spectralmc_amd.basket import BasketConfig, use_basket_engine
+
+        use_basket_engine(pricer, BasketConfig(n_assets=n_assets, timesteps=T, network_size=N, batches_per_mc_run=M,
+                                               mc_seed=7, math=args.math), store_paths=pricer.store_paths)
     tcfg = make_training_config(num_batches=args.warmup + args.steps, batch_size=B, learning_rate=1e-2)
     session = expect_success(pricer.open_session(tcfg))
 
@@ -198,8 +219,11 @@ def main() -> None:
     ev1.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / (args.kernel_iters * launches_per_call)
     contracts_per_launch = min(eng.chunk, eng.B)
-    bytes_launch = algorithmic_bytes_per_contract(T, N, M, pricer.store_paths) * contracts_per_launch + \
-        48 * contracts_per_launch
+    if n_assets:
+        bytes_launch = eng.algorithmic_bytes_per_contract() * contracts_per_launch
+    else:
+        bytes_launch = algorithmic_bytes_per_contract(T, N, M, pricer.store_paths) * contracts_per_launch + \
+            48 * contracts_per_launch
     # live: HIP events on the MC stream around each MC-part launch inside the timed region
     # (Sobol draw + path/CF kernel + cursor update; the path/CF kernel is >99 % of it)
     live = [a.elapsed_time(b_) for a, b_ in (session.mc_events or [])]
@@ -211,7 +235,7 @@ def main() -> None:
     fused = session.program.fused
     if fused is not None:
         prog = session.program
-        widths_all = [6] + list(widths) + [N]
+        widths_all = [n_inputs] + list(widths) + [N]
         macs = sum(4 * a_ * b_ for a_, b_ in zip(widths_all[:-1], widths_all[1:]))  # complex = 4 real MACs
         macs_bwd = macs + sum(4 * a_ * b_ for a_, b_ in zip(widths_all[1:-1], widths_all[2:]))
         flops = 2.0 * (macs + macs_bwd) * B  # forward + weight grads + input grads (not layer 0)
@@ -267,7 +291,8 @@ def main() -> None:
     total_units = world * B * P * args.steps
     value = total_units / elapsed
     line = {
-        "metric": "training-steps/sec (contracts*paths/s) + HBM GB/s, GBM 4096x65536",
+        "metric": "training-steps/sec (contracts*paths/s) + HBM GB/s, GBM 4096x65536"
+                  + (f" [{args.config}: basket of {n_assets} correlated assets]" if n_assets else ""),
         "value": value,
         "unit": "contracts*paths/s",
         "n_gpus": world,
@@ -279,9 +304,11 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: Sobol contracts (seed 7, make_domain_bounds defaults), random-init CVNN (seed 123)",
+        "data": ("synthetic: Sobol basket contracts (seed 7, basket.default_basket_bounds), random-init CVNN (seed 123)"
+                 if n_assets else
+                 "synthetic: Sobol contracts (seed 7, make_domain_bounds defaults), random-init CVNN (seed 123)"),
         "config": {"workload": desc, "contracts_per_gpu": B, "global_contracts": world * B, "paths": P,
-                   "timesteps": T, "network_size": N, "batches_per_mc_run": M,
+                   "timesteps": T, "network_size": N, "batches_per_mc_run": M, "assets": n_assets or 1,
                    "path_store": args.store, "math": args.math, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": eng.kernel_name, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -294,7 +321,7 @@ def main() -> None:
         "final_loss": final.loss,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(B, T, N, M, widths, args.cpu_seconds)
+        cb = cpu_baseline(B, T, N, M, widths, args.cpu_seconds, n_assets)
         line["cpu_baseline"] = cb
         line["speedup_vs_cpu"] = value / cb["value"]
     if rank == 0:

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 4
+#define SMC_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -144,6 +144,23 @@ int64_t smc_path_pitch(int64_t n_paths, int32_t dtype);
  * draws for path p, step t, laid out [t][p]). */
 int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t cols,
                     int32_t dtype, void* out_dev, void* stream);
+
+/* ---- correlated multi-asset (basket) engine ---------------------------------
+ * Extension of the reference engine (BASELINE.json configs[4]; per-asset dynamics as
+ * SimulateBlackScholes, src/spectralmc/gbm.py:224-257, log-Euler; normalisation gbm.py:428-440;
+ * targets as _simulate_fft, gbm_trainer.py:806-817) with an equal-weight basket put.
+ * contracts_dev: [B][3A+4] f64 rows (K, T, r, rho, X0[A], d[A], v[A]); the equicorrelation
+ * matrix (1-rho) I + rho 11^T is Cholesky-factored in LDS per contract.
+ * paths_dev: [chunk][A][T][pitch] f32 (SMC_STORE_ALL) or [chunk][A][pitch] (SMC_STORE_TERMINAL),
+ * reused per launch of chunk_contracts; terminal_sum_dev (may be NULL): [B][A] f64 sums of the
+ * terminal rows; targets_dev: [B][N] complex64.  math: 0 (portable, CPU-reproducible) or
+ * SMC_MATH_HW.  Needs 1 <= A <= 8, N % 4 == 0, N <= 4096, N*M a multiple of 2048. */
+int32_t smc_basket_train_targets(const double* contracts_dev, int64_t n_contracts, int32_t n_assets,
+                                 int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
+                                 uint64_t mc_seed, const int64_t* ordinal_dev, int64_t ordinal0,
+                                 int32_t math, int32_t normalization, int32_t store_mode,
+                                 void* paths_dev, int64_t path_pitch, int64_t chunk_contracts,
+                                 double* terminal_sum_dev, void* targets_dev, void* stream);
 
 /* ---- complex-valued MLP training step --------------------------------------
  * Replaces the network half of _torch_step (src/spectralmc/gbm_trainer.py:819-835) for

@@ -489,3 +489,163 @@ void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, 
   free(cs);
   free(sn);
 }
+
+/* ======================================================================================
+ * BASKET (extension, BASELINE.json configs[4]): exact restatement of the f32 HIP basket engine
+ * (spectralmc_amd/csrc/basket.hip) in portable math.  Per-asset dynamics follow the reference
+ * log-Euler recursion (gbm.py:224-257) and normalisation (gbm.py:428-440); the payoff is the
+ * equal-weight basket put; targets as gbm_trainer.py:806-817 (batch mean, then N-point DFT).
+ * contracts: [B][3A+4] (K, T, r, rho, X0[A], d[A], v[A]).  paths: [B][A][T][P] or NULL;
+ * terminal_sum: [B][A]; targets: [B][N] interleaved complex64.
+ * ====================================================================================== */
+#define B_MAX_ASSETS 8
+
+static void basket_cholesky(int A, double rho, double* L) {
+  for (int i = 0; i < A; ++i)
+    for (int k = 0; k <= i; ++k) {
+      double s = i == k ? 1.0 : rho;
+      for (int m = 0; m < k; ++m) s = s - L[i * B_MAX_ASSETS + m] * L[k * B_MAX_ASSETS + m];
+      L[i * B_MAX_ASSETS + k] = i == k ? sqrt(s > 0.0 ? s : 0.0) : s / L[k * B_MAX_ASSETS + k];
+    }
+}
+
+void oracle_basket_cholesky(int32_t A, double rho, double* L /* [8][8] */) { basket_cholesky(A, rho, L); }
+
+void oracle_basket_kernel(const double* contracts, int64_t B, int32_t A, int32_t T, int32_t N, int32_t M,
+                          uint64_t seed, int64_t ordinal0, int32_t normalize, float* paths, double* terminal_sum,
+                          float* targets) {
+  const double kLog2e = 1.4426950408889634;
+  const int64_t P = (int64_t)N * M;
+  const int width = 3 * A + 4;
+  float* X = (float*)malloc(sizeof(float) * (size_t)A * (size_t)P); /* terminal rows [A][P] */
+  double* lane_acc = (double*)malloc(sizeof(double) * (size_t)K_THREADS * (size_t)A);
+  const int cols = N / 4;
+  const int G = cols <= K_THREADS ? K_THREADS / cols : 1;
+  double* part = (double*)malloc(sizeof(double) * (size_t)N * (size_t)G);
+  double* avg = (double*)malloc(sizeof(double) * (size_t)N);
+  double* cs = (double*)malloc(sizeof(double) * (size_t)N);
+  double* sn = (double*)malloc(sizeof(double) * (size_t)N);
+  for (int j = 0; j < N; ++j) twiddle(j, N, &sn[j], &cs[j]);
+  for (int64_t b = 0; b < B; ++b) {
+    const double* c = contracts + (int64_t)width * b;
+    const double K = c[0], Tm = c[1], r = c[2], rho = c[3];
+    double L[B_MAX_ASSETS * B_MAX_ASSETS];
+    basket_cholesky(A, rho, L);
+    const double dt = Tm / (double)T;
+    const double sq = sqrt(dt);
+    float ca[B_MAX_ASSETS], cb[B_MAX_ASSETS], x0[B_MAX_ASSETS], Lf[B_MAX_ASSETS][B_MAX_ASSETS];
+    for (int i = 0; i < A; ++i) {
+      const double v = c[4 + 2 * A + i], d = c[4 + A + i];
+      const double drift = r - d - 0.5 * v * v;
+      ca[i] = (float)(drift * dt * kLog2e);
+      cb[i] = (float)(v * sq * kLog2e);
+      x0[i] = (float)c[4 + i];
+      for (int k = 0; k <= i; ++k) Lf[i][k] = (float)L[i * B_MAX_ASSETS + k];
+    }
+    const uint64_t ordinal = (uint64_t)(ordinal0 + b);
+    const int64_t groups = P / GROUP;
+#pragma omp parallel for schedule(static)
+    for (int64_t gi = 0; gi < groups; ++gi) {
+      xoshiro128 g;
+      path_stream(seed, ordinal, (uint64_t)gi, &g);
+      float x[B_MAX_ASSETS][GROUP];
+      for (int i = 0; i < A; ++i)
+        for (int j = 0; j < GROUP; ++j) x[i][j] = x0[i];
+      for (int t = 0; t < T; ++t) {
+        for (int j = 0; j < GROUP; ++j) {
+          float z[B_MAX_ASSETS + 1];
+          for (int k = 0; k < A; k += 2) {
+            double z0, z1;
+            normal_pair(&g, 0, &z0, &z1);
+            z[k] = (float)z0;
+            z[k + 1] = (float)z1;
+          }
+          for (int i = 0; i < A; ++i) {
+            float w = Lf[i][0] * z[0];
+            for (int k = 1; k <= i; ++k) w = fmaf(Lf[i][k], z[k], w);
+            x[i][j] = x[i][j] * exp2_any(fmaf(cb[i], w, ca[i]));
+          }
+        }
+        if (paths)
+          for (int i = 0; i < A; ++i)
+            for (int j = 0; j < GROUP; ++j)
+              paths[((b * A + i) * T + t) * P + gi * GROUP + j] = x[i][j];
+      }
+      for (int i = 0; i < A; ++i)
+        for (int j = 0; j < GROUP; ++j) X[(int64_t)i * P + gi * GROUP + j] = x[i][j];
+    }
+    /* terminal sums: per lane over chunks (f32 4-path partials), wave butterfly, waves 0..7 */
+    memset(lane_acc, 0, sizeof(double) * (size_t)K_THREADS * (size_t)A);
+    for (int64_t chunk = 0; chunk < P; chunk += K_CHUNK)
+      for (int lane = 0; lane < K_THREADS; ++lane)
+        for (int i = 0; i < A; ++i) {
+          float p = 0.0f;
+          for (int j = 0; j < K_PPL; ++j) p += X[(int64_t)i * P + chunk + (int64_t)K_PPL * lane + j];
+          lane_acc[(size_t)lane * A + i] += (double)p;
+        }
+    double tot[B_MAX_ASSETS];
+    for (int i = 0; i < A; ++i) {
+      tot[i] = 0.0;
+      for (int w = 0; w < K_WAVES; ++w) {
+        double v[64], nv[64];
+        for (int l = 0; l < 64; ++l) v[l] = lane_acc[(size_t)(64 * w + l) * A + i];
+        for (int off = 32; off >= 1; off >>= 1) {
+          for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+          memcpy(v, nv, sizeof(v));
+        }
+        tot[i] += v[0];
+      }
+      if (terminal_sum) terminal_sum[b * A + i] = tot[i];
+    }
+    /* payoff + per-column batch sums (thread item (q, g): columns 4q..4q+3, m = g, g + G, ...) */
+    const float Tf = (float)Tm;
+    const float df = exp_any((float)(-r) * Tf);
+    const float Kf = (float)K;
+    const float wA = (float)(1.0 / A);
+    float sc[B_MAX_ASSETS];
+    for (int i = 0; i < A; ++i) {
+      const float F = (float)c[4 + i] * exp_any((float)(r - c[4 + A + i]) * Tf);
+      sc[i] = normalize ? F / (float)(tot[i] / (double)P) : 1.0f;
+    }
+    for (int item = 0; item < cols * G; ++item) {
+      const int q = item % cols, gg = item / cols;
+      double sum[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int m = gg; m < M; m += G)
+        for (int e = 0; e < 4; ++e) {
+          float bs = 0.0f;
+          for (int i = 0; i < A; ++i) bs = bs + X[(int64_t)i * P + (int64_t)m * N + 4 * q + e] * sc[i];
+          const float diff = Kf - bs * wA;
+          sum[e] += (double)(df * (diff > 0.0f ? diff : 0.0f));
+        }
+      for (int e = 0; e < 4; ++e) part[gg * N + 4 * q + e] = sum[e];
+    }
+    for (int n = 0; n < N; ++n) {
+      double t2 = 0.0;
+      for (int gg = 0; gg < G; ++gg) t2 += part[gg * N + n];
+      avg[n] = t2 / (double)M;
+    }
+    float* out = targets + 2 * b * N;
+    for (int k = 0; k <= N / 2; ++k) {
+      double re = 0.0, im = 0.0;
+      int idx = 0;
+      for (int n = 0; n < N; ++n) {
+        re = fma(avg[n], cs[idx], re);
+        im = fma(-avg[n], sn[idx], im);
+        idx += k;
+        if (idx >= N) idx -= N;
+      }
+      out[2 * k] = (float)re;
+      out[2 * k + 1] = (float)im;
+      if (k != 0 && 2 * k != N) {
+        out[2 * (N - k)] = (float)re;
+        out[2 * (N - k) + 1] = (float)(-im);
+      }
+    }
+  }
+  free(part);
+  free(avg);
+  free(cs);
+  free(sn);
+  free(lane_acc);
+  free(X);
+}

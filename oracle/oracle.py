@@ -64,6 +64,10 @@ def lib() -> ctypes.CDLL:
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_kernel_cf.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_basket_kernel.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64,
+                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_basket_cholesky.argtypes = [ctypes.c_int32, ctypes.c_double, ctypes.c_void_p]
         L.oracle_log_pos.argtypes = [ctypes.c_float]
         L.oracle_log_pos.restype = ctypes.c_float
         L.oracle_exp2.argtypes = [ctypes.c_float]
@@ -221,6 +225,51 @@ def kernel_targets(contracts: np.ndarray, timesteps: int, network_size: int, bat
     _, terminal, rowsum = kernel_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme,
                                        sliced=sliced)
     return kernel_cf(contracts, terminal, rowsum[:, -1], network_size, batches, normalize), rowsum
+
+
+# --------------------------------------------------------------------------- basket (extension)
+def basket_fields(n_assets: int) -> tuple[str, ...]:
+    """Contract row of the basket engine (spectralmc_amd/basket.py BasketInputs order)."""
+    return ("K", "T", "r", "rho") + tuple(f"X0_{i}" for i in range(n_assets)) + tuple(
+        f"d_{i}" for i in range(n_assets)) + tuple(f"v_{i}" for i in range(n_assets))
+
+
+def basket_cholesky(n_assets: int, rho: float) -> np.ndarray:
+    L = np.zeros((8, 8), dtype=np.float64)
+    lib().oracle_basket_cholesky(n_assets, float(rho), _ptr(L))
+    return L[:n_assets, :n_assets].copy()
+
+
+def basket_kernel(contracts: np.ndarray, n_assets: int, timesteps: int, network_size: int, batches: int,
+                  seed: int, ordinal0: int = 0, normalize: bool = True,
+                  want_paths: bool = False) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
+    """KERNEL mode restatement of the f32 basket engine (csrc/basket.hip, portable math):
+    (paths [B,A,T,P] or None, terminal sums [B,A] f64, targets [B,N] complex64)."""
+    contracts = np.ascontiguousarray(contracts, dtype=np.float64)
+    B = contracts.shape[0]
+    assert contracts.shape[1] == 3 * n_assets + 4
+    P = network_size * batches
+    paths = np.empty((B, n_assets, timesteps, P), dtype=np.float32) if want_paths else None
+    tsum = np.empty((B, n_assets), dtype=np.float64)
+    out = np.empty((B, network_size), dtype=np.complex64)
+    lib().oracle_basket_kernel(_ptr(contracts), B, n_assets, timesteps, network_size, batches, seed, ordinal0,
+                               int(normalize), _ptr(paths), _ptr(tsum), _ptr(out))
+    return paths, tsum, out
+
+
+def basket_reference_targets(contracts: np.ndarray, n_assets: int, terminal: np.ndarray, network_size: int,
+                             batches: int) -> np.ndarray:
+    """numpy statement of the basket payoff + FFT (reference gbm_trainer.py:806-817 shape:
+    FFT of each batch row, then the mean) from given terminal values [B,A,P] (f64)."""
+    contracts = np.asarray(contracts, dtype=np.float64)
+    B, A = contracts.shape[0], n_assets
+    K, T, r = contracts[:, 0], contracts[:, 1], contracts[:, 2]
+    X0, d = contracts[:, 4:4 + A], contracts[:, 4 + A:4 + 2 * A]
+    F = X0 * np.exp((r[:, None] - d) * T[:, None])
+    scale = F / terminal.mean(axis=2)
+    basket = (terminal * scale[:, :, None]).mean(axis=1)
+    put = np.exp(-r * T)[:, None] * np.maximum(K[:, None] - basket, 0.0)
+    return np.fft.fft(put.reshape(B, batches, network_size), axis=2).mean(axis=1)
 
 
 # --------------------------------------------------------------------------- CVNN step

@@ -34,7 +34,7 @@ STORE_TERMINAL = 1
 MATH_HW = 0x100
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 
@@ -67,6 +67,8 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_cvnn_reduce_grads": (_c_i32, [_c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
     "smc_adam_step": (_c_i32, [_c_i32, _c_i64, _c_vp, _c_vp, _c_vp]),
     "smc_adam_norm_partials": (_c_i64, [_c_i64]),
+    "smc_basket_train_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_i32, _c_u64, _c_vp, _c_i64,
+                                          _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
 }
 
 CVNN_MAX_LAYERS = 8

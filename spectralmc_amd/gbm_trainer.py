@@ -679,9 +679,13 @@ class TrainingSession:
         self.global_batch = config.batch_size * world
         pricer._cvnn.train()
         dev = pricer._torch_device
-        self.engine = TrainingEngine(pricer._cfg, sampler, config.batch_size, model_dtype=pricer._dtype.to_torch(),
-                                     device=dev, rank=rank, world_size=world, store_paths=pricer.store_paths,
-                                     math=pricer.math_mode)
+        factory = getattr(pricer, "mc_engine_factory", None)  # e.g. basket.use_basket_engine
+        if factory is not None:
+            self.engine = factory(pricer, config.batch_size, dev, rank, world)
+        else:
+            self.engine = TrainingEngine(pricer._cfg, sampler, config.batch_size, model_dtype=pricer._dtype.to_torch(),
+                                         device=dev, rank=rank, world_size=world, store_paths=pricer.store_paths,
+                                         math=pricer.math_mode)
         self.params = list(pricer._cvnn.parameters())
         self.program = _StepProgram(pricer, self.engine, adam, self.params, ctx)
         self.sobol_skip0 = pricer._sobol_skip

@@ -1,0 +1,162 @@
+"""Correlated multi-asset (basket) engine through the C ABI vs the oracle's kernel-mode
+restatement (oracle_basket_kernel): bit-exact in portable math; HW math within the stated
+north-star tolerance; statistics of the correlated drivers; training through GbmCVNNPricer."""
+
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from spectralmc_amd import _lib
+from spectralmc_amd.basket import BasketConfig, BasketEngine, basket_targets, use_basket_engine
+from spectralmc_amd.gbm_trainer import GbmCVNNPricer
+from spectralmc_amd.models.numerical import Precision
+from tests.helpers import (
+    expect_success,
+    make_black_scholes_config,
+    make_domain_bounds,
+    make_gbm_cvnn_config,
+    make_simulation_params,
+    make_test_cvnn,
+    make_training_config,
+)
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _contracts(oracle, cfg: BasketConfig, n: int, skip: int = 0) -> np.ndarray:
+    lo, hi = cfg.arrays()
+    return oracle.sobol_contracts(cfg.mc_seed, skip, n, lo, hi)
+
+
+@pytest.mark.parametrize("A", [1, 3, 4, 8])
+@pytest.mark.parametrize("T", [16, 5])
+def test_portable_bit_exact_vs_oracle(oracle, A, T) -> None:
+    cfg = BasketConfig(n_assets=A, timesteps=T, network_size=64, batches_per_mc_run=64, math="portable")
+    B = 6
+    c = _contracts(oracle, cfg, B)
+    want_paths, want_sum, want_t = oracle.basket_kernel(c, A, T, 64, 64, cfg.mc_seed, ordinal0=3, want_paths=True)
+    cd = torch.from_numpy(c).to(DEV)
+    paths = torch.empty((B, A, T, cfg.total_paths), dtype=torch.float32, device=DEV)
+    tsum = torch.empty((B, A), dtype=torch.float64, device=DEV)
+    got = basket_targets(cd, cfg, ordinal0=3, paths=paths, terminal_sum=tsum)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(paths.cpu().numpy(), want_paths)
+    np.testing.assert_array_equal(tsum.cpu().numpy(), want_sum)
+    np.testing.assert_array_equal(got.cpu().numpy(), want_t)
+
+
+def test_terminal_store_and_padded_pitch_same_targets(oracle) -> None:
+    cfg = BasketConfig(n_assets=4, timesteps=16, network_size=256, batches_per_mc_run=16, math="portable")
+    B = 5
+    c = _contracts(oracle, cfg, B, skip=64)
+    _, _, want = oracle.basket_kernel(c, 4, 16, 256, 16, cfg.mc_seed)
+    cd = torch.from_numpy(c).to(DEV)
+    got_term = basket_targets(cd, cfg)
+    pitch = int(_lib.lib().smc_path_pitch(cfg.total_paths, 0))
+    paths = torch.empty((B, 4, 16, pitch), dtype=torch.float32, device=DEV)
+    got_all = basket_targets(cd, cfg, paths=paths, pitch=pitch)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got_term.cpu().numpy(), want)
+    np.testing.assert_array_equal(got_all.cpu().numpy(), want)
+
+
+def test_hw_math_within_tolerance(oracle) -> None:
+    """HW transcendentals (~1 ulp per op): targets within 1e-4 of the oracle relative to the row scale."""
+    cfg = BasketConfig(n_assets=4, timesteps=16, network_size=256, batches_per_mc_run=64, math="hw")
+    B = 16
+    c = _contracts(oracle, cfg, B)
+    _, want_sum, want = oracle.basket_kernel(c, 4, 16, 256, 64, cfg.mc_seed)
+    tsum = torch.empty((B, 4), dtype=torch.float64, device=DEV)
+    got = basket_targets(torch.from_numpy(c).to(DEV), cfg, terminal_sum=tsum).cpu().numpy()
+    np.testing.assert_allclose(tsum.cpu().numpy(), want_sum, rtol=1e-4)
+    scale = np.abs(want).max(axis=1, keepdims=True) + 1e-30
+    assert float((np.abs(got - want) / scale).max()) < 1e-4
+
+
+def test_correlation_and_forward_statistics(oracle) -> None:
+    """Log-returns of the terminal values have correlation rho and per-asset mean/variance of GBM."""
+    A, T = 3, 4
+    cfg = BasketConfig(n_assets=A, timesteps=T, network_size=256, batches_per_mc_run=256, math="hw")
+    rho, v, Tm, r = 0.6, np.array([0.2, 0.3, 0.4]), 1.0, 0.03
+    d = np.array([0.0, 0.01, 0.02])
+    X0 = np.array([100.0, 50.0, 10.0])
+    row = np.concatenate([[100.0, Tm, r, rho], X0, d, v])
+    c = torch.from_numpy(np.tile(row, (2, 1))).to(DEV)
+    paths = torch.empty((2, A, T, cfg.total_paths), dtype=torch.float32, device=DEV)
+    basket_targets(c, cfg, paths=paths)
+    lr = np.log(paths[0, :, -1, :].double().cpu().numpy() / X0[:, None])
+    corr = np.corrcoef(lr)
+    for i in range(A):
+        for k in range(i):
+            assert abs(corr[i, k] - rho) < 0.01, corr
+        assert lr[i].std() == pytest.approx(v[i] * np.sqrt(Tm), rel=0.01)
+        assert lr[i].mean() == pytest.approx((r - d[i] - 0.5 * v[i] ** 2) * Tm, abs=0.01)
+    # different contract ordinals draw different streams
+    assert not torch.equal(paths[0], paths[1])
+
+
+def test_chunked_launches_match_single_launch(oracle) -> None:
+    cfg = BasketConfig(n_assets=4, timesteps=16, network_size=64, batches_per_mc_run=32, math="portable")
+    B = 12
+    per = 4 * 16 * int(_lib.lib().smc_path_pitch(cfg.total_paths, 0)) * 4
+    big = BasketEngine(cfg, B, device=torch.device(DEV))
+    small = BasketEngine(cfg, B, device=torch.device(DEV), path_buffer_bytes=5 * per)
+    assert small.chunk == 4 and big.chunk == B
+    for e in (big, small):
+        e.set_position(0, 0)
+        e.enqueue_step()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(big.buffers.targets.cpu().numpy(), small.buffers.targets.cpu().numpy())
+    c = _contracts(oracle, cfg, B)
+    np.testing.assert_array_equal(big.buffers.contracts.cpu().numpy(), c)
+    _, _, want = oracle.basket_kernel(c, 4, 16, 64, 32, cfg.mc_seed)
+    np.testing.assert_array_equal(big.buffers.targets.cpu().numpy(), want)
+
+
+def test_bad_shapes_fail_loudly() -> None:
+    cfg = BasketConfig(n_assets=2, timesteps=4, network_size=64, batches_per_mc_run=32)
+    c = torch.zeros((2, cfg.dim), dtype=torch.float64, device=DEV)
+    t = torch.empty((2, 64), dtype=torch.complex64, device=DEV)
+    p = torch.empty((2, 2, 2048), dtype=torch.float32, device=DEV)
+    L = _lib.lib()
+    st = L.smc_basket_train_targets(_lib.ptr(c), 2, 9, 4, 64, 32, 7, None, 0, 0, 1, _lib.STORE_TERMINAL,
+                                    _lib.ptr(p), 0, 2, None, _lib.ptr(t), None)
+    assert st == 1
+    st = L.smc_basket_train_targets(_lib.ptr(c), 2, 2, 4, 64, 30, 7, None, 0, 0, 1, _lib.STORE_TERMINAL,
+                                    _lib.ptr(p), 0, 2, None, _lib.ptr(t), None)
+    assert st == 2
+    assert b"2048" in L.smc_last_error_string()
+
+
+def test_pricer_trains_on_baskets_and_matches_oracle_step(oracle) -> None:
+    """One GbmCVNNPricer step on basket contracts (portable math) vs the oracle targets + torch-cpu step."""
+    A, T, N, M, B = 4, 16, 128, 16, 32
+    bcfg = BasketConfig(n_assets=A, timesteps=T, network_size=N, batches_per_mc_run=M, mc_seed=7, math="portable")
+    sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=M, threads_per_block=256, mc_seed=7,
+                                buffer_size=512, dtype=Precision.float32)
+    model = make_test_cvnn(n_inputs=bcfg.dim, n_outputs=N, seed=123, dtype=torch.float32)
+    cpu_model = copy.deepcopy(model).cpu()
+    cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                               domain_bounds=make_domain_bounds())
+    pricer = expect_success(GbmCVNNPricer.create(cfg))
+    pricer.warmup_steps = 0
+    use_basket_engine(pricer, bcfg)
+    res = expect_success(pricer.train(make_training_config(num_batches=1, batch_size=B, learning_rate=1e-2)))
+
+    c = _contracts(oracle, bcfg, B)
+    _, _, targets = oracle.basket_kernel(c, A, T, N, M, 7)
+    x = torch.tensor(c, dtype=torch.float32)
+    ref = oracle.torch_step(cpu_model, x, torch.zeros_like(x), torch.from_numpy(targets),
+                            torch.optim.Adam(cpu_model.parameters(), lr=1e-2))
+    assert res.final_loss == pytest.approx(ref.loss, rel=1e-4)
+
+    # and several graph-replayed steps stay finite
+    pricer.warmup_steps = 2
+    res = expect_success(pricer.train(make_training_config(num_batches=5, batch_size=B, learning_rate=1e-2)))
+    assert np.isfinite(res.final_loss)

@@ -35,6 +35,9 @@ for step in "$@"; do
     bench_hw_terminal) run bench_hw_terminal 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --store terminal --math hw ;;
     bench_terminal) run bench_terminal 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --store terminal --math portable ;;
     bench_c1) run bench_c1 600 python bench.py --config c1 --steps 50 --warmup 5 --no-cpu-baseline ;;
+    basket)  run basket 600 python -u -m pytest tests/test_gpu_basket.py -x -v --timeout 120 --timeout-method thread -rf ;;
+    bench_c5) run bench_c5 600 python bench.py --config c5 --steps 10 --warmup 3 --kernel-iters 2 ;;
+    prof_c5) cd /tmp && run prof_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv -- python "$ROOT/bench.py" --config c5 --steps 5 --warmup 2 --kernel-iters 1 --no-cpu-baseline; cd "$ROOT" ;;
     bench_c3) run bench_c3 900 python bench.py --config c3 --steps 3 --warmup 2 --kernel-iters 1 --no-cpu-baseline ;;
     prof)    cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT" ;;
     prof_default) cd /tmp && run prof_default 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_default" -o run --output-format csv -- python "$ROOT/bench.py"; cd "$ROOT" ;;
