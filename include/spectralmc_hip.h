@@ -161,6 +161,9 @@ int32_t smc_basket_train_targets(const double* contracts_dev, int64_t n_contract
                                  int32_t math, int32_t normalization, int32_t store_mode,
                                  void* paths_dev, int64_t path_pitch, int64_t chunk_contracts,
                                  double* terminal_sum_dev, void* targets_dev, void* stream);
+/* Basket workgroups (one per contract) resident on the current device at once, for sizing
+ * chunk_contracts in whole rounds; -1 on a bad argument or a failed device query. */
+int64_t smc_basket_resident_slots(int32_t n_assets, int32_t network_size, int32_t math);
 
 /* ---- complex-valued MLP training step --------------------------------------
  * Replaces the network half of _torch_step (src/spectralmc/gbm_trainer.py:819-835) for

@@ -69,6 +69,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_adam_norm_partials": (_c_i64, [_c_i64]),
     "smc_basket_train_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_i32, _c_u64, _c_vp, _c_i64,
                                           _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
+    "smc_basket_resident_slots": (_c_i64, [_c_i32, _c_i32, _c_i32]),
 }
 
 CVNN_MAX_LAYERS = 8

@@ -171,6 +171,12 @@ class BasketEngine:
         per_contract = self.A * rows * self.pitch * 4
         budget = path_buffer_bytes if path_buffer_bytes is not None else DEFAULT_PATH_BUFFER_BYTES
         max_chunk = max(1, min(B, budget // per_contract))
+        if max_chunk < B:
+            # several launches: whole rounds of resident workgroups, so no launch ends in a
+            # part-filled round (C5: 1171 -> 1024 contracts per launch, 2 full rounds each)
+            slots = int(_lib.lib().smc_basket_resident_slots(self.A, self.N, self._math))
+            if 0 < slots <= max_chunk:
+                max_chunk -= max_chunk % slots
         launches = -(-B // max_chunk)
         self.chunk = -(-B // launches)  # equal launches
         shape = (self.chunk, self.A, rows, self.pitch)

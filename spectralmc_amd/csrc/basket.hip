@@ -272,6 +272,37 @@ int32_t launch_basket_k(const BasketArgs& a, hipStream_t stream) {
   return check_launch("basket_kernel");
 }
 
+// Workgroups of basket_kernel<A, HW> resident on the current device at once (occupancy x CUs).
+template <int A, bool HW>
+int64_t basket_slots_k(int N) {
+  int dev = 0, cus = 0, per_cu = 0;
+  const size_t lds = basket_lds_bytes(A, N);
+  auto kernel = basket_kernel<A, HW>;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return (void)hipGetLastError(), -1;
+  if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess)
+    return (void)hipGetLastError(), -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBThreads, lds) != hipSuccess)
+    return (void)hipGetLastError(), -1;
+  return static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
+}
+
+template <bool HW>
+int64_t basket_slots(int A, int N) {
+  switch (A) {
+    case 1: return basket_slots_k<1, HW>(N);
+    case 2: return basket_slots_k<2, HW>(N);
+    case 3: return basket_slots_k<3, HW>(N);
+    case 4: return basket_slots_k<4, HW>(N);
+    case 5: return basket_slots_k<5, HW>(N);
+    case 6: return basket_slots_k<6, HW>(N);
+    case 7: return basket_slots_k<7, HW>(N);
+    case 8: return basket_slots_k<8, HW>(N);
+    default: return -1;
+  }
+}
+
 template <bool HW>
 int32_t launch_basket(int A, const BasketArgs& a, hipStream_t stream) {
   switch (A) {
@@ -332,6 +363,11 @@ int32_t smc_basket_train_targets(const double* contracts_dev, int64_t n_contract
     if (st) return st;
   }
   return SMC_OK;
+}
+
+int64_t smc_basket_resident_slots(int32_t n_assets, int32_t network_size, int32_t math) {
+  if (n_assets < 1 || n_assets > kMaxAssets || network_size <= 0 || network_size > 4096) return -1;
+  return math == SMC_MATH_HW ? basket_slots<true>(n_assets, network_size) : basket_slots<false>(n_assets, network_size);
 }
 
 #pragma GCC visibility pop

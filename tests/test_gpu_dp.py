@@ -24,7 +24,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _train(batch: int, outfile: str) -> None:
+def _train(batch: int, outfile: str, basket: int = 0) -> None:
     from spectralmc_amd.gbm_trainer import GbmCVNNPricer
     from spectralmc_amd.models.numerical import Precision
     from tests.helpers import (
@@ -37,42 +37,48 @@ def _train(batch: int, outfile: str) -> None:
         make_training_config,
     )
 
-    sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=M, mc_seed=7, buffer_size=1,
+    m = 32 if basket else M  # the basket engine takes N*M in multiples of 2048
+    sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=m, mc_seed=7, buffer_size=1,
                                 dtype=Precision.float32)
-    model = make_test_cvnn(n_inputs=6, n_outputs=N, seed=123, dtype=torch.float32, device="cuda:0",
+    model = make_test_cvnn(n_inputs=3 * basket + 4 if basket else 6, n_outputs=N, seed=123, dtype=torch.float32, device="cuda:0",
                            hidden_layers=2)
     cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
                                domain_bounds=make_domain_bounds())
     pricer = expect_success(GbmCVNNPricer.create(cfg))
+    if basket:
+        from spectralmc_amd.basket import BasketConfig, use_basket_engine
+
+        use_basket_engine(pricer, BasketConfig(n_assets=basket, timesteps=T, network_size=N, batches_per_mc_run=m))
     res = expect_success(pricer.train(make_training_config(num_batches=STEPS, batch_size=batch)))
     snap = res.updated_config
     np.savez(outfile, loss=res.final_loss, grad_norm=res.final_grad_norm, sobol_skip=snap.sobol_skip,
              **{f"p{i}": p.detach().cpu().numpy() for i, p in enumerate(model.parameters())})
 
 
-def _rank(rank: int, world: int, port: int, outdir: str) -> None:
+def _rank(rank: int, world: int, port: int, outdir: str, basket: int) -> None:
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _train(B_LOCAL, os.path.join(outdir, f"rank{rank}.npz"))
+        _train(B_LOCAL, os.path.join(outdir, f"rank{rank}.npz"), basket)
     finally:
         dist.destroy_process_group()
 
 
-def test_two_ranks_match_one_process_with_the_global_batch(tmp_path) -> None:
+@pytest.mark.parametrize("basket", [0, 4], ids=["single_asset", "basket4"])
+def test_two_ranks_match_one_process_with_the_global_batch(tmp_path, basket) -> None:
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, str(tmp_path), basket)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=600)
         assert p.exitcode == 0, f"rank exited with {p.exitcode}"
     single = tmp_path / "single.npz"
-    _train(2 * B_LOCAL, str(single))
+    _train(2 * B_LOCAL, str(single), basket)
     r0, r1, s = np.load(tmp_path / "rank0.npz"), np.load(tmp_path / "rank1.npz"), np.load(single)
     for k in r0.files:
         np.testing.assert_array_equal(r0[k], r1[k])  # replicas stay bit-identical

@@ -36,6 +36,7 @@ for step in "$@"; do
     bench_terminal) run bench_terminal 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --store terminal --math portable ;;
     bench_c1) run bench_c1 600 python bench.py --config c1 --steps 50 --warmup 5 --no-cpu-baseline ;;
     basket)  run basket 600 python -u -m pytest tests/test_gpu_basket.py -x -v --timeout 120 --timeout-method thread -rf ;;
+    dp)      run dp 600 python -u -m pytest tests/test_gpu_dp.py -x -v --timeout 300 --timeout-method thread -rf ;;
     bench_c5) run bench_c5 600 python bench.py --config c5 --steps 10 --warmup 3 --kernel-iters 2 ;;
     prof_c5) cd /tmp && run prof_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv -- python "$ROOT/bench.py" --config c5 --steps 5 --warmup 2 --kernel-iters 1 --no-cpu-baseline; cd "$ROOT" ;;
     bench_c3) run bench_c3 900 python bench.py --config c3 --steps 3 --warmup 2 --kernel-iters 1 --no-cpu-baseline ;;
