@@ -1,0 +1,60 @@
+"""Kernel-only driver for rocprofv3: launches smc_basket_train_targets on one C5-sized launch
+(1024 contracts x 4 assets x 131072 paths x T=16, store all, padded pitch) `--iters` times.
+
+    rocprofv3 --kernel-trace --pmc WRITE_SIZE -- python tools/kprof_basket.py
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from spectralmc_amd import _lib  # noqa: E402
+from spectralmc_amd.basket import BasketConfig  # noqa: E402
+from spectralmc_amd.sobol_sampler import SobolEngine  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=1024)
+    ap.add_argument("--A", type=int, default=4)
+    ap.add_argument("--T", type=int, default=16)
+    ap.add_argument("--N", type=int, default=256)
+    ap.add_argument("--M", type=int, default=512)
+    ap.add_argument("--math", default="hw", choices=["hw", "portable"])
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    cfg = BasketConfig(n_assets=a.A, timesteps=a.T, network_size=a.N, batches_per_mc_run=a.M, math=a.math)
+    lo, hi = cfg.arrays()
+    c = lo + (hi - lo) * SobolEngine(cfg.dim, 7).random(a.B)
+    dev = torch.device("cuda", 0)
+    cd = torch.from_numpy(c).to(dev)
+    P = cfg.total_paths
+    pitch = int(_lib.lib().smc_path_pitch(P, 0))
+    paths = torch.empty((a.B, a.A, a.T, pitch), dtype=torch.float32, device=dev)
+    tg = torch.empty((a.B, a.N), dtype=torch.complex64, device=dev)
+    L = _lib.lib()
+    mh = _lib.MATH_HW if a.math == "hw" else 0
+
+    def launch():
+        _lib.check(L.smc_basket_train_targets(_lib.ptr(cd), a.B, a.A, a.T, a.N, a.M, 7, None, 0, mh, 1,
+                                              _lib.STORE_ALL, _lib.ptr(paths), pitch, a.B, None, _lib.ptr(tg), None))
+
+    launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"basket A={a.A} {a.math}: {e0.elapsed_time(e1) / a.iters:.3f} ms/launch checksum",
+          float(tg.abs().double().mean()))
+
+
+if __name__ == "__main__":
+    main()
