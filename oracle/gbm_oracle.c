@@ -533,14 +533,15 @@ void oracle_basket_kernel(const double* contracts, int64_t B, int32_t A, int32_t
     basket_cholesky(A, rho, L);
     const double dt = Tm / (double)T;
     const double sq = sqrt(dt);
-    float ca[B_MAX_ASSETS], cb[B_MAX_ASSETS], x0[B_MAX_ASSETS], Lf[B_MAX_ASSETS][B_MAX_ASSETS];
+    /* y_i = a_i + sum_{k<=i} (b_i L_ik) z_k, b_i L_ik rounded once from f64 */
+    float ca[B_MAX_ASSETS], x0[B_MAX_ASSETS], Lb[B_MAX_ASSETS][B_MAX_ASSETS];
     for (int i = 0; i < A; ++i) {
       const double v = c[4 + 2 * A + i], d = c[4 + A + i];
       const double drift = r - d - 0.5 * v * v;
       ca[i] = (float)(drift * dt * kLog2e);
-      cb[i] = (float)(v * sq * kLog2e);
+      const double bi = v * sq * kLog2e;
       x0[i] = (float)c[4 + i];
-      for (int k = 0; k <= i; ++k) Lf[i][k] = (float)L[i * B_MAX_ASSETS + k];
+      for (int k = 0; k <= i; ++k) Lb[i][k] = (float)(bi * L[i * B_MAX_ASSETS + k]);
     }
     const uint64_t ordinal = (uint64_t)(ordinal0 + b);
     const int64_t groups = P / GROUP;
@@ -561,9 +562,9 @@ void oracle_basket_kernel(const double* contracts, int64_t B, int32_t A, int32_t
             z[k + 1] = (float)z1;
           }
           for (int i = 0; i < A; ++i) {
-            float w = Lf[i][0] * z[0];
-            for (int k = 1; k <= i; ++k) w = fmaf(Lf[i][k], z[k], w);
-            x[i][j] = x[i][j] * exp2_any(fmaf(cb[i], w, ca[i]));
+            float y = ca[i];
+            for (int k = 0; k <= i; ++k) y = fmaf(Lb[i][k], z[k], y);
+            x[i][j] = x[i][j] * exp2_any(y);
           }
         }
         if (paths)

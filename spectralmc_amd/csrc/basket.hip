@@ -18,8 +18,9 @@
 //
 // Per lane, per step t, per path j = 0..3: ceil(A/2) Box-Muller pairs from the lane's
 // PathStream (smc_rng.h; the same (seed, contract ordinal, group) keying as the single-asset
-// engine) -> z[0..A) (an odd A discards the last pair's second normal); w = L z (f32, k order);
-// x_i *= 2^(a_i + b_i w_i).  oracle/gbm_oracle.c (oracle_basket_kernel) restates this bit for bit
+// engine) -> z[0..A) (an odd A discards the last pair's second normal);
+// y_i = a_i + sum_{k<=i} (b_i L_ik) z_k (f32 fma chain in k order, b_i L_ik rounded once from f64);
+// x_i *= 2^y_i.  oracle/gbm_oracle.c (oracle_basket_kernel) restates this bit for bit
 // in portable math.
 
 #include <cmath>
@@ -38,6 +39,9 @@ constexpr int kBWaves = kBThreads / 64;
 constexpr int kBPaths = 4;                      // paths per lane
 constexpr int kBChunk = kBThreads * kBPaths;    // paths per workgroup pass
 constexpr int kMaxAssets = 8;
+#ifndef SMC_BASKET_MIN_BLOCKS
+#define SMC_BASKET_MIN_BLOCKS 1
+#endif
 constexpr double kBLog2e = 1.4426950408889634;
 
 struct BasketArgs {
@@ -74,8 +78,9 @@ __device__ void cholesky_equicorr(int A, double rho, double* L) {
 }
 
 template <int A, bool HW>
-__global__ __launch_bounds__(kBThreads) void basket_kernel(BasketArgs a) {
+__global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kernel(BasketArgs a) {
   typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
@@ -99,16 +104,17 @@ __global__ __launch_bounds__(kBThreads) void basket_kernel(BasketArgs a) {
   const double dt = Tm / static_cast<double>(T);
   const double sq = sqrt(dt);
   constexpr double zscale = HW ? PathStream::kNormalScale<true> : 1.0;
-  float ca[A], cb[A], x0[A], Lf[A][A];
+  // y_i = a_i + sum_{k <= i} (b_i L_ik) z_k: the volatility coefficient is folded into the factor
+  float ca[A], x0[A], Lb[A][A];
 #pragma unroll
   for (int i = 0; i < A; ++i) {
     const double v = c[4 + 2 * A + i], d = c[4 + A + i];
     const double drift = r - d - 0.5 * v * v;
     ca[i] = static_cast<float>(drift * dt * kBLog2e);
-    cb[i] = static_cast<float>(v * sq * kBLog2e * zscale);
+    const double bi = v * sq * kBLog2e * zscale;
     x0[i] = static_cast<float>(c[4 + i]);
 #pragma unroll
-    for (int k = 0; k < A; ++k) Lf[i][k] = k <= i ? static_cast<float>(Ld[i * kMaxAssets + k]) : 0.0f;
+    for (int k = 0; k < A; ++k) Lb[i][k] = k <= i ? static_cast<float>(bi * Ld[i * kMaxAssets + k]) : 0.0f;
   }
 
   const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
@@ -128,19 +134,26 @@ __global__ __launch_bounds__(kBThreads) void basket_kernel(BasketArgs a) {
 #pragma unroll
       for (int j = 0; j < kBPaths; ++j) x[i][j] = x0[i];
     for (int t = 0; t < T; ++t) {
+      // path pairs (j, j + 1): draws in path order, then the correlation and the step as packed
+      // f32 ops (v_pk_fma_f32 / v_pk_mul_f32; same IEEE results as the scalar ops)
 #pragma unroll
-      for (int j = 0; j < kBPaths; ++j) {
-        float z[A + 1];
+      for (int j = 0; j < kBPaths; j += 2) {
+        float z0[A + 1], z1[A + 1];
 #pragma unroll
-        for (int k = 0; k < A; k += 2) s.template normal_pair<HW>(z[k], z[k + 1]);
+        for (int k = 0; k < A; k += 2) s.template normal_pair<HW>(z0[k], z0[k + 1]);
+#pragma unroll
+        for (int k = 0; k < A; k += 2) s.template normal_pair<HW>(z1[k], z1[k + 1]);
 #pragma unroll
         for (int i = 0; i < A; ++i) {
-          float w = Lf[i][0] * z[0];
+          f2 y = {ca[i], ca[i]};
 #pragma unroll
-          for (int k = 1; k <= i; ++k) w = fmaf(Lf[i][k], z[k], w);
-          const float y = fmaf(cb[i], w, ca[i]);
-          if constexpr (HW) x[i][j] = x[i][j] * __builtin_amdgcn_exp2f(y);
-          else x[i][j] = x[i][j] * math::exp2_any(y);
+          for (int k = 0; k <= i; ++k) y = __builtin_elementwise_fma(f2{Lb[i][k], Lb[i][k]}, f2{z0[k], z1[k]}, y);
+          f2 e;
+          if constexpr (HW) e = f2{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+          else e = f2{math::exp2_any(y.x), math::exp2_any(y.y)};
+          const f2 xv = f2{x[i][j], x[i][j + 1]} * e;
+          x[i][j] = xv.x;
+          x[i][j + 1] = xv.y;
         }
       }
       if (a.store_all || t == T - 1) {

@@ -27,6 +27,7 @@ def main() -> None:
     ap.add_argument("--M", type=int, default=512)
     ap.add_argument("--math", default="hw", choices=["hw", "portable"])
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--store", default="all", choices=["all", "terminal"])
     a = ap.parse_args()
     cfg = BasketConfig(n_assets=a.A, timesteps=a.T, network_size=a.N, batches_per_mc_run=a.M, math=a.math)
     lo, hi = cfg.arrays()
@@ -35,14 +36,15 @@ def main() -> None:
     cd = torch.from_numpy(c).to(dev)
     P = cfg.total_paths
     pitch = int(_lib.lib().smc_path_pitch(P, 0))
-    paths = torch.empty((a.B, a.A, a.T, pitch), dtype=torch.float32, device=dev)
+    store = _lib.STORE_ALL if a.store == "all" else _lib.STORE_TERMINAL
+    paths = torch.empty((a.B, a.A, a.T if a.store == "all" else 1, pitch), dtype=torch.float32, device=dev)
     tg = torch.empty((a.B, a.N), dtype=torch.complex64, device=dev)
     L = _lib.lib()
     mh = _lib.MATH_HW if a.math == "hw" else 0
 
     def launch():
         _lib.check(L.smc_basket_train_targets(_lib.ptr(cd), a.B, a.A, a.T, a.N, a.M, 7, None, 0, mh, 1,
-                                              _lib.STORE_ALL, _lib.ptr(paths), pitch, a.B, None, _lib.ptr(tg), None))
+                                              store, _lib.ptr(paths), pitch, a.B, None, _lib.ptr(tg), None))
 
     launch()
     torch.cuda.synchronize()
@@ -52,7 +54,7 @@ def main() -> None:
         launch()
     e1.record()
     torch.cuda.synchronize()
-    print(f"basket A={a.A} {a.math}: {e0.elapsed_time(e1) / a.iters:.3f} ms/launch checksum",
+    print(f"basket A={a.A} {a.math} {a.store}: {e0.elapsed_time(e1) / a.iters:.3f} ms/launch checksum",
           float(tg.abs().double().mean()))
 
 
