@@ -133,7 +133,7 @@ def basket_targets(contracts: torch.Tensor, cfg: BasketConfig, *, ordinal0: int 
 
 class BasketEngine:
     """Device buffers + launches of the basket Monte-Carlo side of one training step
-    (the ``TrainingEngine`` interface; DESIGN.md §9)."""
+    (the ``TrainingEngine`` interface; DESIGN.md §8)."""
 
     kernel_name = "basket_kernel"
 
