@@ -190,6 +190,9 @@ __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kerne
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's terminal-row stores
   __syncthreads();
+#if defined(SMC_EXPERIMENT_NO_CF)  // tools/micro decomposition builds only
+  return;
+#endif
 
   // payoff: per-asset forward scale, equal-weight basket, discounted put (f32, asset order)
   const float Tf = static_cast<float>(Tm);

@@ -740,6 +740,156 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void pipelined_kernel(Eng
   }
 }
 
+// ---- experiment (SMC_SPECIALIZED builds): producer / store wave specialisation ------------
+// Waves 0-3 compute (each lane: virtual lanes l and l + 256 of the 512-lane chunk mapping, i.e. the
+// same two 4-path groups and streams as contract_kernel's lanes l and l + 256) and stage each row
+// in an LDS ring; waves 4-7 copy rows from the ring to HBM (same addresses and dwordx4 coalescing)
+// and keep the terminal-row sums of virtual lanes l and l + 256 in contract_kernel's order, so the
+// results are bit-identical.  Counters in LDS (ready / freed per ring slot) decouple the two roles:
+// compute waves never wait on the store queue.  Every spin is bounded, so a protocol error gives
+// wrong numbers, never a hang.
+#ifndef SMC_SPECIALIZED
+#define SMC_SPECIALIZED 0
+#endif
+#ifndef SMC_RING
+#define SMC_RING 8
+#endif
+constexpr int kRing = SMC_RING;              // staged rows (8 KB each)
+constexpr int kRoleWaves = kWaves / 2;       // waves per role
+constexpr int kRoleLanes = kThreads / 2;
+
+__device__ __forceinline__ void ring_wait(const int* ctr, int target) {
+  for (int it = 0; it < (1 << 16); ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ void ring_signal(int* ctr) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // this wave's LDS accesses done
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+size_t specialized_lds_bytes(int N) {
+  const size_t cf = (static_cast<size_t>(N > 4 * kThreads ? N : 4 * kThreads) + 3 * static_cast<size_t>(N)) *
+                    sizeof(double);
+  const size_t ring = static_cast<size_t>(kRing) * kThreads * 16;
+  return 16 * sizeof(double) + (cf > ring ? cf : ring);
+}
+
+template <bool LOG_EULER, bool HW>
+__global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void specialized_kernel(EngineArgs a) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x;
+  constexpr int T = kRowBlock;
+  const int64_t P = a.P;
+  const int64_t pitch = a.pitch ? a.pitch : P;
+  double* lds_acc = lds;                                   // [kWaves]
+  int* ready = reinterpret_cast<int*>(lds + kWaves);       // [kRing]
+  int* freed = ready + kRing;                              // [kRing]
+  v4f* ring = reinterpret_cast<v4f*>(lds + 16);            // [kRing][kThreads]
+  if (tid < 2 * kRing) ready[tid] = 0;
+  __syncthreads();
+  const Contract c = load_contract(a.contracts + b * 6);
+  const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
+  float* base = static_cast<float*>(a.paths) + b * T * pitch;
+  const int64_t nchunks = P / kChunk;
+  if (wave < kRoleWaves) {  // compute
+    const Stepper<float, LOG_EULER, HW> step(c, T);
+    const float x0 = static_cast<float>(c.X0);
+    constexpr bool kPacked = HW && LOG_EULER;
+    for (int64_t ci = 0; ci < nchunks; ++ci) {
+      const int64_t chunk = ci * kChunk;
+      PathStream s0(a.seed, ordinal, static_cast<uint64_t>(chunk / kPathsPerLane + tid));
+      PathStream s1(a.seed, ordinal, static_cast<uint64_t>(chunk / kPathsPerLane + tid + kRoleLanes));
+      float x[2][kPathsPerLane], zl[2][kPathsPerLane], zh[2][kPathsPerLane];
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) x[0][j] = x[1][j] = x0;
+#pragma unroll
+      for (int i = 0; i < kRowBlock; ++i) {
+#if defined(SMC_SPEC_NOCOMPUTE)  // tools/micro decomposition builds only
+#pragma unroll
+        for (int j = 0; j < kPathsPerLane; ++j) x[0][j] = x[1][j] = x0 + static_cast<float>(i);
+        if (false)
+#endif
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          PathStream& s = h ? s1 : s0;
+          if constexpr (kPacked) {
+            if ((i & 1) == 0) s.hw_log_increments4(step.b, step.a, zl[h], zh[h]);
+            advance_packed(x[h], (i & 1) ? zh[h] : zl[h]);
+          } else {
+            if ((i & 1) == 0) {
+#pragma unroll
+              for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[h][j], zh[h][j]);
+            }
+#pragma unroll
+            for (int j = 0; j < kPathsPerLane; ++j) x[h][j] = step(x[h][j], (i & 1) ? zh[h][j] : zl[h][j]);
+          }
+        }
+        const int64_t seq = ci * kRowBlock + i;
+        const int slot = static_cast<int>(seq % kRing);
+        const int use = static_cast<int>(seq / kRing);
+        ring_wait(freed + slot, kRoleWaves * use);
+        ring[slot * kThreads + tid] = v4f{x[0][0], x[0][1], x[0][2], x[0][3]};
+        ring[slot * kThreads + tid + kRoleLanes] = v4f{x[1][0], x[1][1], x[1][2], x[1][3]};
+        ring_signal(ready + slot);
+      }
+    }
+  } else {  // store
+    const int cl = tid - kRoleLanes;
+    const uint32_t off0 = 16u * cl, off1 = 16u * (cl + kRoleLanes);
+    double acc0 = 0.0, acc1 = 0.0;
+    for (int64_t ci = 0; ci < nchunks; ++ci) {
+      const int64_t chunk = ci * kChunk;
+#pragma unroll
+      for (int i = 0; i < kRowBlock; ++i) {
+        const int64_t seq = ci * kRowBlock + i;
+        const int slot = static_cast<int>(seq % kRing);
+        const int use = static_cast<int>(seq / kRing);
+        ring_wait(ready + slot, kRoleWaves * (use + 1));
+        const v4f v0 = ring[slot * kThreads + cl], v1 = ring[slot * kThreads + cl + kRoleLanes];
+        ring_signal(freed + slot);
+        char* row = reinterpret_cast<char*>(base + i * pitch + chunk);
+#if defined(SMC_SPEC_NOSTORE)  // tools/micro decomposition builds only: terminal row only
+        if (i == kRowBlock - 1)
+#endif
+        {
+          *reinterpret_cast<v4f*>(row + off0) = v0;
+          *reinterpret_cast<v4f*>(row + off1) = v1;
+        }
+        if (i == kRowBlock - 1) {
+          float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+          for (int j = 0; j < kPathsPerLane; ++j) {
+            p0 += v0[j];
+            p1 += v1[j];
+          }
+          acc0 += static_cast<double>(p0);
+          acc1 += static_cast<double>(p1);
+        }
+      }
+    }
+    const double w0 = wave_sum(acc0), w1 = wave_sum(acc1);
+    if (lane == 0) {
+      lds_acc[wave - kRoleWaves] = w0;               // virtual wave (wave - 4)
+      lds_acc[wave - kRoleWaves + kRoleWaves] = w1;  // virtual wave (wave - 4) + 4
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  double tot = 0.0;
+  for (int w = 0; w < kWaves; ++w) tot += lds_acc[w];
+  __syncthreads();  // the ring is dead; the CF phase reuses it
+#if defined(SMC_EXPERIMENT_NO_CF)
+  if (false)
+#endif
+  cf_targets_contract<float>(a, c, b, tot, lds + 16);
+}
+
 // In-place forward normalisation of a stored [B][T][P] matrix (gbm.py:428-438).
 template <typename Real>
 __global__ __launch_bounds__(256) void normalize_kernel(const double* __restrict__ contracts, int64_t B,
@@ -894,9 +1044,33 @@ int32_t launch_pipelined_k(const EngineArgs& a, hipStream_t stream) {
   return check_launch("pipelined_kernel");
 }
 
+template <bool LOG_EULER, bool HW>
+int32_t launch_specialized_k(const EngineArgs& a, hipStream_t stream) {
+  auto kernel = specialized_kernel<LOG_EULER, HW>;
+  const size_t lds = specialized_lds_bytes(a.N);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "specialized_kernel: cannot raise the dynamic LDS limit");
+  }
+  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds, stream, a);
+  return check_launch("specialized_kernel");
+}
+
 template <typename Real>
 int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   if (a.B == 0) return SMC_OK;
+#if SMC_SPECIALIZED
+  if (pipelined_ok(a, sizeof(Real) == 4) && a.store == SMC_STORE_ALL && specialized_lds_bytes(a.N) <= kMaxLds) {
+    const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+    const bool hw = (a.scheme & SMC_MATH_HW) != 0;
+    if (log_euler && hw) return launch_specialized_k<true, true>(a, stream);
+    if (log_euler) return launch_specialized_k<true, false>(a, stream);
+    if (hw) return launch_specialized_k<false, true>(a, stream);
+    return launch_specialized_k<false, false>(a, stream);
+  }
+#endif
 #if !defined(SMC_NO_PIPELINE)
   if (pipelined_ok(a, sizeof(Real) == 4)) {
     const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
