@@ -751,6 +751,7 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void pipelined_kernel(Eng
 #ifndef SMC_SPECIALIZED
 #define SMC_SPECIALIZED 0
 #endif
+#if SMC_SPECIALIZED
 #ifndef SMC_RING
 #define SMC_RING 8
 #endif
@@ -889,6 +890,7 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void specialized_kernel(E
 #endif
   cf_targets_contract<float>(a, c, b, tot, lds + 16);
 }
+#endif  // SMC_SPECIALIZED
 
 // In-place forward normalisation of a stored [B][T][P] matrix (gbm.py:428-438).
 template <typename Real>
@@ -1044,6 +1046,7 @@ int32_t launch_pipelined_k(const EngineArgs& a, hipStream_t stream) {
   return check_launch("pipelined_kernel");
 }
 
+#if SMC_SPECIALIZED
 template <bool LOG_EULER, bool HW>
 int32_t launch_specialized_k(const EngineArgs& a, hipStream_t stream) {
   auto kernel = specialized_kernel<LOG_EULER, HW>;
@@ -1057,6 +1060,7 @@ int32_t launch_specialized_k(const EngineArgs& a, hipStream_t stream) {
   hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds, stream, a);
   return check_launch("specialized_kernel");
 }
+#endif
 
 template <typename Real>
 int32_t launch_engine(EngineArgs a, hipStream_t stream) {
