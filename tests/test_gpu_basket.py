@@ -51,6 +51,26 @@ def test_portable_bit_exact_vs_oracle(oracle, A, T) -> None:
     np.testing.assert_array_equal(got.cpu().numpy(), want_t)
 
 
+@pytest.mark.parametrize("A,N,M,B", [(2, 64, 32, 1100), (4, 2048, 2, 530), (3, 12, 512, 9)])
+def test_persistent_pipelined_and_general_shapes_bit_exact(oracle, A, N, M, B) -> None:
+    """B above the resident grid (512 workgroups): workgroups run several contracts and overlap the
+    previous one's CF re-read (N | 2048); N = 12 takes the one-workgroup-per-contract kernel."""
+    cfg = BasketConfig(n_assets=A, timesteps=4, network_size=N, batches_per_mc_run=M, math="portable")
+    c = _contracts(oracle, cfg, B, skip=5)
+    _, want_sum, want = oracle.basket_kernel(c, A, 4, N, M, cfg.mc_seed, ordinal0=11)
+    cd = torch.from_numpy(c).to(DEV)
+    tsum = torch.empty((B, A), dtype=torch.float64, device=DEV)
+    got = basket_targets(cd, cfg, ordinal0=11, terminal_sum=tsum)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(tsum.cpu().numpy(), want_sum)
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+    if B > 600:  # full path matrix, padded pitch
+        pitch = int(_lib.lib().smc_path_pitch(cfg.total_paths, 0))
+        paths = torch.empty((B, A, 4, pitch), dtype=torch.float32, device=DEV)
+        again = basket_targets(cd, cfg, ordinal0=11, paths=paths, pitch=pitch)
+        np.testing.assert_array_equal(again.cpu().numpy(), want)
+
+
 def test_terminal_store_and_padded_pitch_same_targets(oracle) -> None:
     cfg = BasketConfig(n_assets=4, timesteps=16, network_size=256, batches_per_mc_run=16, math="portable")
     B = 5
