@@ -11,7 +11,8 @@ M-batch mean + N-point DFT -> targets, CVNN forward/backward, Adam, grad norm.  
 every rank processes B contracts per step (contract-sharded data parallel, one RCCL all-reduce).
 
 Rank 0 prints ONE JSON line.  `value` = contracts x paths per second over the whole job.
-The roofline object is for the dominant kernel (the fused path/CF kernel, pipelined_kernel at C2/C3),
+The roofline object is for the dominant kernel (the fused path/CF kernel: contract_kernel, or
+basket_kernel at C5),
 timed with HIP events on its own stream after the timed region; `cpu_baseline` is the
 oracle (CPU restatement: C/OpenMP paths + numpy.fft + torch-cpu CVNN) on a bounded sample.
 """

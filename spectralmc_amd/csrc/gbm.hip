@@ -590,7 +590,7 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void queue_kernel(EngineA
 // and no workgroup ever drains its stores.  Thread tid owns columns 4q..4q+3 (q = tid mod N/4)
 // and batches m = g, g + G, ... (g = tid div N/4, G = kChunk / N) — exactly the quad order of
 // cf_targets_contract, so targets are bit-identical to the unpipelined kernel.
-__device__ __forceinline__ void lds_barrier() {  // LDS-only: no vmcnt drain of the path stores
+[[maybe_unused]] __device__ __forceinline__ void lds_barrier() {  // LDS-only: no vmcnt drain of the path stores
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -1019,13 +1019,13 @@ size_t workspace_bytes(int64_t B, int32_t T, int64_t P, bool all_rows) {
   return static_cast<size_t>(B) * W * (all_rows ? T : 1) * sizeof(double) + static_cast<size_t>(B + 16) * sizeof(uint32_t);
 }
 
-bool pipelined_ok(const EngineArgs& a, bool f32) {
+[[maybe_unused]] bool pipelined_ok(const EngineArgs& a, bool f32) {
   const bool pow2 = a.N >= 4 && (a.N & (a.N - 1)) == 0 && a.N <= kChunk;
   return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T == kRowBlock && pow2 &&
          a.P % kChunk == 0 && (a.pitch == 0 || a.pitch % 4 == 0);
 }
 
-size_t pipelined_lds_bytes(int N) {
+[[maybe_unused]] size_t pipelined_lds_bytes(int N) {
   return (static_cast<size_t>(kWaves) + 4 * static_cast<size_t>(kThreads) + 3 * static_cast<size_t>(N)) *
          sizeof(double);
 }
@@ -1075,7 +1075,7 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
     return launch_specialized_k<false, false>(a, stream);
   }
 #endif
-#if !defined(SMC_NO_PIPELINE)
+#if defined(SMC_PIPELINE)  // opt-in: slower than contract_kernel on MI355X
   if (pipelined_ok(a, sizeof(Real) == 4)) {
     const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
     const bool hw = (a.scheme & SMC_MATH_HW) != 0;
@@ -1249,7 +1249,7 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.targets = &a;  // any non-null: the training call always writes targets
   a.pitch = path_pitch;
   a.slices = slices_for(n_paths, sliced != 0);
-#if !defined(SMC_NO_PIPELINE)
+#if defined(SMC_PIPELINE)
   if (pipelined_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "pipelined_kernel";
 #endif
   return a.slices > 1 ? "queue_kernel" : "contract_kernel";

@@ -112,11 +112,11 @@ def test_path_pitch_is_an_odd_multiple_of_4k() -> None:
 
 
 def test_train_targets_kernel_choice() -> None:
-    """Which path/CF kernel smc_train_targets runs: the pipelined one for 16-step f32 training
-    shapes, the sliced queue kernel with a workspace, the per-contract kernel otherwise."""
+    """Which path/CF kernel smc_train_targets runs: the sliced queue kernel with a workspace, the
+    per-contract kernel otherwise (the pipelined kernel is an opt-in SMC_PIPELINE build)."""
     L = _lib.lib()
-    assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 0) == b"pipelined_kernel"
-    assert L.smc_train_targets_kernel(16, 1024, 262144, 0, 0, 0) == b"pipelined_kernel"
+    assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 0) == b"contract_kernel"
+    assert L.smc_train_targets_kernel(16, 1024, 262144, 0, 0, 0) == b"contract_kernel"
     assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 1) == b"queue_kernel"
     assert L.smc_train_targets_kernel(17, 256, 65536, 0, 0, 0) == b"contract_kernel"
     assert L.smc_train_targets_kernel(16, 256, 65536, 1, 0, 0) == b"contract_kernel"   # f64
