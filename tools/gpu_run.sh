@@ -43,14 +43,15 @@ for step in "$@"; do
     prof)    cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT" ;;
     prof_default) cd /tmp && run prof_default 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_default" -o run --output-format csv -- python "$ROOT/bench.py"; cd "$ROOT" ;;
     prof_hw) cd /tmp && run prof_hw 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_hw" -o run --output-format csv -- python "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --math hw; cd "$ROOT" ;;
+    pmc_c5_sq) cd /tmp && run pmc_c5_sq 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_c5_sq" -o run --output-format csv -- python "$ROOT/tools/kprof_basket.py"; cd "$ROOT" ;;
     pmc_c5_write) cd /tmp && run pmc_c5_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_c5_write" -o run --output-format csv -- python "$ROOT/tools/kprof_basket.py"; cd "$ROOT" ;;
     pmc_c5_fetch) cd /tmp && run pmc_c5_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_c5_fetch" -o run --output-format csv -- python "$ROOT/tools/kprof_basket.py"; cd "$ROOT" ;;
     pmc_c2_write) cd /tmp && run pmc_c2_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_c2_write" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
     pmc_c2_fetch) cd /tmp && run pmc_c2_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_c2_fetch" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
-    pmc_hw_all)  cd /tmp && run pmc_hw_all 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_hw_all" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all; cd "$ROOT" ;;
-    pmc_hw_term) cd /tmp && run pmc_hw_term 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_hw_term" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store terminal; cd "$ROOT" ;;
-    pmc_hw_bytes) cd /tmp && run pmc_hw_bytes 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_hw_bytes" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all; cd "$ROOT" ;;
-    pmc_hw_fetch) cd /tmp && run pmc_hw_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_hw_fetch" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all; cd "$ROOT" ;;
+    pmc_hw_all)  cd /tmp && run pmc_hw_all 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_hw_all" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
+    pmc_hw_term) cd /tmp && run pmc_hw_term 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_hw_term" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store terminal --unsliced; cd "$ROOT" ;;
+    pmc_hw_bytes) cd /tmp && run pmc_hw_bytes 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_hw_bytes" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
+    pmc_hw_fetch) cd /tmp && run pmc_hw_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_hw_fetch" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
