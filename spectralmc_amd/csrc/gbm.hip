@@ -200,7 +200,10 @@ __device__ __forceinline__ void advance_packed(Real (&x)[4], const Real (&y)[4])
 // T > kRowBlock), rows [t0, t0 + nrows) are stored and added to acc[].  MASKED handles the
 // ragged last chunk (nvalid < 4) and P % 4 != 0 with scalar stores; otherwise one dwordx4
 // store per row, addressed as (wave-uniform row base) + (32-bit lane offset).
-template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS, bool MASKED, bool FULLBLOCK>
+// STRAIGHT (with FULLBLOCK, T == kRowBlock, every row stored): t == i, the terminal row is i == 15
+// and every store is unconditional, so the 16-row block is straight-line code — no per-row
+// branches and no per-row condition masks (which otherwise spill SGPRs into VGPR lanes).
+template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS, bool MASKED, bool FULLBLOCK, bool STRAIGHT = false>
 __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                            uint64_t ordinal, int64_t chunk, int nvalid, int t0, int nrows,
                                            Real* contract_base, double (&acc)[ALLROWS ? kRowBlock : 1]) {
@@ -208,7 +211,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   const int T = a.T;
   const int64_t P = a.P;
   const int64_t pitch = a.pitch ? a.pitch : P;
-  const bool store_all = a.store == SMC_STORE_ALL;
+  const bool store_all = STRAIGHT || a.store == SMC_STORE_ALL;
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));  // the lane's group stream
   // f32 HW log-Euler: the RNG hands back the step exponents directly (packed path pairs)
@@ -216,7 +219,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
 #pragma unroll
   for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
-  for (int t = 0; t < t0; t += 2) {  // t0 is a multiple of kRowBlock (even)
+  for (int t = 0; t < (STRAIGHT ? 0 : t0); t += 2) {  // t0 is a multiple of kRowBlock (even)
     if constexpr (kPacked) {
       s.hw_log_increments4(step.b, step.a, zl, zh);
       advance_packed(x, zl);
@@ -234,7 +237,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
 #pragma unroll
   for (int i = 0; i < kRowBlock; ++i) {
     if (FULLBLOCK || i < nrows) {
-      const int t = t0 + i;
+      const int t = STRAIGHT ? i : t0 + i;
       if constexpr (kPacked) {
         if ((i & 1) == 0) s.hw_log_increments4(step.b, step.a, zl, zh);
         advance_packed(x, (i & 1) ? zh : zl);
@@ -246,10 +249,11 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
 #pragma unroll
         for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (i & 1) ? zh[j] : zl[j]);
       }
-      if (store_all || t == T - 1) {
+      const bool last = STRAIGHT ? i == kRowBlock - 1 : t == T - 1;
+      if (store_all || last) {
         char* row = reinterpret_cast<char*>(chunk_base + (store_all ? static_cast<int64_t>(t) * pitch : 0));
         // the terminal row is read back by the CF phase (maybe another workgroup's): write-through
-        const bool handoff = t == T - 1 && a.targets != nullptr;
+        const bool handoff = last && (STRAIGHT || a.targets != nullptr);
         if constexpr (!MASKED) {
           V4 v4;
           v4.x = x[0];
@@ -269,7 +273,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
           }
         }
       }
-      if (ALLROWS || t == T - 1) {
+      if (ALLROWS || last) {
         Real part = 0;
 #pragma unroll
         for (int j = 0; j < kPathsPerLane; ++j) part += (!MASKED || j < nvalid) ? x[j] : Real(0);
@@ -305,6 +309,11 @@ __device__ void simulate_contract(const EngineArgs& a, const Contract& c, uint64
     for (int i = 0; i < kAcc; ++i) acc[i] = 0.0;
     int64_t chunk = p_begin;
     if (nrows == kRowBlock) {  // branch-free fast path: whole 16-row block, whole 2048-path chunks
+      if (T == kRowBlock && store_all) {  // the training shape: straight-line block, every row stored
+        for (; chunk < full_end; chunk += kChunk)
+          lane_paths<Real, LOG_EULER, HW, ALLROWS, false, true, true>(a, step, x0, ordinal, chunk, kPathsPerLane, 0,
+                                                                      kRowBlock, base, acc);
+      }
       for (; chunk < full_end; chunk += kChunk)
         lane_paths<Real, LOG_EULER, HW, ALLROWS, false, true>(a, step, x0, ordinal, chunk, kPathsPerLane, t0, nrows,
                                                               base, acc);
