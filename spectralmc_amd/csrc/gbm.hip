@@ -377,14 +377,26 @@ template <typename Real>
 __device__ void dft_row(const double* avg, const double* cs, const double* sn, int N,
                         typename Complex2<Real>::type* out) {
   using C2 = typename Complex2<Real>::type;
-  for (int k = threadIdx.x; k <= N / 2; k += kThreads) {
-    double re = 0.0, im = 0.0;
-    int idx = 0;
+  // bins k = 0..N/2-1 over the threads; when N/2 is a multiple of the workgroup the Nyquist bin
+  // N/2 would take a whole extra pass for one thread, so thread 0 runs its chain inside its k = 0
+  // loop instead (same fma sequence per chain: same bits)
+  const int kmax = N / 2;
+  const bool fuse_nyq = kmax % kThreads == 0;
+  for (int k = threadIdx.x; k < kmax || (!fuse_nyq && k == kmax); k += kThreads) {
+    const bool nyq = fuse_nyq && k == 0;
+    double re = 0.0, im = 0.0, rq = 0.0, iq = 0.0;
+    int idx = 0, iqx = 0;
     for (int n = 0; n < N; ++n) {
       re = fma(avg[n], cs[idx], re);
       im = fma(-avg[n], sn[idx], im);
       idx += k;
       if (idx >= N) idx -= N;
+      if (nyq) {
+        rq = fma(avg[n], cs[iqx], rq);
+        iq = fma(-avg[n], sn[iqx], iq);
+        iqx += kmax;
+        if (iqx >= N) iqx -= N;
+      }
     }
     C2 v;
     v.x = static_cast<Real>(re);
@@ -393,6 +405,11 @@ __device__ void dft_row(const double* avg, const double* cs, const double* sn, i
     if (k != 0 && 2 * k != N) {
       v.y = static_cast<Real>(-im);
       out[N - k] = v;
+    }
+    if (nyq) {
+      v.x = static_cast<Real>(rq);
+      v.y = static_cast<Real>(iq);
+      out[kmax] = v;
     }
   }
 }
