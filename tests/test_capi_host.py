@@ -124,6 +124,28 @@ def test_train_targets_kernel_choice() -> None:
     assert L.smc_train_targets_kernel(16, 6, 6144, 0, 0, 0) == b"contract_kernel"      # N not 2^k
 
 
+def test_basket_entry_points_validate_before_any_device_work() -> None:
+    """Bad basket arguments are rejected on the host (no GPU needed): asset count, shapes, math."""
+    L = _lib.lib()
+    assert L.smc_basket_resident_slots(0, 256, 0) == -1
+    assert L.smc_basket_resident_slots(9, 256, 0) == -1
+    assert L.smc_basket_resident_slots(4, 0, 0) == -1
+    assert L.smc_basket_resident_slots(4, 8192, 0) == -1
+    fake = 1 << 20  # never dereferenced: validation fails first
+    assert L.smc_basket_train_targets(None, 1, 4, 16, 256, 8, 7, None, 0, 0, 1, 2, fake, 0, 1, None, fake,
+                                      None) == 1
+    assert L.smc_basket_train_targets(fake, 1, 0, 16, 256, 8, 7, None, 0, 0, 1, 2, fake, 0, 1, None, fake,
+                                      None) == 1
+    assert L.smc_basket_train_targets(fake, 1, 4, 16, 256, 3, 7, None, 0, 0, 1, 2, fake, 0, 1, None, fake,
+                                      None) == 2  # N*M not a multiple of 2048
+    assert L.smc_basket_train_targets(fake, 1, 4, 16, 256, 8, 7, None, 0, 7, 1, 2, fake, 0, 1, None, fake,
+                                      None) == 1  # bad math flag
+    assert L.smc_basket_train_targets(fake, 1, 4, 16, 256, 8, 7, None, 0, 0, 1, 3, fake, 0, 1, None, fake,
+                                      None) == 1  # bad store mode
+    assert L.smc_basket_train_targets(fake, 1, 4, 16, 256, 8, 7, None, 0, 0, 1, 2, fake, 100, 1, None, fake,
+                                      None) == 2  # pitch < P
+
+
 def test_engine_workspace_size_and_check() -> None:
     """Sliced contracts (8192-path workgroup slices): f64 slice sums + a u32 arrival counter
     per contract; too small a workspace is a shape error raised before any launch."""
