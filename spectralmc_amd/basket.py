@@ -14,7 +14,10 @@ per chunk of contracts, after the Sobol draw; no host synchronisation.
 
 ``BasketEngine`` has the interface of ``engine.TrainingEngine`` (``buffers``,
 ``enqueue_step``, ``set_position``, ``global_batch``), so a ``GbmCVNNPricer`` whose CVNN has
-3A+4 inputs trains on baskets through ``use_basket_engine``.
+3A+4 inputs trains on baskets through ``use_basket_engine``.  Snapshots of such a pricer
+record the network, optimizer and Sobol/normal positions as usual but not the basket
+configuration: call ``use_basket_engine`` again on the restored pricer.  ``predict_price``
+stays single-asset (the reference has no basket pricing API).
 """
 
 from __future__ import annotations
