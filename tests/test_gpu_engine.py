@@ -85,6 +85,8 @@ PATH_CASES = [
     # (T, P, scheme, dtype)
     (16, 1024, 0, "float32"),     # T specialised kernel, C1 paths
     (16, 3000, 1, "float32"),     # simple Euler, ragged last chunk
+    (16, 4096, 0, "float32"),     # straight-line 16-row block, two full chunks, all row sums
+    (16, 4096, 0, "float64"),     # the same block in f64
     (1, 513, 0, "float32"),       # T = 1, P % 4 != 0 -> scalar stores
     (20, 4196, 0, "float32"),     # two row blocks (16 + 4), ragged paths
     (100, 64, 1, "float32"),      # seven row blocks with step replay
