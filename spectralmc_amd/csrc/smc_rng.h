@@ -137,6 +137,8 @@ struct PathStream {
 #if defined(SMC_EXPERIMENT_NO_RNG)
       s0 += 0x9E3779B9u;
       const uint32_t ua = s0, ub = s0 ^ s1;
+#elif defined(SMC_EXPERIMENT_HALF_RNG)  // timing only: one generator step per Box-Muller pair
+      const uint32_t ua = next(), ub = __builtin_rotateleft32(ua, 16) ^ 0x9E3779B9u;
 #else
       const uint32_t ua = next(), ub = next();
 #endif
