@@ -133,8 +133,8 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
 /* Workspace bytes smc_train_targets needs for sliced contracts (0: P too small to slice). */
 int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, int64_t n_paths,
                                    int32_t all_rows);
-/* Name of the kernel smc_train_targets launches for this shape ("pipelined_kernel",
- * "contract_kernel" or "queue_kernel"; sliced = a workspace is passed).  Static string. */
+/* Name of the kernel smc_train_targets launches for this shape ("contract_kernel" or
+ * "queue_kernel"; sliced = a workspace is passed).  Static string. */
 const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, int64_t n_paths,
                                      int32_t dtype, int64_t path_pitch, int32_t sliced);
 /* Recommended row pitch (elements) for a path scratch buffer of n_paths columns: the row

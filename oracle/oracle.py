@@ -152,10 +152,13 @@ def normalize_paths(contracts: np.ndarray, paths: np.ndarray, rowsum: np.ndarray
     return out
 
 
-def cf_targets(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndarray, network_size: int,
+def cf_targets(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndarray | None, network_size: int,
                batches: int, normalize: bool = True) -> np.ndarray:
     """Per contract: put payoff on the (normalised) terminal row, FFT of each of the M batch
-    rows of length N, mean over batches (gbm.py:464-474, gbm_trainer.py:814-817)."""
+    rows of length N, mean over batches (gbm.py:464-474, gbm_trainer.py:814-817).
+
+    terminal_sum None: the row mean is ``numpy.mean`` of the stored terminal row in the sim
+    dtype (gbm.py:437 ``cp.mean(sims, axis=1)`` on the CPU path: pairwise, dtype accumulator)."""
     dt_np = terminal.dtype.type
     B, P = terminal.shape
     assert P == network_size * batches
@@ -167,7 +170,7 @@ def cf_targets(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.nda
     F = X0.astype(dt_np) * np.exp((r - d).astype(dt_np) * Tm)
     df = np.exp((-r).astype(dt_np) * Tm)
     if normalize:
-        mean = (terminal_sum / P).astype(dt_np)
+        mean = terminal.mean(axis=1) if terminal_sum is None else (terminal_sum / P).astype(dt_np)
         scale = (F / mean).astype(dt_np)
         sims_T = (terminal * scale[:, None]).astype(dt_np)
     else:
@@ -181,10 +184,12 @@ def cf_targets(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.nda
 def training_targets(contracts: np.ndarray, timesteps: int, network_size: int, batches: int, seed: int,
                      ordinal0: int = 0, scheme: int = 0, normalize: bool = True, dtype: str = "float32",
                      threads: int = 0) -> np.ndarray:
-    """The Monte-Carlo side of one training step for a batch of contracts."""
-    _, terminal, rowsum = gbm_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme, dtype,
-                                    want_paths=False, threads=threads)
-    return cf_targets(contracts, terminal, rowsum[:, -1], network_size, batches, normalize)
+    """The Monte-Carlo side of one training step for a batch of contracts, as the reference CPU
+    path computes it (pinned bit-for-bit by tests/golden/gbm_golden.npz, made by the
+    reference's own gbm.py + _simulate_fft on these normals)."""
+    _, terminal, _ = gbm_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme, dtype,
+                               want_paths=False, threads=threads)
+    return cf_targets(contracts, terminal, None, network_size, batches, normalize)
 
 
 # --------------------------------------------------------------------------- kernel mode

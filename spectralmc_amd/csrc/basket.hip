@@ -268,241 +268,15 @@ __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kerne
   }
 }
 
-// ---- persistent variant with the CF phase pipelined (N divides 2048) -------------------------
-// The resident workgroups loop over contracts b = blockIdx.x, + gridDim.x, ...  While simulating
-// contract b chunk by chunk, each thread re-reads its OWN terminal stores of the same chunk of its
-// previous contract (A dwordx4, same thread and addresses: program order) and adds that
-// contract's basket payoffs to 4 column sums.  With N | 2048 thread tid's paths of a chunk are
-// columns 4q..4q+3 (q = tid mod N/4) of batch m = chunk/N + tid div N/4, so a thread visits its
-// batches in ascending m, as the item (q, g) of basket_kernel's CF phase: bit-identical targets.
-// The CF re-read (2 MB per contract at C5) then streams under the next contract's stores instead
-// of after a drain.
-__device__ __forceinline__ void blds_barrier() {  // LDS-only: no vmcnt drain of the path stores
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-template <int A, bool HW>
-__global__ __launch_bounds__(kBThreads, 4) void basket_pipelined_kernel(BasketArgs a) {  // <= 128 VGPRs: 2 per CU
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  extern __shared__ double lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int T = a.T, N = a.N, M = a.M;
-  const int64_t P = a.P;
-  double* Ld = lds;                              // [8][8]
-  double* wsum = Ld + kMaxAssets * kMaxAssets;   // [kBWaves][A]
-  double* part = wsum + kBWaves * A + A;         // [4 kBThreads] = [G][N]
-  double* avg = part + 4 * kBThreads;            // [N]
-  double* cs = avg + N;
-  double* sn = cs + N;
-  for (int j = tid; j < N; j += kBThreads) math::twiddle(j, N, sn[j], cs[j]);
-  const int Q = N / 4, G = kBChunk / N;
-  const int q = tid % Q, g = tid / Q;
-  const int64_t pitch = a.pitch;
-  const int64_t rows = a.store_all ? T : 1;
-  const uint32_t lane_off = static_cast<uint32_t>(kBPaths * sizeof(float)) * tid;
-  constexpr double zscale = HW ? PathStream::kNormalScale<true> : 1.0;
-  const float wA = static_cast<float>(1.0 / A);
-
-  int64_t prev = -1;
-  const float* prev_term = nullptr;  // asset 0's terminal row of the previous contract
-  float psc[A], pK = 0.0f, pdf = 0.0f;
-  double colsum[4];
-
-  auto payoff4 = [&](const v4f (&v)[A], bool live) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float bs = 0.0f;
-#pragma unroll
-      for (int i = 0; i < A; ++i) bs = bs + v[i][e] * psc[i];
-      const float diff = pK - bs * wA;
-      const double pay = static_cast<double>(pdf * (diff > 0.0f ? diff : 0.0f));
-      colsum[e] += live ? pay : 0.0;
-    }
-  };
-  auto finish_cf = [&](int64_t pb) {  // column sums -> batch mean -> DFT -> targets row pb
-#pragma unroll
-    for (int e = 0; e < 4; ++e) part[g * N + 4 * q + e] = colsum[e];
-    blds_barrier();
-    for (int n = tid; n < N; n += kBThreads) {
-      double t2 = 0.0;
-      for (int gg = 0; gg < G; ++gg) t2 += part[gg * N + n];
-      avg[n] = t2 / static_cast<double>(M);
-    }
-    blds_barrier();
-    float2* out = a.targets + pb * N;
-    for (int k = tid; k <= N / 2; k += kBThreads) {
-      double re = 0.0, im = 0.0;
-      int idx = 0;
-      for (int n = 0; n < N; ++n) {
-        re = fma(avg[n], cs[idx], re);
-        im = fma(-avg[n], sn[idx], im);
-        idx += k;
-        if (idx >= N) idx -= N;
-      }
-      out[k] = make_float2(static_cast<float>(re), static_cast<float>(im));
-      if (k != 0 && 2 * k != N) out[N - k] = make_float2(static_cast<float>(re), static_cast<float>(-im));
-    }
-    blds_barrier();  // part / avg are reused
-  };
-
-  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    const double* c = a.contracts + b * (3 * A + 4);
-    const double K = c[0], Tm = c[1], r = c[2], rho = c[3];
-    if (tid == 0) cholesky_equicorr(A, rho, Ld);
-    blds_barrier();
-    const double dt = Tm / static_cast<double>(T);
-    const double sq = sqrt(dt);
-    float ca[A], x0[A], Lb[A][A];
-#pragma unroll
-    for (int i = 0; i < A; ++i) {
-      const double v = c[4 + 2 * A + i], d = c[4 + A + i];
-      const double drift = r - d - 0.5 * v * v;
-      ca[i] = static_cast<float>(drift * dt * kBLog2e);
-      const double bi = v * sq * kBLog2e * zscale;
-      x0[i] = static_cast<float>(c[4 + i]);
-#pragma unroll
-      for (int k = 0; k < A; ++k) Lb[i][k] = k <= i ? static_cast<float>(bi * Ld[i * kMaxAssets + k]) : 0.0f;
-    }
-    const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
-    float* cbase = a.paths + b * A * rows * pitch;
-    const float* term = cbase + (rows - 1) * pitch;
-    const bool have_prev = prev >= 0;
-    const float* src = have_prev ? prev_term : term;  // unconditional loads; discarded the first time
-    double acc[A];
-#pragma unroll
-    for (int i = 0; i < A; ++i) acc[i] = 0.0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) colsum[e] = 0.0;
-
-    for (int64_t chunk = 0; chunk < P; chunk += kBChunk) {
-      v4f pv[A];
-#pragma unroll
-      for (int i = 0; i < A; ++i)
-        pv[i] = *reinterpret_cast<const v4f*>(src + i * rows * pitch + chunk + kBPaths * tid);
-      PathStream s(a.seed, ordinal, static_cast<uint64_t>(chunk / kBPaths + tid));
-      float x[A][kBPaths];
-#pragma unroll
-      for (int i = 0; i < A; ++i)
-#pragma unroll
-        for (int j = 0; j < kBPaths; ++j) x[i][j] = x0[i];
-      for (int t = 0; t < T; ++t) {
-#pragma unroll
-        for (int j = 0; j < kBPaths; j += 2) {
-          float z0[A + 1], z1[A + 1];
-#pragma unroll
-          for (int k = 0; k < A; k += 2) s.template normal_pair<HW>(z0[k], z0[k + 1]);
-#pragma unroll
-          for (int k = 0; k < A; k += 2) s.template normal_pair<HW>(z1[k], z1[k + 1]);
-#pragma unroll
-          for (int i = 0; i < A; ++i) {
-            f2 y = {ca[i], ca[i]};
-#pragma unroll
-            for (int k = 0; k <= i; ++k) y = __builtin_elementwise_fma(f2{Lb[i][k], Lb[i][k]}, f2{z0[k], z1[k]}, y);
-            f2 e;
-            if constexpr (HW) e = f2{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
-            else e = f2{math::exp2_any(y.x), math::exp2_any(y.y)};
-            const f2 xv = f2{x[i][j], x[i][j + 1]} * e;
-            x[i][j] = xv.x;
-            x[i][j + 1] = xv.y;
-          }
-        }
-        if (a.store_all || t == T - 1) {
-          const int64_t row = a.store_all ? t : 0;
-#pragma unroll
-          for (int i = 0; i < A; ++i) {
-            const v4f v = {x[i][0], x[i][1], x[i][2], x[i][3]};
-            char* rb = reinterpret_cast<char*>(cbase + (i * rows + row) * pitch + chunk);
-            *reinterpret_cast<v4f*>(rb + lane_off) = v;
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < A; ++i) {
-        float p = 0.0f;
-#pragma unroll
-        for (int j = 0; j < kBPaths; ++j) p += x[i][j];
-        acc[i] += static_cast<double>(p);
-      }
-      payoff4(pv, have_prev);
-    }
-    // terminal sums of contract b: lane over chunks, wave butterfly, waves 0..7
-#pragma unroll
-    for (int i = 0; i < A; ++i) {
-      const double w = bwave_sum(acc[i]);
-      if (lane == 0) wsum[wave * A + i] = w;
-    }
-    blds_barrier();
-    double tot[A];
-#pragma unroll
-    for (int i = 0; i < A; ++i) {
-      double sum = 0.0;
-      for (int w = 0; w < kBWaves; ++w) sum += wsum[w * A + i];
-      tot[i] = sum;
-    }
-    if (a.terminal_sum) {
-#pragma unroll
-      for (int i = 0; i < A; ++i)
-        if (tid == i) a.terminal_sum[b * A + i] = tot[i];
-    }
-    blds_barrier();  // wsum / Ld are rewritten for the next contract
-    if (have_prev) finish_cf(prev);
-    // this contract becomes the pending CF phase
-    const float Tf = static_cast<float>(Tm);
-    pdf = math::exp_any(static_cast<float>(-r) * Tf);
-    pK = static_cast<float>(K);
-#pragma unroll
-    for (int i = 0; i < A; ++i) {
-      const float F = static_cast<float>(c[4 + i]) * math::exp_any(static_cast<float>(r - c[4 + A + i]) * Tf);
-      psc[i] = a.normalize ? F / static_cast<float>(tot[i] / static_cast<double>(P)) : 1.0f;
-    }
-    prev = b;
-    prev_term = term;
-  }
-  if (prev >= 0) {  // the last contract: its own re-read, kB chunks in flight per thread
-    constexpr int kB = A <= 2 ? 8 : (A <= 4 ? 4 : 2);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) colsum[e] = 0.0;
-    for (int64_t c0 = 0; c0 < P; c0 += kB * kBChunk) {
-      v4f v[kB][A];
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        const int64_t chunk = c0 + u * kBChunk < P ? c0 + u * kBChunk : P - kBChunk;
-#pragma unroll
-        for (int i = 0; i < A; ++i)
-          v[u][i] = *reinterpret_cast<const v4f*>(prev_term + i * rows * pitch + chunk + kBPaths * tid);
-      }
-#pragma unroll
-      for (int u = 0; u < kB; ++u) payoff4(v[u], c0 + u * kBChunk < P);
-    }
-    finish_cf(prev);
-  }
-}
-
 size_t basket_lds_bytes(int A, int N) {
   const size_t part = static_cast<size_t>(N > 4 * kBThreads ? N : 4 * kBThreads);
   return (kMaxAssets * kMaxAssets + static_cast<size_t>(kBWaves) * A + A + part + 3 * static_cast<size_t>(N)) *
          sizeof(double);
 }
 
-// The pipelined persistent kernel takes every N dividing 2048 (its thread -> column mapping) and
-// A <= 4 (its prefetched terminal values must fit the 128 VGPRs of two workgroups per CU).
-// Off by default (SMC_BASKET_PIPELINED=1 builds): at A = 4 the kernel needs 128 VGPRs with 19
-// spilled, and on MI355X a C5 launch of 1024 contracts takes 7.96 ms (7.15 ms per 1024 at 2048 per
-// launch) against 7.36 ms for basket_kernel — DESIGN.md §8.
-#ifndef SMC_BASKET_PIPELINED
-#define SMC_BASKET_PIPELINED 0
-#endif
-bool basket_pipelined_ok(int A, int N) {
-  return SMC_BASKET_PIPELINED && A <= 4 && N >= 4 && N <= kBChunk && kBChunk % N == 0;
-}
-
 template <int A, bool HW>
-const void* basket_kernel_ptr(int N) {
-  return basket_pipelined_ok(A, N) ? reinterpret_cast<const void*>(basket_pipelined_kernel<A, HW>)
-                                : reinterpret_cast<const void*>(basket_kernel<A, HW>);
+const void* basket_kernel_ptr() {
+  return reinterpret_cast<const void*>(basket_kernel<A, HW>);
 }
 
 // Workgroups of the kernel launched for <A, HW, N> resident on the current device (occupancy x CUs).
@@ -510,7 +284,7 @@ template <int A, bool HW>
 int64_t basket_slots_k(int N) {
   int dev = 0, cus = 0, per_cu = 0;
   const size_t lds = basket_lds_bytes(A, N);
-  const void* kernel = basket_kernel_ptr<A, HW>(N);
+  const void* kernel = basket_kernel_ptr<A, HW>();
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return (void)hipGetLastError(), -1;
   if (lds > 64 * 1024 &&
@@ -524,13 +298,6 @@ int64_t basket_slots_k(int N) {
 template <int A, bool HW>
 int32_t launch_basket_k(const BasketArgs& a, hipStream_t stream) {
   const size_t lds = basket_lds_bytes(A, a.N);
-  if (basket_pipelined_ok(A, a.N)) {
-    const int64_t slots = basket_slots_k<A, HW>(a.N);  // also raises the LDS limit
-    if (slots <= 0) return fail(SMC_ERR_HIP, "basket_pipelined_kernel: occupancy query failed");
-    const unsigned grid = static_cast<unsigned>(a.B < slots ? a.B : slots);
-    hipLaunchKernelGGL((basket_pipelined_kernel<A, HW>), dim3(grid), dim3(kBThreads), lds, stream, a);
-    return check_launch("basket_pipelined_kernel");
-  }
   auto kernel = basket_kernel<A, HW>;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -379,9 +379,10 @@ __device__ void dft_row(const double* avg, const double* cs, const double* sn, i
   using C2 = typename Complex2<Real>::type;
   // bins k = 0..N/2-1 over the threads; when N/2 is a multiple of the workgroup the Nyquist bin
   // N/2 would take a whole extra pass for one thread, so thread 0 runs its chain inside its k = 0
-  // loop instead (same fma sequence per chain: same bits)
+  // loop instead (same fma sequence per chain: same bits).  Only for even N with kmax > 0: odd N
+  // has no Nyquist bin (bin kmax is an ordinary pair with N - kmax), and N = 1 has only bin 0.
   const int kmax = N / 2;
-  const bool fuse_nyq = kmax % kThreads == 0;
+  const bool fuse_nyq = (N % 2) == 0 && kmax > 0 && kmax % kThreads == 0;
   for (int k = threadIdx.x; k < kmax || (!fuse_nyq && k == kmax); k += kThreads) {
     const bool nyq = fuse_nyq && k == 0;
     double re = 0.0, im = 0.0, rq = 0.0, iq = 0.0;
@@ -605,319 +606,6 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void queue_kernel(EngineA
   }
 }
 
-// ---- training fast path: persistent workgroups, CF phase pipelined into the next contract ----
-// Conditions (pipelined_ok): f32, T <= kRowBlock, P a multiple of kChunk, N a power of two
-// dividing kChunk (N >= 4), terminal-row sums only, targets requested, no slices.
-// Each of the gridDim.x resident workgroups runs contracts b = blockIdx.x, + gridDim.x, ...
-// While it simulates contract b, chunk by chunk, every thread re-reads its OWN 16-B terminal
-// store of the same chunk of the previous contract (same thread, same address: program order,
-// no fence) and adds the put payoffs to 4 column sums; the loads are issued before the chunk's
-// compute and consumed after it, so their latency (long behind the write stream) is hidden
-// and no workgroup ever drains its stores.  Thread tid owns columns 4q..4q+3 (q = tid mod N/4)
-// and batches m = g, g + G, ... (g = tid div N/4, G = kChunk / N) — exactly the quad order of
-// cf_targets_contract, so targets are bit-identical to the unpipelined kernel.
-[[maybe_unused]] __device__ __forceinline__ void lds_barrier() {  // LDS-only: no vmcnt drain of the path stores
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-#ifndef SMC_ROW_POLICY
-#define SMC_ROW_POLICY 0  // tools/micro experiment: 1 = non-temporal stores for the non-terminal rows
-#endif
-
-// One 2048-path chunk of a kRowBlock-step contract: the lane's 4 paths through all steps in
-// straight-line code — no control flow between the caller's prefetch load and its use, so the
-// compiler waits for that load with a counted vmcnt instead of draining the chunk's row stores.
-// Returns the lane's f32 sum of its 4 terminal values (lane_paths' order).
-template <bool LOG_EULER, bool HW, bool STORE_ALL>
-__device__ __forceinline__ float chunk16(const Stepper<float, LOG_EULER, HW>& step, float x0, PathStream& s,
-                                         char* chunk_base, uint32_t lane_off, int64_t pitch_bytes) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  constexpr bool kPacked = HW && LOG_EULER;
-  float x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
-#pragma unroll
-  for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
-#pragma unroll
-  for (int i = 0; i < kRowBlock; ++i) {
-    if constexpr (kPacked) {
-      if ((i & 1) == 0) s.hw_log_increments4(step.b, step.a, zl, zh);
-      advance_packed(x, (i & 1) ? zh : zl);
-    } else {
-      if ((i & 1) == 0) {
-#pragma unroll
-        for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (i & 1) ? zh[j] : zl[j]);
-    }
-    if (STORE_ALL || i == kRowBlock - 1) {
-      const v4f v = {x[0], x[1], x[2], x[3]};
-      v4f* dst = reinterpret_cast<v4f*>(chunk_base + (STORE_ALL ? i * pitch_bytes : 0) + lane_off);
-      if (SMC_ROW_POLICY == 1 && i < kRowBlock - 1) __builtin_nontemporal_store(v, dst);
-      else *dst = v;
-    }
-  }
-  float part = 0.0f;
-#pragma unroll
-  for (int j = 0; j < kPathsPerLane; ++j) part += x[j];
-  return part;
-}
-
-template <bool LOG_EULER, bool HW, bool STORE_ALL>
-__global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void pipelined_kernel(EngineArgs a) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  extern __shared__ double lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int T = kRowBlock;
-  const int N = a.N, M = a.M;
-  const int64_t P = a.P;
-  constexpr bool store_all = STORE_ALL;
-  const int64_t pitch = a.pitch ? a.pitch : P;
-  const int64_t pitch_bytes = pitch * static_cast<int64_t>(sizeof(float));
-  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(float)) * tid;
-  const int G = kChunk / N;  // batches per chunk
-  const int Q = N / 4;
-  const int q = tid % Q, g = tid / Q;
-  double* lds_acc = lds;                // [kWaves]
-  double* part = lds + kWaves;          // [G][N] = [4 kThreads]
-  double* avg = part + 4 * kThreads;    // [N]
-  double* cs = avg + N;                 // [N]
-  double* sn = cs + N;                  // [N]
-  for (int j = tid; j < N; j += kThreads) math::twiddle(j, N, sn[j], cs[j]);  // once per workgroup
-
-  // the pending CF phase (previous contract of this workgroup)
-  int64_t prev = -1;
-  const float* prev_row = nullptr;
-  Payoff<float> prev_pay{};
-  double colsum[4];
-
-  auto finish_cf = [&](int64_t pb) {  // column sums -> batch mean -> DFT -> targets row pb
-#pragma unroll
-    for (int e = 0; e < 4; ++e) part[g * N + 4 * q + e] = colsum[e];
-    lds_barrier();
-    for (int n = tid; n < N; n += kThreads) {
-      double tot = 0.0;
-      for (int gg = 0; gg < G; ++gg) tot += part[gg * N + n];
-      avg[n] = tot / static_cast<double>(M);
-    }
-    lds_barrier();
-    dft_row<float>(avg, cs, sn, N, static_cast<float2*>(a.targets) + pb * N);
-    lds_barrier();  // part / avg are reused by the next contract
-  };
-
-  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    const Contract c = load_contract(a.contracts + b * 6);
-    const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
-    const Stepper<float, LOG_EULER, HW> step(c, T);
-    const float x0 = static_cast<float>(c.X0);
-    float* base = static_cast<float*>(a.paths) + (store_all ? b * T * pitch : b * pitch);
-    const float* term = base + (store_all ? static_cast<int64_t>(T - 1) * pitch : 0);
-    // unconditional prefetch (no branch around the load): the workgroup's first contract reads
-    // its own, not yet written terminal row and discards it
-    const bool have_prev = prev >= 0;
-    const float* src = have_prev ? prev_row : term;
-    double acc = 0.0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) colsum[e] = 0.0;
-    for (int64_t chunk = 0; chunk < P; chunk += kChunk) {
-      const v4f pv = *reinterpret_cast<const v4f*>(src + chunk + 4 * tid);
-      PathStream s(a.seed, ordinal, static_cast<uint64_t>(chunk / kPathsPerLane + tid));
-      acc += static_cast<double>(chunk16<LOG_EULER, HW, STORE_ALL>(step, x0, s, reinterpret_cast<char*>(base + chunk),
-                                                                   lane_off, pitch_bytes));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const double pay = static_cast<double>(prev_pay(pv[e]));
-        colsum[e] += have_prev ? pay : 0.0;
-      }
-    }
-    // terminal-row sum of contract b: lane over chunks, wave butterfly, waves 0..7
-    const double w = wave_sum(acc);
-    if (lane == 0) lds_acc[wave] = w;
-    lds_barrier();
-    double tot = 0.0;
-    for (int ww = 0; ww < kWaves; ++ww) tot += lds_acc[ww];
-    lds_barrier();
-    if (prev >= 0) finish_cf(prev);
-    prev = b;
-    prev_row = term;
-    prev_pay = Payoff<float>(a, c, tot);
-  }
-  if (prev >= 0) {  // the last contract: its own re-read, 16 loads in flight per thread
-    constexpr int kBatch = 16;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) colsum[e] = 0.0;
-    for (int64_t c0 = 0; c0 < P; c0 += kBatch * kChunk) {
-      v4f v[kBatch];
-#pragma unroll
-      for (int u = 0; u < kBatch; ++u) {
-        const int64_t chunk = c0 + u * kChunk < P ? c0 + u * kChunk : P - kChunk;
-        v[u] = *reinterpret_cast<const v4f*>(prev_row + chunk + 4 * tid);
-      }
-#pragma unroll
-      for (int u = 0; u < kBatch; ++u) {
-        if (c0 + u * kChunk < P) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) colsum[e] += static_cast<double>(prev_pay(v[u][e]));
-        }
-      }
-    }
-    finish_cf(prev);
-  }
-}
-
-// ---- experiment (SMC_SPECIALIZED builds): producer / store wave specialisation ------------
-// Waves 0-3 compute (each lane: virtual lanes l and l + 256 of the 512-lane chunk mapping, i.e. the
-// same two 4-path groups and streams as contract_kernel's lanes l and l + 256) and stage each row
-// in an LDS ring; waves 4-7 copy rows from the ring to HBM (same addresses and dwordx4 coalescing)
-// and keep the terminal-row sums of virtual lanes l and l + 256 in contract_kernel's order, so the
-// results are bit-identical.  Counters in LDS (ready / freed per ring slot) decouple the two roles:
-// compute waves never wait on the store queue.  Every spin is bounded, so a protocol error gives
-// wrong numbers, never a hang.
-#ifndef SMC_SPECIALIZED
-#define SMC_SPECIALIZED 0
-#endif
-#if SMC_SPECIALIZED
-#ifndef SMC_RING
-#define SMC_RING 8
-#endif
-constexpr int kRing = SMC_RING;              // staged rows (8 KB each)
-constexpr int kRoleWaves = kWaves / 2;       // waves per role
-constexpr int kRoleLanes = kThreads / 2;
-
-__device__ __forceinline__ void ring_wait(const int* ctr, int target) {
-  for (int it = 0; it < (1 << 16); ++it) {
-    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-__device__ __forceinline__ void ring_signal(int* ctr) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // this wave's LDS accesses done
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-size_t specialized_lds_bytes(int N) {
-  const size_t cf = (static_cast<size_t>(N > 4 * kThreads ? N : 4 * kThreads) + 3 * static_cast<size_t>(N)) *
-                    sizeof(double);
-  const size_t ring = static_cast<size_t>(kRing) * kThreads * 16;
-  return 16 * sizeof(double) + (cf > ring ? cf : ring);
-}
-
-template <bool LOG_EULER, bool HW>
-__global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void specialized_kernel(EngineArgs a) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  extern __shared__ double lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t b = blockIdx.x;
-  constexpr int T = kRowBlock;
-  const int64_t P = a.P;
-  const int64_t pitch = a.pitch ? a.pitch : P;
-  double* lds_acc = lds;                                   // [kWaves]
-  int* ready = reinterpret_cast<int*>(lds + kWaves);       // [kRing]
-  int* freed = ready + kRing;                              // [kRing]
-  v4f* ring = reinterpret_cast<v4f*>(lds + 16);            // [kRing][kThreads]
-  if (tid < 2 * kRing) ready[tid] = 0;
-  __syncthreads();
-  const Contract c = load_contract(a.contracts + b * 6);
-  const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
-  float* base = static_cast<float*>(a.paths) + b * T * pitch;
-  const int64_t nchunks = P / kChunk;
-  if (wave < kRoleWaves) {  // compute
-    const Stepper<float, LOG_EULER, HW> step(c, T);
-    const float x0 = static_cast<float>(c.X0);
-    constexpr bool kPacked = HW && LOG_EULER;
-    for (int64_t ci = 0; ci < nchunks; ++ci) {
-      const int64_t chunk = ci * kChunk;
-      PathStream s0(a.seed, ordinal, static_cast<uint64_t>(chunk / kPathsPerLane + tid));
-      PathStream s1(a.seed, ordinal, static_cast<uint64_t>(chunk / kPathsPerLane + tid + kRoleLanes));
-      float x[2][kPathsPerLane], zl[2][kPathsPerLane], zh[2][kPathsPerLane];
-#pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) x[0][j] = x[1][j] = x0;
-#pragma unroll
-      for (int i = 0; i < kRowBlock; ++i) {
-#if defined(SMC_SPEC_NOCOMPUTE)  // tools/micro decomposition builds only
-#pragma unroll
-        for (int j = 0; j < kPathsPerLane; ++j) x[0][j] = x[1][j] = x0 + static_cast<float>(i);
-        if (false)
-#endif
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          PathStream& s = h ? s1 : s0;
-          if constexpr (kPacked) {
-            if ((i & 1) == 0) s.hw_log_increments4(step.b, step.a, zl[h], zh[h]);
-            advance_packed(x[h], (i & 1) ? zh[h] : zl[h]);
-          } else {
-            if ((i & 1) == 0) {
-#pragma unroll
-              for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[h][j], zh[h][j]);
-            }
-#pragma unroll
-            for (int j = 0; j < kPathsPerLane; ++j) x[h][j] = step(x[h][j], (i & 1) ? zh[h][j] : zl[h][j]);
-          }
-        }
-        const int64_t seq = ci * kRowBlock + i;
-        const int slot = static_cast<int>(seq % kRing);
-        const int use = static_cast<int>(seq / kRing);
-        ring_wait(freed + slot, kRoleWaves * use);
-        ring[slot * kThreads + tid] = v4f{x[0][0], x[0][1], x[0][2], x[0][3]};
-        ring[slot * kThreads + tid + kRoleLanes] = v4f{x[1][0], x[1][1], x[1][2], x[1][3]};
-        ring_signal(ready + slot);
-      }
-    }
-  } else {  // store
-    const int cl = tid - kRoleLanes;
-    const uint32_t off0 = 16u * cl, off1 = 16u * (cl + kRoleLanes);
-    double acc0 = 0.0, acc1 = 0.0;
-    for (int64_t ci = 0; ci < nchunks; ++ci) {
-      const int64_t chunk = ci * kChunk;
-#pragma unroll
-      for (int i = 0; i < kRowBlock; ++i) {
-        const int64_t seq = ci * kRowBlock + i;
-        const int slot = static_cast<int>(seq % kRing);
-        const int use = static_cast<int>(seq / kRing);
-        ring_wait(ready + slot, kRoleWaves * (use + 1));
-        const v4f v0 = ring[slot * kThreads + cl], v1 = ring[slot * kThreads + cl + kRoleLanes];
-        ring_signal(freed + slot);
-        char* row = reinterpret_cast<char*>(base + i * pitch + chunk);
-#if defined(SMC_SPEC_NOSTORE)  // tools/micro decomposition builds only: terminal row only
-        if (i == kRowBlock - 1)
-#endif
-        {
-          *reinterpret_cast<v4f*>(row + off0) = v0;
-          *reinterpret_cast<v4f*>(row + off1) = v1;
-        }
-        if (i == kRowBlock - 1) {
-          float p0 = 0.0f, p1 = 0.0f;
-#pragma unroll
-          for (int j = 0; j < kPathsPerLane; ++j) {
-            p0 += v0[j];
-            p1 += v1[j];
-          }
-          acc0 += static_cast<double>(p0);
-          acc1 += static_cast<double>(p1);
-        }
-      }
-    }
-    const double w0 = wave_sum(acc0), w1 = wave_sum(acc1);
-    if (lane == 0) {
-      lds_acc[wave - kRoleWaves] = w0;               // virtual wave (wave - 4)
-      lds_acc[wave - kRoleWaves + kRoleWaves] = w1;  // virtual wave (wave - 4) + 4
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  double tot = 0.0;
-  for (int w = 0; w < kWaves; ++w) tot += lds_acc[w];
-  __syncthreads();  // the ring is dead; the CF phase reuses it
-#if defined(SMC_EXPERIMENT_NO_CF)
-  if (false)
-#endif
-  cf_targets_contract<float>(a, c, b, tot, lds + 16);
-}
-#endif  // SMC_SPECIALIZED
-
 // In-place forward normalisation of a stored [B][T][P] matrix (gbm.py:428-438).
 template <typename Real>
 __global__ __launch_bounds__(256) void normalize_kernel(const double* __restrict__ contracts, int64_t B,
@@ -1045,80 +733,9 @@ size_t workspace_bytes(int64_t B, int32_t T, int64_t P, bool all_rows) {
   return static_cast<size_t>(B) * W * (all_rows ? T : 1) * sizeof(double) + static_cast<size_t>(B + 16) * sizeof(uint32_t);
 }
 
-[[maybe_unused]] bool pipelined_ok(const EngineArgs& a, bool f32) {
-  const bool pow2 = a.N >= 4 && (a.N & (a.N - 1)) == 0 && a.N <= kChunk;
-  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T == kRowBlock && pow2 &&
-         a.P % kChunk == 0 && (a.pitch == 0 || a.pitch % 4 == 0);
-}
-
-[[maybe_unused]] size_t pipelined_lds_bytes(int N) {
-  return (static_cast<size_t>(kWaves) + 4 * static_cast<size_t>(kThreads) + 3 * static_cast<size_t>(N)) *
-         sizeof(double);
-}
-
-template <bool LOG_EULER, bool HW, bool STORE_ALL>
-int32_t launch_pipelined_k(const EngineArgs& a, hipStream_t stream) {
-  auto kernel = pipelined_kernel<LOG_EULER, HW, STORE_ALL>;
-  const size_t lds = pipelined_lds_bytes(a.N);
-  if (lds > 64 * 1024 &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          static_cast<int>(lds)) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(SMC_ERR_HIP, "pipelined_kernel: cannot raise the dynamic LDS limit");
-  }
-  unsigned grid = 0;
-  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), lds, a.B, &grid)) return st;
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), lds, stream, a);
-  return check_launch("pipelined_kernel");
-}
-
-#if SMC_SPECIALIZED
-template <bool LOG_EULER, bool HW>
-int32_t launch_specialized_k(const EngineArgs& a, hipStream_t stream) {
-  auto kernel = specialized_kernel<LOG_EULER, HW>;
-  const size_t lds = specialized_lds_bytes(a.N);
-  if (lds > 64 * 1024 &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          static_cast<int>(lds)) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(SMC_ERR_HIP, "specialized_kernel: cannot raise the dynamic LDS limit");
-  }
-  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds, stream, a);
-  return check_launch("specialized_kernel");
-}
-#endif
-
 template <typename Real>
 int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   if (a.B == 0) return SMC_OK;
-#if SMC_SPECIALIZED
-  if (pipelined_ok(a, sizeof(Real) == 4) && a.store == SMC_STORE_ALL && specialized_lds_bytes(a.N) <= kMaxLds) {
-    const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
-    const bool hw = (a.scheme & SMC_MATH_HW) != 0;
-    if (log_euler && hw) return launch_specialized_k<true, true>(a, stream);
-    if (log_euler) return launch_specialized_k<true, false>(a, stream);
-    if (hw) return launch_specialized_k<false, true>(a, stream);
-    return launch_specialized_k<false, false>(a, stream);
-  }
-#endif
-#if defined(SMC_PIPELINE)  // opt-in: slower than contract_kernel on MI355X
-  if (pipelined_ok(a, sizeof(Real) == 4)) {
-    const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
-    const bool hw = (a.scheme & SMC_MATH_HW) != 0;
-    const bool sa = a.store == SMC_STORE_ALL;
-#define SMC_PIPE(LE, HWM, SA) \
-  if (log_euler == LE && hw == HWM && sa == SA) return launch_pipelined_k<LE, HWM, SA>(a, stream);
-    SMC_PIPE(true, true, true)
-    SMC_PIPE(true, true, false)
-    SMC_PIPE(true, false, true)
-    SMC_PIPE(true, false, false)
-    SMC_PIPE(false, true, true)
-    SMC_PIPE(false, true, false)
-    SMC_PIPE(false, false, true)
-    SMC_PIPE(false, false, false)
-#undef SMC_PIPE
-  }
-#endif
   if (a.slices < 1 || !a.simulate) a.slices = 1;
   if (a.slices > 1 && (!a.partials || !a.arrivals || !a.queues))
     return fail(SMC_ERR_INVALID_ARGUMENT, "engine: sliced contracts need a workspace");
@@ -1275,9 +892,6 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.targets = &a;  // any non-null: the training call always writes targets
   a.pitch = path_pitch;
   a.slices = slices_for(n_paths, sliced != 0);
-#if defined(SMC_PIPELINE)
-  if (pipelined_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "pipelined_kernel";
-#endif
   return a.slices > 1 ? "queue_kernel" : "contract_kernel";
 }
 

@@ -106,7 +106,7 @@ class TrainingEngine:
         self.paths = self._paths_buf[..., :self.P]  # (chunk, T, P) / (chunk, P) strided view
         # sliced=True: each contract runs as several workgroups (slice row sums + arrival counters
         # in a workspace); the default one-workgroup-per-contract launch takes the
-        # contract_kernel (the pipelined variant is an opt-in SMC_PIPELINE build: slower on MI355X)
+        # contract_kernel
         ws = int(_lib.lib().smc_engine_workspace_bytes(self.chunk, self.T, self.P, 0)) if sliced else 0
         self._workspace = torch.zeros(max(ws, 8), dtype=torch.uint8, device=device) if ws else None
         self._workspace_bytes = ws

@@ -19,6 +19,15 @@ What is taken from the reference, and how:
 * Training step: ``_torch_step`` (gbm_trainer.py:819-835) restated on the reference modules
   (gbm_trainer.py itself needs aioboto3 / CUDA streams).
 
+* GBM / CF targets (``gbm_golden.npz``): the reference's own ``spectralmc.gbm`` (BlackScholes
+  engine, ``SimulateBlackScholes`` kernel body, normalisation, payoff; gbm.py:224-257,400-488)
+  and ``async_normals`` pool, imported behind the CPU shims of ``ref_shim.py`` (cupy -> numpy,
+  numba.cuda.jit -> serial grid emulator with Numba's f64-compute / dtype-store typing), fed
+  with the BUILD's normal matrices through the shimmed ``default_rng(...).standard_normal``.
+  ``_simulate_fft`` (gbm_trainer.py:814-817) is restated as its one line on the engine output.
+  One full C1 training step pair comes from the reference ``cvnn_factory.build_model`` (now
+  importable through the same shims) + ``_torch_step`` restated (gbm_trainer.py:819-835).
+
 Nothing from the reference is copied into the repository: only the numbers it produced.
 """
 
@@ -31,8 +40,37 @@ import types
 import numpy as np
 import torch
 
-REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference/src"
-OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.npz")
+REF = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "/root/reference/src"
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "golden.npz")
+OUT_GBM = os.path.join(HERE, "gbm_golden.npz")
+
+# (name, timesteps, network_size, batches, dtype, scheme, normalization, mc_seed, ordinal0, contract rows)
+# contract rows: a slice of the reference-sampler Sobol points (seed 7, skip 0) or explicit rows.
+EDGE_ROWS = np.array([
+    [100.0, 100.0, 0.0, 0.05, 0.01, 0.4],     # T = 0 maturity: every path stays X0
+    [100.0, 110.0, 1.5, 0.03, 0.01, 0.0],     # v = 0: deterministic forward
+    [100.0, 0.001, 2.0, 0.02, 0.00, 0.3],     # deep OTM put: all-zero targets
+    [10.0, 20_000.0, 3.0, -0.1, 0.05, 1.5],   # deep ITM, high vol
+    [0.001, 0.002, 10.0, 0.2, -0.2, 2.0],     # domain corner
+])
+GBM_CASES = (
+    ("e2e", 16, 128, 4, "float32", "log_euler", "normalize", 7, 0, slice(0, 16)),
+    ("c1", 16, 256, 4, "float32", "log_euler", "normalize", 7, 0, slice(0, 64)),
+    ("raw", 16, 64, 4, "float32", "log_euler", "raw", 7, 5, slice(16, 24)),
+    ("euler", 16, 64, 4, "float32", "simple_euler", "normalize", 7, 0, slice(24, 32)),
+    ("f64", 16, 128, 4, "float64", "log_euler", "normalize", 7, 0, slice(0, 8)),
+    ("f64euler", 5, 64, 4, "float64", "simple_euler", "raw", 31, 3, slice(8, 16)),
+    ("edge", 16, 64, 4, "float32", "log_euler", "normalize", 7, 0, "edge"),
+    ("edgef64", 16, 64, 4, "float64", "log_euler", "normalize", 7, 0, "edge"),
+    ("t1", 1, 16, 64, "float32", "log_euler", "normalize", 9, 100, slice(32, 40)),
+    ("t3", 3, 256, 4, "float32", "log_euler", "normalize", 7, 0, slice(40, 44)),
+    ("n1", 4, 1, 64, "float32", "log_euler", "normalize", 7, 0, slice(44, 48)),
+    ("n5", 4, 5, 16, "float32", "log_euler", "normalize", 7, 0, slice(48, 52)),
+    ("n1025", 4, 1025, 2, "float32", "log_euler", "normalize", 7, 0, slice(52, 54)),
+    ("c2shape", 16, 256, 256, "float32", "log_euler", "normalize", 7, 0, slice(0, 2)),
+    ("c3shape", 16, 1024, 256, "float32", "log_euler", "normalize", 7, 0, slice(2, 3)),
+)
 
 
 def main() -> None:
@@ -136,5 +174,98 @@ def main() -> None:
     print(f"wrote {OUT}: {len(out)} arrays, {os.path.getsize(OUT)} bytes")
 
 
+def main_gbm() -> None:
+    """CF targets and a C1 training step pair from the reference's own gbm.py (shimmed)."""
+    import time
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))  # repo root: oracle (normals)
+    sys.path.insert(0, HERE)
+    import ref_shim
+
+    ref_shim.install(REF)
+    from spectralmc import gbm
+    from spectralmc.cvnn_factory import ActivationCfg, ActivationKind, ExplicitWidth, LinearCfg, build_cvnn_config
+    from spectralmc.cvnn_factory import build_model
+    from spectralmc.effects import ForwardNormalization, PathScheme
+    from spectralmc.models.numerical import Precision
+    from spectralmc.models.torch import FullPrecisionDType
+    from spectralmc.sobol_sampler import SobolSampler, build_bound_spec, build_domain_bounds, build_sobol_config
+
+    fields = ("X0", "K", "T", "r", "d", "v")
+    default_bounds = {"X0": (0.001, 10_000.0), "K": (0.001, 20_000.0), "T": (0.0, 10.0), "r": (-0.20, 0.20),
+                      "d": (-0.20, 0.20), "v": (0.0, 2.0)}
+    bounds = build_domain_bounds(gbm.BlackScholes.Inputs,
+                                 {f: build_bound_spec(*default_bounds[f]).unwrap() for f in fields}).unwrap()
+    sampler = SobolSampler.create(gbm.BlackScholes.Inputs, bounds,
+                                  config=build_sobol_config(seed=7, skip=0).unwrap()).unwrap()
+    step_contracts = [sampler.sample(64).unwrap() for _ in range(2)]  # the trainer's first two C1 batches
+    sobol_rows = np.array([[getattr(p, f) for f in fields] for p in step_contracts[0]])
+
+    def engine(T: int, N: int, M: int, dtype: str, scheme: str, norm: str, seed: int, ordinal0: int):
+        ref_shim.SOURCE.seed, ref_shim.SOURCE.next_ordinal = seed, ordinal0
+        sp = gbm.build_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=M, threads_per_block=256,
+                                         mc_seed=seed, buffer_size=1, dtype=Precision(dtype)).unwrap()
+        cfg = gbm.build_black_scholes_config(sim_params=sp, path_scheme=PathScheme(scheme),
+                                             normalization=ForwardNormalization.NORMALIZE if norm == "normalize" else ForwardNormalization.RAW).unwrap()
+        return gbm.BlackScholes(cfg)
+
+    def simulate_fft(eng, row: np.ndarray, N: int, M: int) -> np.ndarray:
+        """GbmCVNNPricer._simulate_fft (gbm_trainer.py:806-817) on the engine's price()."""
+        pricing = eng.price(inputs=gbm.BlackScholes.Inputs(**dict(zip(fields, (float(x) for x in row))))).unwrap()
+        mat = pricing.put_price.reshape(M, N)
+        return np.mean(np.fft.fft(mat, axis=1), axis=0)
+
+    out: dict[str, np.ndarray] = {}
+    for name, T, N, M, dtype, scheme, norm, seed, ordinal0, rows in GBM_CASES:
+        t0 = time.time()
+        contracts = EDGE_ROWS if isinstance(rows, str) else sobol_rows[rows]
+        eng = engine(T, N, M, dtype, scheme, norm, seed, ordinal0)
+        targets = np.stack([simulate_fft(eng, row, N, M) for row in contracts])
+        out[f"{name}_contracts"] = contracts
+        out[f"{name}_targets"] = targets
+        out[f"{name}_meta"] = np.array([T, N, M, int(dtype == "float64"), int(scheme == "simple_euler"),
+                                        int(norm == "normalize"), seed, ordinal0], dtype=np.int64)
+        print(f"  {name}: {contracts.shape[0]} contracts, targets {targets.dtype}, {time.time() - t0:.1f} s",
+              flush=True)
+
+    # one C1 training-step pair: T=16, N=256, M=4, B=64, mc_seed 7, e2e CVNN (6 -> 32 modReLU -> 256, seed 123)
+    import torch
+
+    T, N, M = 16, 256, 4
+    eng = engine(T, N, M, "float32", "log_euler", "normalize", 7, 0)
+    cfg = build_cvnn_config(dtype=FullPrecisionDType.float32,
+                            layers=[LinearCfg(width=ExplicitWidth(value=32),
+                                              activation=ActivationCfg(kind=ActivationKind.MOD_RELU)),
+                                    LinearCfg(width=ExplicitWidth(value=N))], seed=123).unwrap()
+    net = build_model(n_inputs=6, n_outputs=N, cfg=cfg).unwrap()
+    for k, v in net.state_dict().items():
+        out[f"step_init__{k}"] = v.detach().numpy().copy()
+    adam = torch.optim.Adam(net.parameters(), lr=1e-2)
+    for s, batch in enumerate(step_contracts):
+        rows = np.array([[getattr(p, f) for f in fields] for p in batch])
+        targets = np.stack([simulate_fft(eng, row, N, M) for row in rows])
+        x = torch.tensor(rows, dtype=torch.float32)
+        y = torch.from_numpy(targets)
+        pr, pi = net(x, torch.zeros_like(x))
+        loss = torch.nn.functional.mse_loss(pr, torch.real(y)) + torch.nn.functional.mse_loss(pi, torch.imag(y))
+        adam.zero_grad(set_to_none=True)
+        loss.backward()
+        adam.step()
+        gn = float(torch.nn.utils.clip_grad_norm_(net.parameters(), float("inf")))
+        out[f"step{s}_contracts"] = rows
+        out[f"step{s}_targets"] = targets
+        out[f"step{s}_loss"] = np.array(float(loss.item()))
+        out[f"step{s}_gradnorm"] = np.array(gn)
+        for k, v in net.state_dict().items():
+            out[f"step{s}_after__{k}"] = v.detach().numpy().copy()
+        print(f"  C1 step {s}: loss {float(loss):.6e} grad-norm {gn:.6e}", flush=True)
+
+    np.savez_compressed(OUT_GBM, **out)
+    print(f"wrote {OUT_GBM}: {len(out)} arrays, {os.path.getsize(OUT_GBM)} bytes")
+
+
 if __name__ == "__main__":
-    main()
+    if "--gbm-only" not in sys.argv:
+        main()
+    if "--no-gbm" not in sys.argv:
+        main_gbm()

@@ -32,6 +32,40 @@ def test_library_exports_every_declared_symbol() -> None:
     assert L.smc_abi_version() == _lib.ABI_VERSION
 
 
+INTEGRATION = os.path.join(os.path.dirname(HEADER), "..", "INTEGRATION.md")
+_CTYPES = {"c_int32": ctypes.c_int32, "c_int64": ctypes.c_int64, "c_uint64": ctypes.c_uint64,
+           "c_void_p": ctypes.c_void_p, "c_char_p": ctypes.c_char_p, "None": None,
+           "ctypes.POINTER(c_void_p)": ctypes.POINTER(ctypes.c_void_p)}
+
+
+def test_integration_doc_bindings_match_abi() -> None:
+    """Every ctypes binding INTEGRATION.md shows a maintainer (argtypes and restype) equals the
+    library's own binding table, which test_library_exports_every_declared_symbol ties to the
+    header: the documented reference-side stub cannot drift from the ABI."""
+    text = open(INTEGRATION).read()
+    code = "\n".join(re.findall(r"```python\n(.*?)```", text, flags=re.S))
+    code = re.sub(r"#[^\n]*", "", code)
+    argtypes = re.findall(r"_lib\.(smc_\w+)\.argtypes\s*=\s*\[(.*?)\]\s*\n", code, flags=re.S)
+    restypes = re.findall(r"_lib\.(smc_\w+)\.restype\s*=\s*([\w.()]+)", code)
+    assert len(argtypes) >= 14
+    for name, body in argtypes:
+        items = [t.strip() for t in body.replace("\n", " ").split(",") if t.strip()]
+        assert [_CTYPES[t] for t in items] == _lib.SIGNATURES[name][1], name
+    for name, rt in restypes:
+        assert _CTYPES[rt] == _lib.SIGNATURES[name][0], name
+    assert {n for n, _ in argtypes} == {n for n, _ in restypes}
+    # every documented call passes as many arguments as the header declares
+    calls = re.findall(r"_check\(_lib\.(smc_\w+)\((.*?)\)\)\n", code, flags=re.S)
+    assert len(calls) >= 3
+    for name, args in calls:
+        depth, count = 0, 1
+        for ch in args:
+            depth += ch in "([{"
+            depth -= ch in ")]}"
+            count += ch == "," and depth == 0
+        assert count == len(_lib.SIGNATURES[name][1]), name
+
+
 @pytest.mark.parametrize("seed", [7, 31, 42, 123])
 @pytest.mark.parametrize("skip", [0, 8, 4096])
 def test_host_sobol_bit_exact_with_reference(golden, seed, skip) -> None:
@@ -113,7 +147,7 @@ def test_path_pitch_is_an_odd_multiple_of_4k() -> None:
 
 def test_train_targets_kernel_choice() -> None:
     """Which path/CF kernel smc_train_targets runs: the sliced queue kernel with a workspace, the
-    per-contract kernel otherwise (the pipelined kernel is an opt-in SMC_PIPELINE build)."""
+    per-contract kernel otherwise."""
     L = _lib.lib()
     assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 0) == b"contract_kernel"
     assert L.smc_train_targets_kernel(16, 1024, 262144, 0, 0, 0) == b"contract_kernel"

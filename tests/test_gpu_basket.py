@@ -52,9 +52,9 @@ def test_portable_bit_exact_vs_oracle(oracle, A, T) -> None:
 
 
 @pytest.mark.parametrize("A,N,M,B", [(2, 64, 32, 1100), (4, 2048, 2, 530), (3, 12, 512, 9)])
-def test_persistent_pipelined_and_general_shapes_bit_exact(oracle, A, N, M, B) -> None:
-    """B above the resident grid (512 workgroups): workgroups run several contracts and overlap the
-    previous one's CF re-read (N | 2048); N = 12 takes the one-workgroup-per-contract kernel."""
+def test_multi_round_and_general_shapes_bit_exact(oracle, A, N, M, B) -> None:
+    """B above the resident grid (512 workgroups): several rounds of contract workgroups; N = 2048
+    (4-column quads over the whole workgroup) and N = 12 (not a divisor of the chunk)."""
     cfg = BasketConfig(n_assets=A, timesteps=4, network_size=N, batches_per_mc_run=M, math="portable")
     c = _contracts(oracle, cfg, B, skip=5)
     _, want_sum, want = oracle.basket_kernel(c, A, 4, N, M, cfg.mc_seed, ordinal0=11)

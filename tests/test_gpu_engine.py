@@ -232,20 +232,19 @@ def test_sliced_f64_and_chunked_launches(oracle, golden) -> None:
     np.testing.assert_array_equal(a, b)
 
 
-PIPELINED_CASES = [
-    # (B, T, N, M, scheme, normalize): terminal-only training shapes that take the persistent
-    # pipelined kernel (P % 2048 == 0, N a power of two, T <= 16); B > the resident grid (512 on
-    # MI355X), so workgroups run several contracts and pipeline the previous one's CF phase
+MANY_CONTRACT_CASES = [
+    # (B, T, N, M, scheme, normalize): more contracts than the resident grid (512 workgroups on
+    # MI355X), so the one-workgroup-per-contract launch runs several rounds
     (600, 16, 128, 16, 0, 1),
-    (1100, 5, 256, 8, 1, 1),     # T < 16, simple Euler, 2-3 contracts per workgroup
-    (520, 16, 2048, 2, 0, 0),    # N = kChunk, RAW
+    (1100, 5, 256, 8, 1, 1),     # T < 16, simple Euler
+    (520, 16, 2048, 2, 0, 0),    # N = 2048 (4 x the workgroup: 4-column quads), RAW
     (513, 16, 4, 1024, 0, 1),    # N = 4
 ]
 
 
-@pytest.mark.parametrize("B,T,N,M,scheme,normalize", PIPELINED_CASES)
+@pytest.mark.parametrize("B,T,N,M,scheme,normalize", MANY_CONTRACT_CASES)
 @pytest.mark.parametrize("store", [_lib.STORE_ALL, _lib.STORE_TERMINAL])
-def test_pipelined_kernel_matches_oracle(oracle, golden, B, T, N, M, scheme, normalize, store) -> None:
+def test_multi_round_launches_match_oracle(oracle, golden, B, T, N, M, scheme, normalize, store) -> None:
     c = _contracts(oracle, golden, B, seed=7, skip=3)
     got, _, _ = _run_targets(c, T, N, M, scheme, normalize, "float32", store, ordinal0=9, with_rowsum=False)
     kt, _ = oracle.kernel_targets(c, T, N, M, seed=7, ordinal0=9, scheme=scheme, normalize=bool(normalize))
