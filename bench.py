@@ -67,17 +67,28 @@ def algorithmic_bytes_per_contract(T: int, N: int, M: int, store_all: bool) -> i
     return (T * P * 4 if store_all else P * 4) + P * 4 + N * 8
 
 
+def cpu_threads() -> int:
+    """Host threads for the CPU legs: the process's affinity set, capped by OMP_NUM_THREADS (the
+    GPU box gives one GPU's job a 16-core share; os.cpu_count() there is the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
 def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: float, n_assets: int = 0) -> dict:
-    """Oracle step on the host cores: MC for a time-boxed sample of the B contracts
-    (extrapolated to B) + one full-size CVNN/Adam step on torch-cpu."""
+    """The reference CPU path (north_star: torch-cpu + numpy.fft; oracle/torch_cpu.py) timed on the
+    host cores: MC for a time-boxed sample of the B contracts (extrapolated to B) + one full-size
+    CVNN/Adam step on torch-cpu; plus C1 (BASELINE configs[0]) timed over 10 whole steps, and the
+    C/OpenMP oracle as a second, separately labelled leg."""
     import numpy as np
     import torch
 
     import oracle
+    from oracle.torch_cpu import cpu_path_targets, cpu_training_step
     from tests.helpers import make_domain_bounds, make_test_cvnn
 
     oracle.build()
-    threads = oracle.num_threads()
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     if n_assets:
         from spectralmc_amd.basket import BasketConfig
@@ -86,50 +97,80 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
     else:
         lo, hi = make_domain_bounds().arrays()
     contracts = oracle.sobol_contracts(7, 0, B, lo, hi)
-    done, t_mc = 0, 0.0
-    chunk = max(1, threads)
-    targets = []
-    while done < B and t_mc < budget_s * 0.8:
-        n = min(chunk, B - done)
-        t0 = time.perf_counter()
-        if n_assets:  # kernel-mode basket restatement (the basket has no reference-mode CPU path)
-            targets.append(oracle.basket_kernel(contracts[done:done + n], n_assets, T, N, M, 7, ordinal0=done)[2])
-        else:
-            targets.append(oracle.training_targets(contracts[done:done + n], T, N, M, seed=7, ordinal0=done))
-        t_mc += time.perf_counter() - t0
-        done += n
-    mc_per_contract = t_mc / done
+
+    def sample(fn, budget: float, chunk: int) -> tuple[float, int, list]:
+        done, t_mc, out = 0, 0.0, []
+        while done < B and t_mc < budget:
+            n = min(chunk, B - done)
+            t0 = time.perf_counter()
+            out.append(fn(contracts[done:done + n], done))
+            t_mc += time.perf_counter() - t0
+            done += n
+        return t_mc / done, done, out
+
+    if n_assets:  # kernel-mode basket restatement (the basket has no reference-mode CPU path)
+        per_c, done, tg = sample(lambda c, o: oracle.basket_kernel(c, n_assets, T, N, M, 7, ordinal0=o)[2],
+                                 budget_s * 0.8, threads)
+        path = "oracle C basket kernel-mode (f32)"
+    else:
+        per_c, done, tg = sample(lambda c, o: cpu_path_targets(c, T, N, M, 7, o, normals="numpy"),
+                                 budget_s * 0.6, 2 * threads)
+        path = ("torch-cpu paths (f64 recursion, numpy default_rng normals per contract) + numpy.fft "
+                "(oracle/torch_cpu.py)")
     model = make_test_cvnn(n_inputs=contracts.shape[1], n_outputs=N, seed=123, dtype=torch.float32, device="cpu",
                            hidden_layers=len(widths))
     adam = torch.optim.Adam(model.parameters(), lr=1e-2)
     x = torch.tensor(contracts, dtype=torch.float32)
-    tg = torch.from_numpy(np.concatenate(targets))
-    tg = tg.repeat((B + tg.shape[0] - 1) // tg.shape[0], 1)[:B]
-    oracle.torch_step(model, x, torch.zeros_like(x), tg, adam)  # warm
+    tgt = torch.from_numpy(np.concatenate(tg))
+    tgt = tgt.repeat((B + tgt.shape[0] - 1) // tgt.shape[0], 1)[:B]
+    oracle.torch_step(model, x, torch.zeros_like(x), tgt, adam)  # warm
     t0 = time.perf_counter()
     reps = 3
     for _ in range(reps):
-        oracle.torch_step(model, x, torch.zeros_like(x), tg, adam)
+        oracle.torch_step(model, x, torch.zeros_like(x), tgt, adam)
     t_nn = (time.perf_counter() - t0) / reps
-    step_s = mc_per_contract * B + t_nn
+    step_s = per_c * B + t_nn
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
             cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
-    return {
+    line = {
         "value": B * N * M / step_s,
         "unit": "contracts*paths/s",
         "steps_per_sec": 1.0 / step_s,
         "cores": threads,
+        "affinity_cores": len(os.sched_getaffinity(0)),
+        "machine_cores": os.cpu_count(),
         "kind": "port",
-        "sample": (f"oracle MC ({'f32 basket kernel-mode' if n_assets else 'f64 path recursion'}, OpenMP "
-                   f"{threads} threads) on {done}/{B} contracts "
-                   f"x {N * M} paths x T={T} ({t_mc:.1f}s), extrapolated x{B / done:.1f}, "
-                   f"+ full B={B} CVNN/Adam step on torch-cpu ({t_nn * 1e3:.1f} ms)"),
+        "sample": (f"{path}, {threads} threads, on {done}/{B} contracts x {N * M} paths x T={T} "
+                   f"({per_c * done:.1f}s), extrapolated x{B / done:.1f}, + full B={B} CVNN/Adam step on torch-cpu "
+                   f"({t_nn * 1e3:.1f} ms)"),
         "cpu_model": cpu_model,
     }
+    if not n_assets:
+        # second leg: the C/OpenMP oracle (f64 recursion, this build's normal streams)
+        per_c2, done2, _ = sample(lambda c, o: oracle.training_targets(c, T, N, M, seed=7, ordinal0=o),
+                                  budget_s * 0.2, threads)
+        line["c_openmp_leg"] = {"value": B * N * M / (per_c2 * B + t_nn), "unit": "contracts*paths/s",
+                                "cores": threads, "kind": "port",
+                                "sample": f"oracle/gbm_oracle.c (OpenMP) on {done2}/{B} contracts, extrapolated"}
+        # C1, the reference's own CPU-runnable config (BASELINE configs[0]): 10 whole steps
+        c1B, c1N, c1M = 64, 256, 4
+        m1 = make_test_cvnn(n_inputs=6, n_outputs=c1N, seed=123, dtype=torch.float32, device="cpu", hidden_layers=1)
+        a1 = torch.optim.Adam(m1.parameters(), lr=1e-2)
+        c1 = oracle.sobol_contracts(7, 0, 11 * c1B, lo, hi)
+        cpu_training_step(m1, a1, c1[:c1B], T, c1N, c1M, 7, 0, normals="numpy")  # warm-up step
+        t0 = time.perf_counter()
+        for s in range(1, 11):
+            cpu_training_step(m1, a1, c1[s * c1B:(s + 1) * c1B], T, c1N, c1M, 7, s * c1B, normals="numpy")
+        t1 = (time.perf_counter() - t0) / 10
+        line["c1"] = {"steps_per_sec": 1.0 / t1, "value": c1B * c1N * c1M / t1, "unit": "contracts*paths/s",
+                      "ms_per_step": t1 * 1e3, "steps": 10, "warmup": 1,
+                      "workload": "C1: 64 contracts x 1024 paths (N=256 x M=4), T=16, 2-layer CVNN 6->32->256, "
+                                  "torch-cpu + numpy.fft, whole steps"}
+    return line
 
 
 def main() -> None:

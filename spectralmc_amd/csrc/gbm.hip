@@ -22,6 +22,7 @@
 //     evaluated from an LDS twiddle table (FFT linearity: FFT(mean_m x_m) == mean_m FFT(x_m)).
 
 #include <cmath>
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -200,10 +201,12 @@ __device__ __forceinline__ void advance_packed(Real (&x)[4], const Real (&y)[4])
 // T > kRowBlock), rows [t0, t0 + nrows) are stored and added to acc[].  MASKED handles the
 // ragged last chunk (nvalid < 4) and P % 4 != 0 with scalar stores; otherwise one dwordx4
 // store per row, addressed as (wave-uniform row base) + (32-bit lane offset).
-// STRAIGHT (with FULLBLOCK, T == kRowBlock, every row stored): t == i, the terminal row is i == 15
-// and every store is unconditional, so the 16-row block is straight-line code — no per-row
-// branches and no per-row condition masks (which otherwise spill SGPRs into VGPR lanes).
-template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS, bool MASKED, bool FULLBLOCK, bool STRAIGHT = false>
+// STRAIGHT (with FULLBLOCK, T == kRowBlock): t == i, the terminal row is i == 15 and every store
+// (every row with STRAIGHT_ALL, else the terminal row only) is unconditional, so the 16-row block is
+// straight-line code — no per-row branches and no per-row condition masks (which otherwise spill
+// SGPRs into VGPR lanes).
+template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS, bool MASKED, bool FULLBLOCK, bool STRAIGHT = false,
+          bool STRAIGHT_ALL = true>
 __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                            uint64_t ordinal, int64_t chunk, int nvalid, int t0, int nrows,
                                            Real* contract_base, double (&acc)[ALLROWS ? kRowBlock : 1]) {
@@ -211,7 +214,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   const int T = a.T;
   const int64_t P = a.P;
   const int64_t pitch = a.pitch ? a.pitch : P;
-  const bool store_all = STRAIGHT || a.store == SMC_STORE_ALL;
+  const bool store_all = STRAIGHT ? STRAIGHT_ALL : a.store == SMC_STORE_ALL;
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));  // the lane's group stream
   // f32 HW log-Euler: the RNG hands back the step exponents directly (packed path pairs)
@@ -375,15 +378,15 @@ struct Payoff {
 // their Hermitian mirror); fixed summation order.
 template <typename Real>
 __device__ void dft_row(const double* avg, const double* cs, const double* sn, int N,
-                        typename Complex2<Real>::type* out) {
+                        typename Complex2<Real>::type* out, int tid = threadIdx.x, int nthreads = kThreads) {
   using C2 = typename Complex2<Real>::type;
   // bins k = 0..N/2-1 over the threads; when N/2 is a multiple of the workgroup the Nyquist bin
   // N/2 would take a whole extra pass for one thread, so thread 0 runs its chain inside its k = 0
   // loop instead (same fma sequence per chain: same bits).  Only for even N with kmax > 0: odd N
   // has no Nyquist bin (bin kmax is an ordinary pair with N - kmax), and N = 1 has only bin 0.
   const int kmax = N / 2;
-  const bool fuse_nyq = (N % 2) == 0 && kmax > 0 && kmax % kThreads == 0;
-  for (int k = threadIdx.x; k < kmax || (!fuse_nyq && k == kmax); k += kThreads) {
+  const bool fuse_nyq = (N % 2) == 0 && kmax > 0 && kmax % nthreads == 0;
+  for (int k = tid; k < kmax || (!fuse_nyq && k == kmax); k += nthreads) {
     const bool nyq = fuse_nyq && k == 0;
     double re = 0.0, im = 0.0, rq = 0.0, iq = 0.0;
     int idx = 0, iqx = 0;
@@ -415,6 +418,41 @@ __device__ void dft_row(const double* avg, const double* cs, const double* sn, i
   }
 }
 
+// Payoff sums of the f32 terminal row, N % 4 == 0: item (q, g) = column quad q (4 adjacent
+// columns, one 16-B load per batch row) over batches m = g, g + G, ... in ascending order, into
+// part[g][4q..4q+3].  Items are spread over `nthreads` threads from `tid`; the arithmetic of an
+// item does not depend on which thread runs it.  sc1 (L1-bypassing) loads: the row may have been
+// written by other workgroups (sliced contracts) or other waves of this one.
+template <int kBatch>
+__device__ __forceinline__ void quad_column_sums(const float* row, const Payoff<float>& pay, int N, int M,
+                                                 int cols, int G, double* part, int tid, int nthreads) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), static_cast<short>(0), 0x7fffffff, 0x00020000);
+  const int items = cols * G;
+  for (int item = tid; item < items; item += nthreads) {
+    const int q = item % cols, g = item / cols;
+    double sum[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int m0 = g; m0 < M; m0 += G * kBatch) {
+      v4f v[kBatch];
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        const int m = m0 + u * G < M ? m0 + u * G : M - 1;  // clamped: loads stay unconditional
+        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (m * N + 4 * q) * 4, 0, 16 /* sc1 */);
+      }
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        if (m0 + u * G < M) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sum[e] += static_cast<double>(pay(v[u][e]));
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[g * N + 4 * q + e] = sum[e];
+  }
+}
+
 template <typename Real>
 __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int64_t b,
                                     double terminal_sum, double* lds) {
@@ -442,33 +480,7 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
 
   constexpr int kBatch = 16;  // loads in flight per thread; the sum keeps the m order
   if constexpr (sizeof(Real) == 4) {
-    if (quad) {
-      typedef float v4f __attribute__((ext_vector_type(4)));
-      // sc1 (L1-bypassing) 16-B loads: the row was written by this contract's slices (sc1 stores)
-      const __amdgpu_buffer_rsrc_t rsrc =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<Real*>(row), static_cast<short>(0), 0x7fffffff, 0x00020000);
-      for (int item = tid; item < items; item += kThreads) {
-        const int q = item % cols, g = item / cols;
-        double sum[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int m0 = g; m0 < M; m0 += G * kBatch) {
-          v4f v[kBatch];
-#pragma unroll
-          for (int u = 0; u < kBatch; ++u) {
-            const int m = m0 + u * G < M ? m0 + u * G : M - 1;  // clamped: loads stay unconditional
-            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (m * N + 4 * q) * 4, 0, 16 /* sc1 */);
-          }
-#pragma unroll
-          for (int u = 0; u < kBatch; ++u) {
-            if (m0 + u * G < M) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) sum[e] += static_cast<double>(pay(v[u][e]));
-            }
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) part[g * N + 4 * q + e] = sum[e];
-      }
-    }
+    if (quad) quad_column_sums<kBatch>(row, pay, N, M, cols, G, part, tid, kThreads);
   }
   for (int item = tid; item < items && !quad; item += kThreads) {
     const int n = item % N, g = item / N;
@@ -567,6 +579,65 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void contract_kernel(Engi
   run_slice<Real, LOG_EULER, HW, ALLROWS>(a, blockIdx.x, 0, lds, &flag);
 }
 
+// ---- split training pair: paths_kernel, then cf_kernel --------------------------------------
+// The fused contract_kernel runs each round of resident workgroups into a chip-wide CF phase
+// (every workgroup drains, re-reads its terminal row and evaluates the DFT at about the same
+// time).  Split in two launches instead: paths_kernel simulates and stores every contract and
+// leaves the terminal-row sum (f64, the normalisation's input) in that row's padding column;
+// cf_kernel then streams all terminal rows back at full read bandwidth, one workgroup per
+// contract.  Same arithmetic and orders as contract_kernel: bit-identical targets.
+// f32 scratch only (split_ok): the first 8-B-aligned padding slot after column P of the terminal row
+__device__ __forceinline__ double* pad_sum(const EngineArgs& a, int64_t b) {
+  const int64_t pitch = a.pitch ? a.pitch : a.P;
+  const int64_t row = a.store == SMC_STORE_ALL ? (b * a.T + (a.T - 1)) * pitch : b * pitch;
+  return reinterpret_cast<double*>(static_cast<float*>(a.paths) + row + a.P + (a.P & 1));
+}
+
+// STRAIGHT (T == 16, P a multiple of 2048): only the straight-line 16-row block is compiled in
+// (STORE_ALL: every row; else the terminal row), so the kernel needs ~60 VGPRs instead of ~100.
+// The terminal sum keeps simulate_contract's order: lane over chunks, wave butterfly, waves 0..7.
+template <bool LOG_EULER, bool HW, bool STRAIGHT, bool STORE_ALL>
+__global__ __launch_bounds__(kThreads) void paths_kernel(EngineArgs a) {
+  extern __shared__ double lds[];
+  const int64_t b = blockIdx.x;
+  const Contract c = load_contract(a.contracts + b * 6);
+  const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
+  if constexpr (STRAIGHT) {
+    const Stepper<float, LOG_EULER, HW> step(c, kRowBlock);
+    const float x0 = static_cast<float>(c.X0);
+    const int64_t pitch = a.pitch ? a.pitch : a.P;
+    float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * kRowBlock * pitch : b * pitch);
+    double acc[1] = {0.0};
+    for (int64_t chunk = 0; chunk < a.P; chunk += kChunk)
+      lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(a, step, x0, ordinal, chunk,
+                                                                             kPathsPerLane, 0, kRowBlock, base, acc);
+    const double w = wave_sum(acc[0]);
+    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double tot = 0.0;
+      for (int k = 0; k < kWaves; ++k) tot += lds[k];
+      *pad_sum(a, b) = tot;
+    }
+  } else {
+    simulate_contract<float, LOG_EULER, HW, false>(a, c, ordinal, b, 0, a.P, lds + a.T, lds);
+    if (threadIdx.x == 0) *pad_sum(a, b) = lds[a.T - 1];
+  }
+}
+
+template <typename Real>
+__global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
+  extern __shared__ double lds[];
+  const int64_t b = blockIdx.x;
+  const Contract c = load_contract(a.contracts + b * 6);
+  cf_targets_contract<Real>(a, c, b, *pad_sum(a, b), lds);
+}
+
+bool split_ok(const EngineArgs& a, bool f32) {
+  const int64_t pitch = a.pitch ? a.pitch : a.P;
+  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && pitch >= a.P + (a.P & 1) + 2;
+}
+
 // Sliced contracts on persistent workgroups.  Contract b belongs to queue b mod 8; a workgroup
 // takes items (slice k of a contract) from the queue of the XCD it runs on (s_getreg XCC_ID), so
 // the slices of a contract run side by side on one XCD, finish within a few tens of microseconds
@@ -604,6 +675,180 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void queue_kernel(EngineA
     for (int x = 0; x < 8; ++x) drain_queue(x);
     if (threadIdx.x < 9) __hip_atomic_store(queues + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// ---- overlap_kernel: the training shape with the CF phase moved off the store stream ----------
+// A persistent workgroup of 8 compute waves + 1 CF wave runs contracts b = blockIdx.x, + gridDim.x,
+// ...  The compute waves simulate contract b (the contract kernel's straight-line 16-row block,
+// same streams, stores and terminal-sum order) while the CF wave runs the payoff, M-mean and DFT
+// of the workgroup's previous contract — so no wave ever drains its store queue between contracts
+// and the 256 KB terminal-row re-read streams beside the next contract's stores instead of after
+// a chip-wide synchronised drain (contract_kernel's rounds all reach their CF phase together).
+// Hand-off, per contract iteration k (contract b_k; the CF wave holds b_{k-1}):
+//   BAR1  compute waves: after chunk 0 of b_k, `s_waitcnt vmcnt(R)` (R = stores per chunk) — every
+//         store of b_{k-1} is older than chunk 0's R stores, so all of them are done (in L2, this
+//         XCD); the CF wave then re-reads b_{k-1}'s terminal row with L1-bypassing loads.
+//   BAR2  compute waves: wave sums of b_k's terminal row in LDS; the CF wave reads their total.
+// Barriers are LDS-only (no vmcnt drain).  Results are bit-identical to contract_kernel: same
+// per-lane streams, same row-sum order (lane over chunks, wave butterfly, waves 0..7), same CF
+// item arithmetic (quad_column_sums) and DFT chains.
+constexpr int kOverlapThreads = kThreads + 64;
+
+__device__ __forceinline__ void lds_barrier() {  // LDS visibility only: no vmcnt drain of the stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ void wave_lds_sync() {  // this wave's LDS writes visible to its own lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// The CF wave reads the terminal row as P / 256 pieces of 1 KiB — one global_load_lds_dwordx4 each
+// (no VGPR destination) — through an LDS ring that keeps kRing - 1 pieces in flight: the re-read
+// runs beside the compute waves' store stream, where one read's latency is long.
+constexpr int kRing = 32;
+constexpr int kPiece = 256;  // floats per piece (64 lanes x 16 B)
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+size_t overlap_lds_bytes(int N) {
+  return (static_cast<size_t>(kWaves) + 4 * static_cast<size_t>(kThreads) + 3 * static_cast<size_t>(N)) *
+             sizeof(double) +
+         static_cast<size_t>(kRing) * kPiece * sizeof(float);
+}
+
+// Payoff sums of one contract's terminal row by ONE wave, streamed in row-major order: lane l of
+// piece i holds element e = 256 i + 4 l = (batch m = e / N, columns n0..n0+3 with n0 = e mod N),
+// and adds the 4 payoffs to part[m mod G][n0..n0+3].  Every item (column quad, group g) thus sums
+// its batches m = g, g + G, ... in ascending order from 0.0 — quad_column_sums' arithmetic.  One
+// piece covers 256 / N < G batch rows, so no two lanes of a piece share a part entry.
+__device__ void stream_column_sums(const float* row, const Payoff<float>& pay, int N, int64_t P, int G,
+                                   double* part, float* ring, int lane) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  for (int i = lane; i < G * N; i += 64) part[i] = 0.0;
+  const int pieces = static_cast<int>(P / kPiece);
+  auto issue = [&](int i) {
+    __builtin_amdgcn_global_load_lds(row + static_cast<int64_t>(kPiece) * i + 4 * lane,
+                                     (lds_void_ptr)(ring + (i % kRing) * kPiece), 16, 0,
+                                     16 /* sc1: L1-bypassing */);
+  };
+  const int pre = pieces < kRing - 1 ? pieces : kRing - 1;
+  for (int i = 0; i < pre; ++i) issue(i);
+  int n0 = (4 * lane) % N, g = ((4 * lane) / N) % G;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");  // part zeroed before the first add
+  for (int i = 0; i < pieces; ++i) {
+    if (i + kRing - 1 < pieces) {
+      issue(i + kRing - 1);
+      asm volatile("s_waitcnt vmcnt(31)" ::: "memory");  // piece i landed (kRing - 1 younger in flight)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const v4f x = *reinterpret_cast<const v4f*>(ring + (i % kRing) * kPiece + 4 * lane);
+    double* p = part + g * N + n0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p[e] += static_cast<double>(pay(x[e]));
+    n0 += kPiece;
+    while (n0 >= N) {
+      n0 -= N;
+      if (++g == G) g = 0;
+    }
+  }
+}
+static_assert(kRing == 32, "stream_column_sums waits with vmcnt(kRing - 1)");
+
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
+__global__ __launch_bounds__(kOverlapThreads) __attribute__((amdgpu_waves_per_eu(5, 8)))
+void overlap_kernel(EngineArgs a) {
+  extern __shared__ double lds[];
+  constexpr int T = kRowBlock;
+  // wave index made provably wave-uniform: the role branch is uniform control flow
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int N = a.N, M = a.M;
+  const int64_t P = a.P;
+  const int64_t pitch = a.pitch ? a.pitch : P;
+  double* wsum = lds;                    // [kWaves]
+  double* part = lds + kWaves;           // [G][N] = [4 kThreads] (N <= 4 kThreads)
+  double* avg = part + 4 * kThreads;     // [N]
+  double* cs = avg + N;                  // [N]
+  double* sn = cs + N;                   // [N]
+  float* ring = reinterpret_cast<float*>(sn + N);  // [kRing][kPiece] (16-B aligned: N % 4 == 0)
+  const int64_t nk = (a.B - blockIdx.x + gridDim.x - 1) / gridDim.x;  // contracts of this workgroup
+  const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
+  auto row_of = [&](int64_t b) {
+    return static_cast<float*>(a.paths) + (STORE_ALL ? b * T * pitch : b * pitch);
+  };
+
+  if (wave < kWaves) {  // ---- compute waves: simulate and store, contract after contract
+    for (int64_t k = 0; k < nk; ++k) {
+      const int64_t b = blockIdx.x + k * gridDim.x;
+      const Contract c = load_contract(a.contracts + b * 6);
+      const Stepper<float, LOG_EULER, HW> step(c, T);
+      const float x0 = static_cast<float>(c.X0);
+      const uint64_t ordinal = static_cast<uint64_t>(ord0 + b);
+      float* base = row_of(b);
+      double acc[1] = {0.0};
+      for (int64_t chunk = 0; chunk < P; chunk += kChunk) {
+        lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(a, step, x0, ordinal, chunk,
+                                                                               kPathsPerLane, 0, kRowBlock, base, acc);
+        if (chunk == 0) {  // BAR1: every store of the previous contract has completed
+          if constexpr (STORE_ALL) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+          lds_barrier();
+        }
+      }
+      const double w = wave_sum(acc[0]);
+      if (lane == 0) wsum[wave] = w;
+      lds_barrier();  // BAR2
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();  // BAR1 of the tail: the last contract's stores are done
+    return;
+  }
+
+  // ---- CF wave: payoff, M-mean and DFT of the previous contract
+  for (int j = lane; j < N; j += 64) math::twiddle(j, N, sn[j], cs[j]);
+  const int cols = N / 4;
+  const int G = cols <= kThreads ? kThreads / cols : 1;
+  int64_t prev = -1;
+  double prev_tot = 0.0;
+#ifndef SMC_OVERLAP_CF_MODE
+#define SMC_OVERLAP_CF_MODE 0  // tools/micro decomposition builds: 1 no CF work, 2 no DFT, 4 CF wave prio 0
+#endif
+  if (SMC_OVERLAP_CF_MODE != 4) __builtin_amdgcn_s_setprio(3);  // issue before the compute waves
+  auto run_cf = [&](int64_t pb, double tot) {
+    if (SMC_OVERLAP_CF_MODE == 1) return;
+    const Contract c = load_contract(a.contracts + pb * 6);
+    const Payoff<float> pay(a, c, tot);
+    const float* row = row_of(pb) + (STORE_ALL ? static_cast<int64_t>(T - 1) * pitch : 0);
+    stream_column_sums(row, pay, N, P, G, part, ring, lane);
+    wave_lds_sync();
+    for (int n = lane; n < N; n += 64) {
+      double t = 0.0;
+      for (int g = 0; g < G; ++g) t += part[g * N + n];
+      avg[n] = t / static_cast<double>(M);
+    }
+    wave_lds_sync();
+    if (SMC_OVERLAP_CF_MODE != 2) dft_row<float>(avg, cs, sn, N, static_cast<float2*>(a.targets) + pb * N, lane, 64);
+    wave_lds_sync();  // part / avg are reused by the next contract
+  };
+  for (int64_t k = 0; k < nk; ++k) {
+    lds_barrier();  // BAR1
+    if (prev >= 0) run_cf(prev, prev_tot);
+    lds_barrier();  // BAR2
+    double tot = 0.0;
+    for (int w = 0; w < kWaves; ++w) tot += wsum[w];
+    prev = blockIdx.x + k * gridDim.x;
+    prev_tot = tot;
+  }
+  lds_barrier();  // tail BAR1
+  if (prev >= 0) run_cf(prev, prev_tot);
+}
+
+bool overlap_ok(const EngineArgs& a, bool f32) {
+  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T == kRowBlock && a.N % 4 == 0 &&
+         a.N <= 1024 && a.P % kChunk == 0 && a.P < (int64_t{1} << 29) && (a.pitch == 0 || a.pitch % 4 == 0);
 }
 
 // In-place forward normalisation of a stored [B][T][P] matrix (gbm.py:428-438).
@@ -665,7 +910,7 @@ size_t lds_bytes(int T, int N, bool cf) {
 
 // Resident workgroups of a persistent kernel on the current device (occupancy x CUs, cached
 // per (device, kernel)); grid = min(work items, that).
-int32_t resident_grid(const void* kernel, size_t lds, int64_t items, unsigned* grid) {
+int32_t resident_grid(const void* kernel, int threads, size_t lds, int64_t items, unsigned* grid) {
   struct Entry {
     int dev;
     const void* kernel;
@@ -682,7 +927,7 @@ int32_t resident_grid(const void* kernel, size_t lds, int64_t items, unsigned* g
   if (slots == 0) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, lds) != hipSuccess) {
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) != hipSuccess) {
       (void)hipGetLastError();
       return fail(SMC_ERR_HIP, "engine: occupancy query failed");
     }
@@ -704,7 +949,8 @@ int32_t launch_engine_k(const EngineArgs& a, size_t lds, hipStream_t stream) {
       return fail(SMC_ERR_HIP, "queue_kernel: cannot raise the dynamic LDS limit");
     }
     unsigned grid = 0;
-    if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), lds, a.B * a.slices, &grid)) return st;
+    if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kThreads, lds, a.B * a.slices, &grid))
+      return st;
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), lds, stream, a);
     return check_launch("queue_kernel");
   }
@@ -733,9 +979,118 @@ size_t workspace_bytes(int64_t B, int32_t T, int64_t P, bool all_rows) {
   return static_cast<size_t>(B) * W * (all_rows ? T : 1) * sizeof(double) + static_cast<size_t>(B + 16) * sizeof(uint32_t);
 }
 
+// Workgroups per CU for the overlap kernel: 2 (8 contracts per workgroup at C2; a third slot
+// would leave a partly filled last round).  SMC_OVERLAP_WGS_PER_CU overrides (tuning only; the
+// results do not depend on the grid).
+int overlap_wgs_per_cu() {
+  static int v = [] {
+    const char* e = getenv("SMC_OVERLAP_WGS_PER_CU");
+    const int x = e ? atoi(e) : 2;
+    return x >= 1 && x <= 8 ? x : 2;
+  }();
+  return v;
+}
+
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
+int32_t launch_overlap_k(const EngineArgs& a, hipStream_t stream) {
+  auto kernel = overlap_kernel<LOG_EULER, HW, STORE_ALL>;
+  const size_t lds = overlap_lds_bytes(a.N);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "overlap_kernel: cannot raise the dynamic LDS limit");
+  }
+  unsigned grid = 0;
+  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kOverlapThreads, lds, a.B, &grid)) return st;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ==
+      hipSuccess && cus > 0) {
+    const int64_t cap = static_cast<int64_t>(overlap_wgs_per_cu()) * cus;
+    if (grid > cap) grid = static_cast<unsigned>(cap);
+  }
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kOverlapThreads), lds, stream, a);
+  return check_launch("overlap_kernel");
+}
+
+// Dynamic LDS of paths_kernel: its own need, or SMC_PATHS_LDS_KB (tuning: fewer resident
+// workgroups per CU).  The results do not depend on it.
+size_t paths_lds_bytes(size_t need) {
+  static const size_t pad = [] {
+    const char* e = getenv("SMC_PATHS_LDS_KB");
+    const long v = e ? atol(e) : 0;
+    return v > 0 && v <= 160 ? static_cast<size_t>(v) * 1024 : size_t{0};
+  }();
+  return pad > need ? pad : need;
+}
+
+template <bool LOG_EULER, bool HW, bool STRAIGHT, bool STORE_ALL>
+int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
+  const size_t lds1 = paths_lds_bytes(lds_bytes(a.T, a.N, false)), lds2 = lds_bytes(a.T, a.N, true);
+  auto k1 = paths_kernel<LOG_EULER, HW, STRAIGHT, STORE_ALL>;
+  auto k2 = cf_kernel<float>;
+  if ((lds1 > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(k1),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                static_cast<int>(lds1)) != hipSuccess) ||
+      (lds2 > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(k2),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                static_cast<int>(lds2)) != hipSuccess)) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "paths_kernel / cf_kernel: cannot raise the dynamic LDS limit");
+  }
+  hipLaunchKernelGGL(k1, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds1, stream, a);
+  if (int32_t st = check_launch("paths_kernel")) return st;
+  hipLaunchKernelGGL(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
+  return check_launch("cf_kernel");
+}
+
+// Training-shape kernel choice: 0 fused contract_kernel, 1 overlap_kernel, 2 paths + cf pair
+#ifndef SMC_TRAIN_MODE
+#define SMC_TRAIN_MODE 2
+#endif
+
 template <typename Real>
 int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   if (a.B == 0) return SMC_OK;
+  if constexpr (sizeof(Real) == 4) {
+    if (SMC_TRAIN_MODE == 2 && split_ok(a, true)) {
+      const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+      const bool hw = (a.scheme & SMC_MATH_HW) != 0;
+      const bool straight = a.T == kRowBlock && a.P % kChunk == 0;
+      const bool sa = a.store == SMC_STORE_ALL;
+#define SMC_SPLIT(LE, HWM, ST, SA) \
+  if (log_euler == LE && hw == HWM && straight == ST && (!ST || sa == SA)) return launch_split_k<LE, HWM, ST, SA>(a, stream);
+      SMC_SPLIT(true, true, true, true)
+      SMC_SPLIT(true, true, true, false)
+      SMC_SPLIT(true, false, true, true)
+      SMC_SPLIT(true, false, true, false)
+      SMC_SPLIT(false, true, true, true)
+      SMC_SPLIT(false, true, true, false)
+      SMC_SPLIT(false, false, true, true)
+      SMC_SPLIT(false, false, true, false)
+      SMC_SPLIT(true, true, false, true)
+      SMC_SPLIT(true, false, false, true)
+      SMC_SPLIT(false, true, false, true)
+      SMC_SPLIT(false, false, false, true)
+#undef SMC_SPLIT
+    }
+  }
+  if (SMC_TRAIN_MODE == 1 && overlap_ok(a, sizeof(Real) == 4)) {
+    const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+    const bool hw = (a.scheme & SMC_MATH_HW) != 0;
+    const bool sa = a.store == SMC_STORE_ALL;
+#define SMC_OVERLAP(LE, HWM, SA) \
+  if (log_euler == LE && hw == HWM && sa == SA) return launch_overlap_k<LE, HWM, SA>(a, stream);
+    SMC_OVERLAP(true, true, true)
+    SMC_OVERLAP(true, true, false)
+    SMC_OVERLAP(true, false, true)
+    SMC_OVERLAP(true, false, false)
+    SMC_OVERLAP(false, true, true)
+    SMC_OVERLAP(false, true, false)
+    SMC_OVERLAP(false, false, true)
+    SMC_OVERLAP(false, false, false)
+#undef SMC_OVERLAP
+  }
   if (a.slices < 1 || !a.simulate) a.slices = 1;
   if (a.slices > 1 && (!a.partials || !a.arrivals || !a.queues))
     return fail(SMC_ERR_INVALID_ARGUMENT, "engine: sliced contracts need a workspace");
@@ -892,6 +1247,9 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.targets = &a;  // any non-null: the training call always writes targets
   a.pitch = path_pitch;
   a.slices = slices_for(n_paths, sliced != 0);
+  a.store = SMC_STORE_ALL;
+  if (SMC_TRAIN_MODE == 2 && split_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "paths_kernel+cf_kernel";
+  if (SMC_TRAIN_MODE == 1 && overlap_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "overlap_kernel";
   return a.slices > 1 ? "queue_kernel" : "contract_kernel";
 }
 

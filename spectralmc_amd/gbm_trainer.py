@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import asyncio
 import math
+import time
 import warnings
 from dataclasses import dataclass
 from typing import Callable, Iterable, Literal, Protocol, Sequence, runtime_checkable
@@ -525,14 +526,19 @@ class GbmCVNNPricer:
             return opened
         session = opened.value
         try:
+            t_prev = time.perf_counter()
             for i in range(config.num_batches):
                 stepped = session.step(prefetch_next=i + 1 < config.num_batches)
                 if isinstance(stepped, Failure):
                     return stepped
                 if logger is not None:
+                    # read_metrics synchronises, so with a logger every step ends on the host:
+                    # batch_time is the wall time of this step (enqueue -> network done)
                     loss, gn = session.read_metrics()
-                    logger(StepMetrics(step=session.global_step, batch_time=float("nan"), loss=loss, grad_norm=gn,
+                    now = time.perf_counter()
+                    logger(StepMetrics(step=session.global_step, batch_time=now - t_prev, loss=loss, grad_norm=gn,
                                        lr=config.learning_rate, optimizer=session.adam, model=self._cvnn))
+                    t_prev = now
                 do_commit, template = self._should_commit_now(blockchain_store, commit_plan, session.global_step)
                 if do_commit:
                     session.sync()
@@ -553,6 +559,7 @@ class GbmCVNNPricer:
             return adam_res
         adam = adam_res.value
         self._cvnn.train()
+        start = self._sobol_skip
         sobol_skip, global_step = self._sobol_skip, self._global_step
         loss_v, gn = 0.0, 0.0
         try:
@@ -562,18 +569,31 @@ class GbmCVNNPricer:
             return Failure(EngineFailure(code=exc.code, message=exc.message))
         engine.set_position(sobol_skip, self._mc_engine.ordinal)
         for _ in range(config.num_batches):
+            if sobol_skip + config.batch_size > MAX_POINTS:  # the device draw indexes 30 bits
+                sampler.skip(sobol_skip - start)
+                return Failure(SamplerInitFailed(error=SequenceExhausted(requested_end=sobol_skip + config.batch_size)))
+            t0 = time.perf_counter()
             buf = engine.enqueue_step()
             host = buf.contracts.cpu().numpy()
             for row in host:
                 res = validate_model(BlackScholes.Inputs, **{f: float(row[i]) for i, f in enumerate(FIELDS)})
                 if isinstance(res, Failure):
+                    sampler.skip(sobol_skip - start)
                     return Failure(SamplerInitFailed(error=SamplerValidationFailed(error=res.error)))
             loss, gn = self._torch_step(buf.real_in, buf.imag_in, buf.targets, adam)
             loss_v = float(loss.item())
             sobol_skip += config.batch_size
             global_step += 1
             self._mc_engine.advance(config.batch_size)
-        sampler.skip(sobol_skip - self._sobol_skip)
+            # the same per-step hooks as train(): logger, interval commits (reference _run_batch)
+            self._global_step, self._sobol_skip = global_step, sobol_skip
+            if logger is not None:
+                logger(StepMetrics(step=global_step, batch_time=time.perf_counter() - t0, loss=loss_v, grad_norm=gn,
+                                   lr=config.learning_rate, optimizer=adam, model=self._cvnn))
+            do_commit, template = self._should_commit_now(blockchain_store, commit_plan, global_step)
+            if do_commit:
+                self._commit_to_blockchain(blockchain_store, adam, template, loss_v, batch=global_step)
+        sampler.skip(sobol_skip - start)
         return self._finish(adam, _BatchState(sobol_skip, global_step, loss_v, gn), config, blockchain_store,
                             commit_plan)
 

@@ -146,16 +146,19 @@ def test_path_pitch_is_an_odd_multiple_of_4k() -> None:
 
 
 def test_train_targets_kernel_choice() -> None:
-    """Which path/CF kernel smc_train_targets runs: the sliced queue kernel with a workspace, the
-    per-contract kernel otherwise."""
+    """Which path/CF kernels smc_train_targets runs: the sliced queue kernel with a workspace; the
+    split pair paths_kernel + cf_kernel for f32 training (terminal-row sum parked in the scratch
+    row's padding, so it needs a padded pitch such as smc_path_pitch); contract_kernel otherwise."""
     L = _lib.lib()
-    assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 0) == b"contract_kernel"
-    assert L.smc_train_targets_kernel(16, 1024, 262144, 0, 0, 0) == b"contract_kernel"
+    split = b"paths_kernel+cf_kernel"
+    assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 0) == split                 # C2
+    assert L.smc_train_targets_kernel(16, 1024, 262144, 0, L.smc_path_pitch(262144, 0), 0) == split  # C3
+    assert L.smc_train_targets_kernel(16, 1024, 262144, 0, 0, 0) == b"contract_kernel"      # no padding
     assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 1) == b"queue_kernel"
     assert L.smc_train_targets_kernel(17, 256, 65536, 0, 0, 0) == b"contract_kernel"
-    assert L.smc_train_targets_kernel(16, 256, 65536, 1, 0, 0) == b"contract_kernel"   # f64
-    assert L.smc_train_targets_kernel(16, 256, 1024, 0, 0, 0) == b"contract_kernel"    # P % 2048
-    assert L.smc_train_targets_kernel(16, 6, 6144, 0, 0, 0) == b"contract_kernel"      # N not 2^k
+    assert L.smc_train_targets_kernel(17, 256, 65536, 0, 66560, 0) == split                 # generic block
+    assert L.smc_train_targets_kernel(16, 256, 65536, 1, 66560, 0) == b"contract_kernel"    # f64
+    assert L.smc_train_targets_kernel(16, 6, 6144, 0, 6144, 0) == b"contract_kernel"        # pitch == P
 
 
 def test_basket_entry_points_validate_before_any_device_work() -> None:

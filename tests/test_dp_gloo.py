@@ -64,10 +64,9 @@ def _run(rank: int, world: int, outdir: str) -> None:
         buffers.contracts.copy_(torch.from_numpy(contracts))
         buffers.real_in.copy_(torch.from_numpy(contracts))
         buffers.targets.copy_(torch.from_numpy(targets))
-        prog.handoff(0)
-        prog.fwd_bwd(0)
-        prog.reduce()
-        prog.update()
+        slot = s % 2  # the session's alternating network input slots
+        prog.handoff(slot)
+        prog.run_nn(slot)  # TrainingSession's network half: fwd/bwd, all-reduce, Adam (eager here)
         losses.append(float(prog.loss))
     np.savez(os.path.join(outdir, f"rank{rank}_w{world}.npz"), losses=np.array(losses),
              **{f"p{i}": p.detach().numpy() for i, p in enumerate(params)})

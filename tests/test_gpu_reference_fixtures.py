@@ -88,8 +88,8 @@ def test_c2_bench_instantiation_whole_rounds(oracle, gbm_golden) -> None:
     B = 4 * cus
     _, _, m = unpack(gbm_golden, "c2shape")
     assert (m["T"], m["N"], m["M"]) == (16, 256, 256) and m["ordinal0"] == 0
-    assert _lib.lib().smc_train_targets_kernel(16, 256, 65536, _lib.DTYPE_F32,
-                                               _lib.lib().smc_path_pitch(65536, 0), 0) == b"contract_kernel"
+    kernel = _lib.lib().smc_train_targets_kernel(16, 256, 65536, _lib.DTYPE_F32, _lib.lib().smc_path_pitch(65536, 0), 0)
+    assert kernel in (b"overlap_kernel", b"contract_kernel")
     lo, hi = make_domain_bounds().arrays()
     contracts = oracle.sobol_contracts(7, 0, B, lo, hi)
     np.testing.assert_array_equal(contracts[:2], gbm_golden["c2shape_contracts"])
@@ -157,8 +157,8 @@ def test_c2_network_fused_step_matches_oracle(oracle) -> None:
     off = 0
     for (name, pg), pc in zip(model.named_parameters(), cpu_model.parameters(), strict=True):
         k = pc.numel()
-        a, b = pg.detach().cpu().double().reshape(-1), pc.detach().double().reshape(-1)
-        resolved = g_cpu[off:off + k].abs() > 1e-5 * float(g_cpu.abs().max())
-        assert float((a - b)[resolved].abs().max(initial=0.0)) < 1e-5, name
-        assert int((~resolved & ((a - b).abs() > 1e-5)).sum()) <= max(2, k // 1000), name
+        a, b = pg.detach().cpu().double().reshape(-1).numpy(), pc.detach().double().reshape(-1).numpy()
+        resolved = (g_cpu[off:off + k].abs() > 1e-5 * float(g_cpu.abs().max())).numpy()
+        assert float(np.abs(a - b)[resolved].max(initial=0.0)) < 1e-5, name
+        assert int((~resolved & (np.abs(a - b) > 1e-5)).sum()) <= max(2, k // 1000), name
         off += k

@@ -14,6 +14,7 @@ import torch
 from spectralmc.gbm import BlackScholes
 from spectralmc.gbm_trainer import GbmCVNNPricer
 from spectralmc.models.numerical import Precision
+from spectralmc.result import Failure
 from tests.helpers import (
     expect_success,
     make_black_scholes_config,
@@ -97,22 +98,30 @@ def test_graph_replay_matches_eager() -> None:
     assert r_e.final_loss == r_g.final_loss
 
 
-def test_lockstep_training_is_bit_exact() -> None:
-    a, ma = _pricer()
-    b, mb = _pricer()
+PRECISIONS = [torch.float32, torch.float64]  # reference tests/helpers/fixtures.py:19-107
+
+
+@pytest.mark.parametrize("dtype", PRECISIONS)
+def test_lockstep_training_is_bit_exact(dtype) -> None:
+    """Reference tests/test_gbm_trainer.py:182-193 (both precisions)."""
+    a, ma = _pricer(dtype=dtype)
+    b, mb = _pricer(dtype=dtype)
     assert max_param_diff(ma, mb) == 0.0
     cfg = make_training_config(num_batches=4, batch_size=24)
     expect_success(a.train(cfg))
     expect_success(b.train(cfg))
     assert max_param_diff(ma, mb) == 0.0
+    assert all(p.dtype == dtype for p in ma.parameters())
 
 
-def test_snapshot_restore_continues_identically() -> None:
+@pytest.mark.parametrize("dtype", PRECISIONS)
+def test_snapshot_restore_continues_identically(dtype) -> None:
+    """Reference tests/test_gbm_trainer.py:201-263 (both precisions)."""
     cfg2 = make_training_config(num_batches=2, batch_size=16)
-    straight, m_s = _pricer()
+    straight, m_s = _pricer(dtype=dtype)
     expect_success(straight.train(make_training_config(num_batches=4, batch_size=16)))
 
-    first, m_f = _pricer()
+    first, m_f = _pricer(dtype=dtype)
     r1 = expect_success(first.train(cfg2))
     snap = r1.updated_config
     assert snap.global_step == 2 and snap.sobol_skip == 32
@@ -122,8 +131,10 @@ def test_snapshot_restore_continues_identically() -> None:
     assert max_param_diff(m_s, m_f) == 0.0
 
 
-def test_adam_state_round_trip() -> None:
-    p, _ = _pricer()
+@pytest.mark.parametrize("dtype", PRECISIONS)
+def test_adam_state_round_trip(dtype) -> None:
+    """Reference tests/test_gbm_trainer.py:271-294 (both precisions)."""
+    p, _ = _pricer(dtype=dtype)
     r = expect_success(p.train(make_training_config(num_batches=2, batch_size=8)))
     st = r.updated_config.optimizer_state
     assert st is not None and len(st.param_states) == len(list(r.updated_config.cvnn.parameters()))
@@ -131,7 +142,11 @@ def test_adam_state_round_trip() -> None:
     again = expect_success(type(st).from_torch(back))
     for pid, ps in st.param_states.items():
         assert ps.step == 2
-        assert torch.equal(expect_success(ps.exp_avg.to_torch()), expect_success(again.param_states[pid].exp_avg.to_torch()))
+        a = expect_success(ps.exp_avg.to_torch())
+        assert a.dtype == dtype
+        assert torch.equal(a, expect_success(again.param_states[pid].exp_avg.to_torch()))
+        assert torch.equal(expect_success(ps.exp_avg_sq.to_torch()),
+                           expect_success(again.param_states[pid].exp_avg_sq.to_torch()))
 
 
 def test_multi_chunk_equals_single_chunk(monkeypatch) -> None:
@@ -174,6 +189,114 @@ def test_predict_price_finite_and_parity() -> None:
         fwd = c.X0 * math.exp((c.r - c.d) * c.T)
         assert r.call_price - r.put_price == pytest.approx(fwd - c.K * math.exp(-c.r * c.T), rel=1e-9, abs=1e-9)
     assert expect_success(p.predict_price([])) == []
+
+
+@pytest.mark.parametrize("dtype", PRECISIONS)
+def test_predict_price_matches_cpu_ifft_mean(dtype) -> None:
+    """predict_price (reference gbm_trainer.py:1709-1767): CVNN spectrum -> ifft(dim=1).mean(1)
+    -> put = Re; call by put-call parity.  Compared with a torch-cpu copy of the same trained
+    weights running the reference's own arithmetic (forward, ifft, mean) in float64."""
+    p, model = _pricer(dtype=dtype)
+    expect_success(p.train(make_training_config(num_batches=3, batch_size=16)))
+    rng = np.random.default_rng(5)
+    contracts = [BlackScholes.Inputs(X0=float(rng.uniform(50, 150)), K=float(rng.uniform(50, 150)),
+                                     T=float(rng.uniform(0.1, 3.0)), r=float(rng.uniform(-0.05, 0.08)),
+                                     d=float(rng.uniform(0.0, 0.05)), v=float(rng.uniform(0.05, 0.8)))
+                 for _ in range(24)]
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)  # |Im| of an untrained spectrum's mean IFFT
+        got = expect_success(p.predict_price(contracts))
+    cpu = copy.deepcopy(model).cpu().double().eval()
+    x = torch.tensor([[c.X0, c.K, c.T, c.r, c.d, c.v] for c in contracts], dtype=torch.float64)
+    with torch.no_grad():
+        pr, pi = cpu(x, torch.zeros_like(x))
+        coeff = torch.fft.ifft(torch.complex(pr, pi), dim=1).mean(dim=1)
+    tol = 1e-5 if dtype == torch.float32 else 1e-10
+    for r, c, k in zip(got, contracts, coeff, strict=True):
+        scale = max(abs(float(k.real)), float(pr.abs().max()) / pr.shape[1])
+        assert r.put_price == pytest.approx(float(k.real), rel=0, abs=tol * scale)
+        disc, fwd = math.exp(-c.r * c.T), c.X0 * math.exp((c.r - c.d) * c.T)
+        assert r.call_price == pytest.approx(float(k.real) + fwd - c.K * disc, rel=0, abs=tol * scale + 1e-9 * fwd)
+        assert r.underlying == pytest.approx(fwd, rel=1e-12)
+        assert r.put_price_intrinsic == pytest.approx(disc * max(c.K - fwd, 0.0), rel=1e-12, abs=1e-12)
+
+
+def test_host_validated_path_logs_and_commits(tmp_path) -> None:
+    """A domain whose lower bounds admit invalid contracts (X0 lower = 0) takes the host-validated
+    loop: it calls the logger every step with the step's wall time, commits at the interval like
+    the device loop (reference _run_batch), trains the same contracts and targets as the device
+    loop, and stops with SequenceExhausted past 2^30 Sobol points."""
+    import asyncio
+
+    from spectralmc_amd.errors.sampler import SequenceExhausted
+    from spectralmc_amd.gbm_trainer import IntervalCommit
+    from spectralmc_amd.sobol_sampler import MAX_POINTS
+    from spectralmc_amd.storage import AsyncBlockchainModelStore
+
+    sp = _sim()
+    bounds = make_domain_bounds(x0=(0.0, 10_000.0))
+
+    def make(seed: int = 123, sobol_skip: int = 0):
+        m = make_test_cvnn(n_inputs=6, n_outputs=N, seed=seed, dtype=torch.float32)
+        cfg = make_gbm_cvnn_config(m, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                                   domain_bounds=bounds, sobol_skip=sobol_skip)
+        return expect_success(GbmCVNNPricer.create(cfg)), m
+
+    store = AsyncBlockchainModelStore(tmp_path / "store")
+    checked, m_c = make()
+    logged = []
+    res = expect_success(checked.train(make_training_config(num_batches=3, batch_size=16), logger=logged.append,
+                                       blockchain_store=store, commit_plan=IntervalCommit(interval=1)))
+    assert [m.step for m in logged] == [1, 2, 3]
+    assert all(math.isfinite(m.batch_time) and m.batch_time > 0 for m in logged)
+    assert logged[-1].loss == res.final_loss
+    versions = asyncio.run(store.list_versions())
+    assert len(versions) == 3
+    assert res.updated_config.global_step == 3 and res.updated_config.sobol_skip == 48
+    # the same three steps on the device loop (positive bounds give the same Sobol rows here)
+    dev_bounds = make_domain_bounds(x0=(1e-300, 10_000.0))
+    m_d = make_test_cvnn(n_inputs=6, n_outputs=N, seed=123, dtype=torch.float32)
+    dcfg = make_gbm_cvnn_config(m_d, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                                domain_bounds=dev_bounds)
+    dev = expect_success(GbmCVNNPricer.create(dcfg))
+    dev.fused_network = False  # the checked loop runs the torch _torch_step
+    r_d = expect_success(dev.train(make_training_config(num_batches=3, batch_size=16)))
+    assert r_d.final_loss == pytest.approx(res.final_loss, rel=1e-5)
+    late, _ = make(sobol_skip=MAX_POINTS - 20)
+    out = late.train(make_training_config(num_batches=2, batch_size=16))
+    assert isinstance(out, Failure) and isinstance(out.error.error, SequenceExhausted)
+
+
+def test_c1_training_step_pair_matches_reference_fixture() -> None:
+    """Two C1 training steps on the GPU (B = 64, T = 16, N = 256, M = 4, mc_seed 7, CVNN
+    6 -> 32 modReLU -> 256 seed 123, lr 1e-2) against the loss / grad norm / weights the
+    reference's own gbm.py + cvnn_factory + _torch_step produced (tests/golden/gbm_golden.npz)."""
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with np.load(os.path.join(root, "tests", "golden", "gbm_golden.npz"), allow_pickle=False) as data:
+        g = {k: data[k] for k in data.files}
+    sp = make_simulation_params(timesteps=16, network_size=256, batches_per_mc_run=4, mc_seed=7, buffer_size=1,
+                                dtype=Precision.float32)
+    for steps in (1, 2):
+        model = make_test_cvnn(n_inputs=6, n_outputs=256, seed=123, dtype=torch.float32)
+        for k, v in model.state_dict().items():
+            np.testing.assert_array_equal(v.cpu().numpy(), g[f"step_init__{k}"])
+        cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                                   domain_bounds=make_domain_bounds())
+        pricer = expect_success(GbmCVNNPricer.create(cfg))
+        res = expect_success(pricer.train(make_training_config(num_batches=steps, batch_size=64, learning_rate=1e-2)))
+        s = steps - 1
+        assert res.final_loss == pytest.approx(float(g[f"step{s}_loss"]), rel=1e-4)       # north-star 1e-4
+        assert res.final_grad_norm == pytest.approx(float(g[f"step{s}_gradnorm"]), rel=1e-3)
+        for k, v in model.state_dict().items():
+            ref = g[f"step{s}_after__{k}"]
+            diff = np.abs(v.detach().cpu().numpy() - ref)
+            # 2 Adam steps of lr 1e-2 (|update| ~ lr sign(g)): equal to f32 noise except where a
+            # gradient element is ~0 and may take either sign
+            assert int((diff > 2e-4).sum()) <= max(2, diff.size // 1000), k
 
 
 def test_gbm_engine_price_vs_black(oracle) -> None:
