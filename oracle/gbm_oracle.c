@@ -348,10 +348,16 @@ int32_t oracle_num_threads(void) {
  * that many paths (gbm.hip kSliceChunks * kChunk = 8192 when smc_train_targets gets a workspace),
  * each reduced like a whole contract, and the slice sums are added in slice order from 0.0. */
 void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t P, uint64_t seed, int64_t ordinal0,
-                         int32_t scheme, int64_t slice_paths, float* paths, float* terminal, double* rowsum) {
+                         int32_t scheme, int64_t slice_paths, int32_t wg, float* paths, float* terminal,
+                         double* rowsum) {
+  /* wg: lanes of the engine workgroup (512: contract/paths/queue kernels; 1024: resident_kernel) —
+   * sets the chunk (4 wg paths) and the wave count of the row-sum order */
+  const int lanes = wg > 0 ? wg : K_THREADS;
+  const int64_t chunk_paths = (int64_t)K_PPL * lanes;
+  const int waves = lanes / 64;
   const double kLog2e = 1.4426950408889634;
   float* X = (float*)malloc(sizeof(float) * (size_t)T * (size_t)P);
-  double* lane_acc = (double*)malloc(sizeof(double) * (size_t)K_THREADS * (size_t)T);
+  double* lane_acc = (double*)malloc(sizeof(double) * (size_t)lanes * (size_t)T);
   for (int64_t b = 0; b < B; ++b) {
     const double* c = contracts + 6 * b;
     const double dt = c[2] / (double)T;
@@ -398,9 +404,9 @@ void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t 
     for (int64_t p_begin = 0; p_begin < P; p_begin += span) {
       const int64_t p_end = p_begin + span < P ? p_begin + span : P;
       /* per lane: sequential over the slice's chunks of f32 4-path partial sums, in f64 */
-      memset(lane_acc, 0, sizeof(double) * (size_t)K_THREADS * (size_t)T);
-      for (int64_t chunk = p_begin; chunk < p_end; chunk += K_CHUNK)
-        for (int lane = 0; lane < K_THREADS; ++lane) {
+      memset(lane_acc, 0, sizeof(double) * (size_t)lanes * (size_t)T);
+      for (int64_t chunk = p_begin; chunk < p_end; chunk += chunk_paths)
+        for (int lane = 0; lane < lanes; ++lane) {
           const int64_t p0 = chunk + (int64_t)K_PPL * lane;
           for (int t = 0; t < T; ++t) {
             float part = 0.0f;
@@ -410,7 +416,7 @@ void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t 
         }
       for (int t = 0; t < T; ++t) {
         double tot = 0.0;
-        for (int w = 0; w < K_WAVES; ++w) {
+        for (int w = 0; w < waves; ++w) {
           double v[64], nv[64];
           for (int l = 0; l < 64; ++l) v[l] = lane_acc[(size_t)(64 * w + l) * T + t];
           for (int off = 32; off >= 1; off >>= 1) {
@@ -428,19 +434,54 @@ void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t 
   free(X);
 }
 
+/* gbm.hip use_fft / fft_row: power-of-two N in 2..2048 takes the radix-2 DIT FFT (bit-reversed
+ * load, stage len = 2..N, butterfly t = x[i1] (cs - i sn)[(j mod h) N/len] with 4 products and 2
+ * sums, x[i1] = x[i0] - t, x[i0] = x[i0] + t); other N the direct DFT chains. */
+static int use_fft(int N) { return N >= 2 && (N & (N - 1)) == 0 && N <= 2048; }
+
+static void fft_real(const double* avg, const double* cs, const double* sn, int N, double* xr, double* xi) {
+  int logN = 0;
+  while ((1 << logN) < N) ++logN;
+  for (int n = 0; n < N; ++n) {
+    unsigned r = 0;
+    for (int bit = 0; bit < logN; ++bit) r |= (unsigned)((n >> bit) & 1) << (logN - 1 - bit);
+    xr[r] = avg[n];
+    xi[r] = 0.0;
+  }
+  for (int s = 1; s <= logN; ++s) {
+    const int h = 1 << (s - 1), shift = logN - s;
+    for (int j = 0; j < N / 2; ++j) {
+      const int pos = j & (h - 1);
+      const int i0 = ((j >> (s - 1)) << s) + pos, i1 = i0 + h;
+      const double wr = cs[pos << shift], wi = -sn[pos << shift];
+      const double ar = xr[i1], ai = xi[i1];
+      const double tr = ar * wr - ai * wi;
+      const double ti = ar * wi + ai * wr;
+      const double br = xr[i0], bi = xi[i0];
+      xr[i1] = br - tr;
+      xi[i1] = bi - ti;
+      xr[i0] = br + tr;
+      xi[i0] = bi + ti;
+    }
+  }
+}
+
 /* targets: [B][N] interleaved complex64 (re, im) */
-void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, int32_t normalize,
+void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, int32_t normalize, int32_t wg,
                       const float* terminal, const double* terminal_sum, float* targets) {
+  const int lanes = wg > 0 ? wg : K_THREADS;  /* G = lanes / column quads (resident_kernel: 4096 / N) */
   const int64_t P = (int64_t)N * M;
   /* gbm.hip cf_targets_contract: with N % 4 == 0 a thread owns 4 adjacent columns (16-B loads),
    * so the m-groups per column are counted over N/4 column quads */
   const int cols = (N % 4 == 0 && P < ((int64_t)1 << 29)) ? N / 4 : N;
-  const int G = cols <= K_THREADS ? K_THREADS / cols : 1;
+  const int G = cols <= lanes ? lanes / cols : 1;
   const int items = N * G;
   double* part = (double*)malloc(sizeof(double) * (size_t)items);
   double* avg = (double*)malloc(sizeof(double) * (size_t)N);
   double* cs = (double*)malloc(sizeof(double) * (size_t)N);
   double* sn = (double*)malloc(sizeof(double) * (size_t)N);
+  double* xr = (double*)malloc(sizeof(double) * (size_t)N);
+  double* xi = (double*)malloc(sizeof(double) * (size_t)N);
   for (int j = 0; j < N; ++j) twiddle(j, N, &sn[j], &cs[j]);
   for (int64_t b = 0; b < B; ++b) {
     const double* c = contracts + 6 * b;
@@ -467,6 +508,18 @@ void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, 
       avg[n] = tot / (double)M;
     }
     float* out = targets + 2 * b * N;
+    if (use_fft(N)) {
+      fft_real(avg, cs, sn, N, xr, xi);
+      for (int k = 0; k <= N / 2; ++k) {
+        out[2 * k] = (float)xr[k];
+        out[2 * k + 1] = (float)xi[k];
+        if (k != 0 && 2 * k != N) {
+          out[2 * (N - k)] = (float)xr[k];
+          out[2 * (N - k) + 1] = (float)(-xi[k]);
+        }
+      }
+      continue;
+    }
     for (int k = 0; k <= N / 2; ++k) {
       double re = 0.0, im = 0.0;
       int idx = 0;
@@ -484,6 +537,8 @@ void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, 
       }
     }
   }
+  free(xr);
+  free(xi);
   free(part);
   free(avg);
   free(cs);

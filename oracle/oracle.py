@@ -61,9 +61,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_num_threads.restype = ctypes.c_int32
         L.oracle_kernel_paths.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
                                           ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
-                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+                                          ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_kernel_cf.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
-                                       ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p]
         L.oracle_basket_kernel.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64,
                                            ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -198,38 +199,51 @@ SLICE_PATHS = 8192
 
 
 def kernel_paths(contracts: np.ndarray, timesteps: int, n_paths: int, seed: int, ordinal0: int = 0,
-                 scheme: int = 0, want_paths: bool = False,
-                 sliced: bool = False) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
+                 scheme: int = 0, want_paths: bool = False, sliced: bool = False,
+                 wg: int = 512) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
     """f32 KERNEL mode: exact restatement of the HIP engine (paths, terminal, rowsum in its order).
-    sliced: row sums in the sliced-contract order (engine with a workspace)."""
+    sliced: row sums in the sliced-contract order (engine with a workspace); wg: lanes of the
+    engine workgroup whose reduction order to follow (1024 = resident_kernel)."""
     contracts = np.ascontiguousarray(contracts, dtype=np.float64)
     B = contracts.shape[0]
     paths = np.empty((B, timesteps, n_paths), dtype=np.float32) if want_paths else None
     terminal = np.empty((B, n_paths), dtype=np.float32)
     rowsum = np.empty((B, timesteps), dtype=np.float64)
     lib().oracle_kernel_paths(_ptr(contracts), B, timesteps, n_paths, seed, ordinal0, scheme,
-                              SLICE_PATHS if sliced else 0, _ptr(paths), _ptr(terminal), _ptr(rowsum))
+                              SLICE_PATHS if sliced else 0, wg, _ptr(paths), _ptr(terminal), _ptr(rowsum))
     return paths, terminal, rowsum
 
 
 def kernel_cf(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndarray, network_size: int,
-              batches: int, normalize: bool = True) -> np.ndarray:
+              batches: int, normalize: bool = True, wg: int = 512) -> np.ndarray:
     contracts = np.ascontiguousarray(contracts, dtype=np.float64)
     terminal = np.ascontiguousarray(terminal, dtype=np.float32)
     terminal_sum = np.ascontiguousarray(terminal_sum, dtype=np.float64)
     out = np.empty((contracts.shape[0], network_size), dtype=np.complex64)
-    lib().oracle_kernel_cf(_ptr(contracts), contracts.shape[0], network_size, batches, int(normalize),
+    lib().oracle_kernel_cf(_ptr(contracts), contracts.shape[0], network_size, batches, int(normalize), wg,
                            _ptr(terminal), _ptr(terminal_sum), _ptr(out))
     return out
 
 
+def engine_wg(timesteps: int, network_size: int, n_paths: int, with_rowsum: bool = False,
+              sliced: bool = False) -> int:
+    """Lanes of the engine workgroup smc_train_targets uses for an f32 training launch: 1024 for
+    resident_kernel (T = 16, 4096 | P <= 65,536, N | 4096, N <= 1024, no row sums, no workspace),
+    512 otherwise (gbm.hip resident_ok)."""
+    N, P = network_size, n_paths
+    ok = (timesteps == 16 and not with_rowsum and not sliced and P % 4096 == 0 and P // 4096 <= 16
+          and 4 <= N <= 1024 and 4096 % N == 0)
+    return 1024 if ok else 512
+
+
 def kernel_targets(contracts: np.ndarray, timesteps: int, network_size: int, batches: int, seed: int,
                    ordinal0: int = 0, scheme: int = 0, normalize: bool = True,
-                   sliced: bool = False) -> tuple[np.ndarray, np.ndarray]:
-    """(targets [B,N] complex64, rowsum [B,T]) exactly as the f32 HIP engine computes them."""
+                   sliced: bool = False, wg: int = 512) -> tuple[np.ndarray, np.ndarray]:
+    """(targets [B,N] complex64, rowsum [B,T]) exactly as the f32 HIP engine computes them
+    (wg: engine_wg(...) of the launch)."""
     _, terminal, rowsum = kernel_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme,
-                                       sliced=sliced)
-    return kernel_cf(contracts, terminal, rowsum[:, -1], network_size, batches, normalize), rowsum
+                                       sliced=sliced, wg=wg)
+    return kernel_cf(contracts, terminal, rowsum[:, -1], network_size, batches, normalize, wg=wg), rowsum
 
 
 # --------------------------------------------------------------------------- basket (extension)

@@ -209,7 +209,8 @@ template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS, bool MASKED, boo
           bool STRAIGHT_ALL = true>
 __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                            uint64_t ordinal, int64_t chunk, int nvalid, int t0, int nrows,
-                                           Real* contract_base, double (&acc)[ALLROWS ? kRowBlock : 1]) {
+                                           Real* contract_base, double (&acc)[ALLROWS ? kRowBlock : 1],
+                                           Real* x_out = nullptr) {
   using V4 = typename Vec4T<Real>::type;
   const int T = a.T;
   const int64_t P = a.P;
@@ -283,6 +284,10 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
         acc[ALLROWS ? i : 0] += static_cast<double>(part);
       }
     }
+  }
+  if (x_out) {  // the lane's final values (the terminal row when t0 + nrows == T)
+#pragma unroll
+    for (int j = 0; j < kPathsPerLane; ++j) x_out[j] = x[j];
   }
 }
 
@@ -453,6 +458,70 @@ __device__ __forceinline__ void quad_column_sums(const float* row, const Payoff<
   }
 }
 
+// Power-of-two N (2..2048): the targets come from an in-LDS radix-2 FFT instead of the O(N^2)
+// DFT (at C3, N = 1024, the DFT chains were ~20 us per contract).  oracle/gbm_oracle.c restates
+// both; the CF phase's LDS work area holds the FFT's re / im arrays in place of the group sums.
+__host__ __device__ inline bool use_fft(int N) { return N >= 2 && (N & (N - 1)) == 0 && N <= 2048; }
+__host__ __device__ inline int cf_part_doubles(int N) {
+  const int need = use_fft(N) ? 2 * N : N;
+  return need > 4 * kThreads ? need : 4 * kThreads;
+}
+
+// In-place radix-2 decimation-in-time FFT of the real sequence avg[0..N) into xr/xi (LDS), then
+// bins 0..N/2 and their Hermitian mirror -> out.  Stage len = 2, 4, ..., N: butterfly j of N/2,
+// i0 = (j / h) len + j mod h, i1 = i0 + h (h = len/2), w = cs[t] - i sn[t] with t = (j mod h) N/len:
+// (tr, ti) = x[i1] w (4 products, 2 sums, no contraction), x[i1] = x[i0] - t, x[i0] = x[i0] + t.
+__device__ __forceinline__ void lds_barrier() {  // LDS visibility only: no vmcnt drain of the stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <typename Real, int NT = kThreads, bool LDS_ONLY = false>
+__device__ void fft_row(const double* avg, const double* cs, const double* sn, int N, double* xr, double* xi,
+                        typename Complex2<Real>::type* out) {
+  using C2 = typename Complex2<Real>::type;
+  const int tid = threadIdx.x;
+  const int logN = 31 - __builtin_clz(static_cast<unsigned>(N));
+  auto barrier = [] {
+    if constexpr (LDS_ONLY) lds_barrier();
+    else __syncthreads();
+  };
+  for (int n = tid; n < N; n += NT) {
+    const int r = static_cast<int>(__builtin_bitreverse32(static_cast<unsigned>(n)) >> (32 - logN));
+    xr[r] = avg[n];
+    xi[r] = 0.0;
+  }
+  barrier();
+  for (int s = 1; s <= logN; ++s) {
+    const int h = 1 << (s - 1), shift = logN - s;  // twiddle index t = (j mod h) << shift
+    for (int j = tid; j < N / 2; j += NT) {
+      const int pos = j & (h - 1);
+      const int i0 = ((j >> (s - 1)) << s) + pos, i1 = i0 + h;
+      const double wr = cs[pos << shift], wi = -sn[pos << shift];
+      const double ar = xr[i1], ai = xi[i1];
+      const double tr = ar * wr - ai * wi;
+      const double ti = ar * wi + ai * wr;
+      const double br = xr[i0], bi = xi[i0];
+      xr[i1] = br - tr;
+      xi[i1] = bi - ti;
+      xr[i0] = br + tr;
+      xi[i0] = bi + ti;
+    }
+    barrier();
+  }
+  for (int k = tid; k <= N / 2; k += NT) {
+    C2 v;
+    v.x = static_cast<Real>(xr[k]);
+    v.y = static_cast<Real>(xi[k]);
+    out[k] = v;
+    if (k != 0 && 2 * k != N) {
+      v.y = static_cast<Real>(-xi[k]);
+      out[N - k] = v;
+    }
+  }
+}
+
 template <typename Real>
 __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int64_t b,
                                     double terminal_sum, double* lds) {
@@ -473,12 +542,15 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
   const int cols = quad ? N / 4 : N;
   const int G = cols <= kThreads ? kThreads / cols : 1;
   const int items = cols * G;
-  double* part = lds;                                            // [max(4 kThreads, N)]
-  double* avg = part + (N > 4 * kThreads ? N : 4 * kThreads);    // [N]
+  double* part = lds;                                            // [cf_part_doubles(N)]
+  double* avg = part + cf_part_doubles(N);                       // [N]
   double* cs = avg + N;                                          // [N]
   double* sn = cs + N;                                           // [N]
 
-  constexpr int kBatch = 16;  // loads in flight per thread; the sum keeps the m order
+#ifndef SMC_CF_BATCH
+#define SMC_CF_BATCH 8
+#endif
+  constexpr int kBatch = SMC_CF_BATCH;  // loads in flight per thread; the sum keeps the m order
   if constexpr (sizeof(Real) == 4) {
     if (quad) quad_column_sums<kBatch>(row, pay, N, M, cols, G, part, tid, kThreads);
   }
@@ -506,7 +578,10 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
     avg[n] = tot / static_cast<double>(M);
   }
   __syncthreads();
-  dft_row<Real>(avg, cs, sn, N, static_cast<C2*>(a.targets) + b * N);
+#if !defined(SMC_CF_NO_DFT)  // tools/micro decomposition builds only
+  if (use_fft(N)) fft_row<Real>(avg, cs, sn, N, part, part + N, static_cast<C2*>(a.targets) + b * N);
+  else dft_row<Real>(avg, cs, sn, N, static_cast<C2*>(a.targets) + b * N);
+#endif
 }
 
 // Slice k of contract b (paths [k S, (k+1) S), S = kSliceChunks * kChunk; the whole contract
@@ -596,30 +671,41 @@ __device__ __forceinline__ double* pad_sum(const EngineArgs& a, int64_t b) {
 // STRAIGHT (T == 16, P a multiple of 2048): only the straight-line 16-row block is compiled in
 // (STORE_ALL: every row; else the terminal row), so the kernel needs ~60 VGPRs instead of ~100.
 // The terminal sum keeps simulate_contract's order: lane over chunks, wave butterfly, waves 0..7.
+// STRAIGHT launches are persistent: the resident workgroups run contracts b = blockIdx.x,
+// + gridDim.x, ... back to back, so no workgroup drains its store queue between contracts (a
+// wave retires only once its stores are acknowledged) and the chip never runs whole rounds of
+// workgroups that start, ramp up and drain together.  The per-contract barrier is LDS-only.
 template <bool LOG_EULER, bool HW, bool STRAIGHT, bool STORE_ALL>
 __global__ __launch_bounds__(kThreads) void paths_kernel(EngineArgs a) {
   extern __shared__ double lds[];
-  const int64_t b = blockIdx.x;
-  const Contract c = load_contract(a.contracts + b * 6);
-  const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
+  const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
   if constexpr (STRAIGHT) {
-    const Stepper<float, LOG_EULER, HW> step(c, kRowBlock);
-    const float x0 = static_cast<float>(c.X0);
     const int64_t pitch = a.pitch ? a.pitch : a.P;
-    float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * kRowBlock * pitch : b * pitch);
-    double acc[1] = {0.0};
-    for (int64_t chunk = 0; chunk < a.P; chunk += kChunk)
-      lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(a, step, x0, ordinal, chunk,
-                                                                             kPathsPerLane, 0, kRowBlock, base, acc);
-    const double w = wave_sum(acc[0]);
-    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = w;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double tot = 0.0;
-      for (int k = 0; k < kWaves; ++k) tot += lds[k];
-      *pad_sum(a, b) = tot;
+    int parity = 0;
+    for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x, parity ^= 1) {
+      const Contract c = load_contract(a.contracts + b * 6);
+      const Stepper<float, LOG_EULER, HW> step(c, kRowBlock);
+      const float x0 = static_cast<float>(c.X0);
+      float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * kRowBlock * pitch : b * pitch);
+      double acc[1] = {0.0};
+      for (int64_t chunk = 0; chunk < a.P; chunk += kChunk)
+        lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(
+            a, step, x0, static_cast<uint64_t>(ord0 + b), chunk, kPathsPerLane, 0, kRowBlock, base, acc);
+      // wave sums in a double-buffered LDS slot: the next contract writes the other slot
+      const double w = wave_sum(acc[0]);
+      double* ws = lds + parity * kWaves;
+      if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = w;
+      lds_barrier();
+      if (threadIdx.x == 0) {
+        double tot = 0.0;
+        for (int k = 0; k < kWaves; ++k) tot += ws[k];
+        *pad_sum(a, b) = tot;
+      }
     }
   } else {
+    const int64_t b = blockIdx.x;
+    const Contract c = load_contract(a.contracts + b * 6);
+    const uint64_t ordinal = static_cast<uint64_t>(ord0 + b);
     simulate_contract<float, LOG_EULER, HW, false>(a, c, ordinal, b, 0, a.P, lds + a.T, lds);
     if (threadIdx.x == 0) *pad_sum(a, b) = lds[a.T - 1];
   }
@@ -631,6 +717,119 @@ __global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
   const int64_t b = blockIdx.x;
   const Contract c = load_contract(a.contracts + b * 6);
   cf_targets_contract<Real>(a, c, b, *pad_sum(a, b), lds);
+}
+
+// ---- resident_kernel: the terminal row never leaves the chip -----------------------------------
+// For P <= 65,536 a 1024-thread workgroup (4 paths per lane, 4096-path chunks, <= 16 chunks) keeps
+// the contract's whole terminal row on chip next to its stores: chunks 0..7 in LDS (128 KiB, one
+// 16-B slot per lane and chunk), later chunks in registers.  Once the contract's terminal sum is
+// known the workgroup evaluates the payoffs from there: lane l of chunk c holds batch
+// m = g + c G (G = 4096 / N, g = 4 l / N) of column quad q = l mod N/4, so each lane's 4 column
+// sums over its chunks are the items (q, g) of the CF phase, summed over m ascending; then the G
+// group sums in order, the M-mean and the FFT (N divides 4096).  No re-read of the terminal row
+// (1.07 GB per C2 step), no CF kernel, no store drain: every barrier is LDS-only.  Persistent: one
+// workgroup per CU runs contracts blockIdx.x, + gridDim.x, ...  Reduction orders follow 1024
+// lanes (oracle kernel mode, wg = 1024): lane over chunks, wave butterfly, waves 0..15 for the
+// terminal sum; item sums in ascending m, groups in order.
+constexpr int kResThreads = 1024;
+constexpr int kResWaves = kResThreads / 64;
+constexpr int kResChunk = kResThreads * kPathsPerLane;  // 4096 paths
+constexpr int kResMaxChunks = 16;
+constexpr int kResLdsChunks = 8;                        // chunks parked in LDS
+constexpr int kResRegChunks = kResMaxChunks - kResLdsChunks;
+constexpr size_t kResTermBytes = static_cast<size_t>(kResLdsChunks) * kResThreads * 16;  // 128 KiB
+
+size_t resident_lds_bytes(int N) {
+  return kResTermBytes + (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N)) * sizeof(double);
+}
+
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
+__global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = a.N, M = a.M;
+  const int64_t P = a.P;
+  const int64_t pitch = a.pitch ? a.pitch : P;
+  const int nch = static_cast<int>(P / kResChunk);
+  const int cols = N / 4;
+  const int G = kResChunk / N;            // batch rows per chunk
+  const int q = tid % cols, g = tid / cols;
+  v4f* term_lds = reinterpret_cast<v4f*>(lds);                      // [kResLdsChunks][kResThreads]
+  double* part = lds;                     // [G][N] = [4096], aliases term_lds once it is consumed;
+                                          // FFT re / im after the M-mean
+  double* wsum = lds + kResTermBytes / sizeof(double);              // [kResWaves]
+  double* avg = wsum + kResWaves;         // [N]
+  double* cs = avg + N;                   // [N]
+  double* sn = cs + N;                    // [N]
+  for (int j = tid; j < N; j += kResThreads) math::twiddle(j, N, sn[j], cs[j]);
+  const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    const Contract c = load_contract(a.contracts + b * 6);
+    const Stepper<float, LOG_EULER, HW> step(c, kRowBlock);
+    const float x0 = static_cast<float>(c.X0);
+    float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * kRowBlock * pitch : b * pitch);
+    // chunks >= kResLdsChunks: a shift register with static indices (a rolled loop indexing a
+    // register array would put it in scratch memory); chunk ch ends in slot ch - nch + kResRegChunks
+    float term[kResRegChunks][kPathsPerLane];
+    double acc[1] = {0.0};
+    for (int ch = 0; ch < nch; ++ch) {
+      float xt[kPathsPerLane];
+      lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(
+          a, step, x0, static_cast<uint64_t>(ord0 + b), static_cast<int64_t>(ch) * kResChunk, kPathsPerLane, 0,
+          kRowBlock, base, acc, xt);
+      if (ch < kResLdsChunks) {
+        term_lds[ch * kResThreads + tid] = v4f{xt[0], xt[1], xt[2], xt[3]};
+      } else {
+#pragma unroll
+        for (int i = 0; i + 1 < kResRegChunks; ++i)
+#pragma unroll
+          for (int j = 0; j < kPathsPerLane; ++j) term[i][j] = term[i + 1][j];
+#pragma unroll
+        for (int j = 0; j < kPathsPerLane; ++j) term[kResRegChunks - 1][j] = xt[j];
+      }
+    }
+    const double w = wave_sum(acc[0]);
+    if (lane == 0) wsum[wave] = w;
+    lds_barrier();
+    double tot = 0.0;
+    for (int k = 0; k < kResWaves; ++k) tot += wsum[k];
+    const Payoff<float> pay(a, c, tot);
+    double colsum[kPathsPerLane] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ch = 0; ch < kResLdsChunks; ++ch) {
+      if (ch < nch) {
+        const v4f v = term_lds[ch * kResThreads + tid];
+#pragma unroll
+        for (int j = 0; j < kPathsPerLane; ++j) colsum[j] += static_cast<double>(pay(v[j]));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kResRegChunks; ++i) {
+      if (i >= kResRegChunks - (nch - kResLdsChunks)) {  // chunk kResLdsChunks + i - (...), ascending
+#pragma unroll
+        for (int j = 0; j < kPathsPerLane; ++j) colsum[j] += static_cast<double>(pay(term[i][j]));
+      }
+    }
+    lds_barrier();  // every lane has read its LDS slots: part may overwrite them
+#pragma unroll
+    for (int j = 0; j < kPathsPerLane; ++j) part[g * N + 4 * q + j] = colsum[j];
+    lds_barrier();
+    for (int n = tid; n < N; n += kResThreads) {
+      double t = 0.0;
+      for (int gg = 0; gg < G; ++gg) t += part[gg * N + n];
+      avg[n] = t / static_cast<double>(M);
+    }
+    lds_barrier();
+    fft_row<float, kResThreads, true>(avg, cs, sn, N, part, part + N, static_cast<float2*>(a.targets) + b * N);
+    lds_barrier();  // part (= term_lds) / avg / wsum are reused by the next contract
+  }
+}
+
+bool resident_ok(const EngineArgs& a, bool f32) {
+  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T == kRowBlock &&
+         a.P % kResChunk == 0 && a.P / kResChunk <= kResMaxChunks && a.N >= 4 && a.N <= 1024 &&
+         kResChunk % a.N == 0 && (a.pitch == 0 || a.pitch % 4 == 0);
 }
 
 bool split_ok(const EngineArgs& a, bool f32) {
@@ -675,180 +874,6 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void queue_kernel(EngineA
     for (int x = 0; x < 8; ++x) drain_queue(x);
     if (threadIdx.x < 9) __hip_atomic_store(queues + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-// ---- overlap_kernel: the training shape with the CF phase moved off the store stream ----------
-// A persistent workgroup of 8 compute waves + 1 CF wave runs contracts b = blockIdx.x, + gridDim.x,
-// ...  The compute waves simulate contract b (the contract kernel's straight-line 16-row block,
-// same streams, stores and terminal-sum order) while the CF wave runs the payoff, M-mean and DFT
-// of the workgroup's previous contract — so no wave ever drains its store queue between contracts
-// and the 256 KB terminal-row re-read streams beside the next contract's stores instead of after
-// a chip-wide synchronised drain (contract_kernel's rounds all reach their CF phase together).
-// Hand-off, per contract iteration k (contract b_k; the CF wave holds b_{k-1}):
-//   BAR1  compute waves: after chunk 0 of b_k, `s_waitcnt vmcnt(R)` (R = stores per chunk) — every
-//         store of b_{k-1} is older than chunk 0's R stores, so all of them are done (in L2, this
-//         XCD); the CF wave then re-reads b_{k-1}'s terminal row with L1-bypassing loads.
-//   BAR2  compute waves: wave sums of b_k's terminal row in LDS; the CF wave reads their total.
-// Barriers are LDS-only (no vmcnt drain).  Results are bit-identical to contract_kernel: same
-// per-lane streams, same row-sum order (lane over chunks, wave butterfly, waves 0..7), same CF
-// item arithmetic (quad_column_sums) and DFT chains.
-constexpr int kOverlapThreads = kThreads + 64;
-
-__device__ __forceinline__ void lds_barrier() {  // LDS visibility only: no vmcnt drain of the stores
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-__device__ __forceinline__ void wave_lds_sync() {  // this wave's LDS writes visible to its own lanes
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-}
-
-// The CF wave reads the terminal row as P / 256 pieces of 1 KiB — one global_load_lds_dwordx4 each
-// (no VGPR destination) — through an LDS ring that keeps kRing - 1 pieces in flight: the re-read
-// runs beside the compute waves' store stream, where one read's latency is long.
-constexpr int kRing = 32;
-constexpr int kPiece = 256;  // floats per piece (64 lanes x 16 B)
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
-
-size_t overlap_lds_bytes(int N) {
-  return (static_cast<size_t>(kWaves) + 4 * static_cast<size_t>(kThreads) + 3 * static_cast<size_t>(N)) *
-             sizeof(double) +
-         static_cast<size_t>(kRing) * kPiece * sizeof(float);
-}
-
-// Payoff sums of one contract's terminal row by ONE wave, streamed in row-major order: lane l of
-// piece i holds element e = 256 i + 4 l = (batch m = e / N, columns n0..n0+3 with n0 = e mod N),
-// and adds the 4 payoffs to part[m mod G][n0..n0+3].  Every item (column quad, group g) thus sums
-// its batches m = g, g + G, ... in ascending order from 0.0 — quad_column_sums' arithmetic.  One
-// piece covers 256 / N < G batch rows, so no two lanes of a piece share a part entry.
-__device__ void stream_column_sums(const float* row, const Payoff<float>& pay, int N, int64_t P, int G,
-                                   double* part, float* ring, int lane) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  for (int i = lane; i < G * N; i += 64) part[i] = 0.0;
-  const int pieces = static_cast<int>(P / kPiece);
-  auto issue = [&](int i) {
-    __builtin_amdgcn_global_load_lds(row + static_cast<int64_t>(kPiece) * i + 4 * lane,
-                                     (lds_void_ptr)(ring + (i % kRing) * kPiece), 16, 0,
-                                     16 /* sc1: L1-bypassing */);
-  };
-  const int pre = pieces < kRing - 1 ? pieces : kRing - 1;
-  for (int i = 0; i < pre; ++i) issue(i);
-  int n0 = (4 * lane) % N, g = ((4 * lane) / N) % G;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");  // part zeroed before the first add
-  for (int i = 0; i < pieces; ++i) {
-    if (i + kRing - 1 < pieces) {
-      issue(i + kRing - 1);
-      asm volatile("s_waitcnt vmcnt(31)" ::: "memory");  // piece i landed (kRing - 1 younger in flight)
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const v4f x = *reinterpret_cast<const v4f*>(ring + (i % kRing) * kPiece + 4 * lane);
-    double* p = part + g * N + n0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) p[e] += static_cast<double>(pay(x[e]));
-    n0 += kPiece;
-    while (n0 >= N) {
-      n0 -= N;
-      if (++g == G) g = 0;
-    }
-  }
-}
-static_assert(kRing == 32, "stream_column_sums waits with vmcnt(kRing - 1)");
-
-template <bool LOG_EULER, bool HW, bool STORE_ALL>
-__global__ __launch_bounds__(kOverlapThreads) __attribute__((amdgpu_waves_per_eu(5, 8)))
-void overlap_kernel(EngineArgs a) {
-  extern __shared__ double lds[];
-  constexpr int T = kRowBlock;
-  // wave index made provably wave-uniform: the role branch is uniform control flow
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int N = a.N, M = a.M;
-  const int64_t P = a.P;
-  const int64_t pitch = a.pitch ? a.pitch : P;
-  double* wsum = lds;                    // [kWaves]
-  double* part = lds + kWaves;           // [G][N] = [4 kThreads] (N <= 4 kThreads)
-  double* avg = part + 4 * kThreads;     // [N]
-  double* cs = avg + N;                  // [N]
-  double* sn = cs + N;                   // [N]
-  float* ring = reinterpret_cast<float*>(sn + N);  // [kRing][kPiece] (16-B aligned: N % 4 == 0)
-  const int64_t nk = (a.B - blockIdx.x + gridDim.x - 1) / gridDim.x;  // contracts of this workgroup
-  const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
-  auto row_of = [&](int64_t b) {
-    return static_cast<float*>(a.paths) + (STORE_ALL ? b * T * pitch : b * pitch);
-  };
-
-  if (wave < kWaves) {  // ---- compute waves: simulate and store, contract after contract
-    for (int64_t k = 0; k < nk; ++k) {
-      const int64_t b = blockIdx.x + k * gridDim.x;
-      const Contract c = load_contract(a.contracts + b * 6);
-      const Stepper<float, LOG_EULER, HW> step(c, T);
-      const float x0 = static_cast<float>(c.X0);
-      const uint64_t ordinal = static_cast<uint64_t>(ord0 + b);
-      float* base = row_of(b);
-      double acc[1] = {0.0};
-      for (int64_t chunk = 0; chunk < P; chunk += kChunk) {
-        lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(a, step, x0, ordinal, chunk,
-                                                                               kPathsPerLane, 0, kRowBlock, base, acc);
-        if (chunk == 0) {  // BAR1: every store of the previous contract has completed
-          if constexpr (STORE_ALL) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-          lds_barrier();
-        }
-      }
-      const double w = wave_sum(acc[0]);
-      if (lane == 0) wsum[wave] = w;
-      lds_barrier();  // BAR2
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();  // BAR1 of the tail: the last contract's stores are done
-    return;
-  }
-
-  // ---- CF wave: payoff, M-mean and DFT of the previous contract
-  for (int j = lane; j < N; j += 64) math::twiddle(j, N, sn[j], cs[j]);
-  const int cols = N / 4;
-  const int G = cols <= kThreads ? kThreads / cols : 1;
-  int64_t prev = -1;
-  double prev_tot = 0.0;
-#ifndef SMC_OVERLAP_CF_MODE
-#define SMC_OVERLAP_CF_MODE 0  // tools/micro decomposition builds: 1 no CF work, 2 no DFT, 4 CF wave prio 0
-#endif
-  if (SMC_OVERLAP_CF_MODE != 4) __builtin_amdgcn_s_setprio(3);  // issue before the compute waves
-  auto run_cf = [&](int64_t pb, double tot) {
-    if (SMC_OVERLAP_CF_MODE == 1) return;
-    const Contract c = load_contract(a.contracts + pb * 6);
-    const Payoff<float> pay(a, c, tot);
-    const float* row = row_of(pb) + (STORE_ALL ? static_cast<int64_t>(T - 1) * pitch : 0);
-    stream_column_sums(row, pay, N, P, G, part, ring, lane);
-    wave_lds_sync();
-    for (int n = lane; n < N; n += 64) {
-      double t = 0.0;
-      for (int g = 0; g < G; ++g) t += part[g * N + n];
-      avg[n] = t / static_cast<double>(M);
-    }
-    wave_lds_sync();
-    if (SMC_OVERLAP_CF_MODE != 2) dft_row<float>(avg, cs, sn, N, static_cast<float2*>(a.targets) + pb * N, lane, 64);
-    wave_lds_sync();  // part / avg are reused by the next contract
-  };
-  for (int64_t k = 0; k < nk; ++k) {
-    lds_barrier();  // BAR1
-    if (prev >= 0) run_cf(prev, prev_tot);
-    lds_barrier();  // BAR2
-    double tot = 0.0;
-    for (int w = 0; w < kWaves; ++w) tot += wsum[w];
-    prev = blockIdx.x + k * gridDim.x;
-    prev_tot = tot;
-  }
-  lds_barrier();  // tail BAR1
-  if (prev >= 0) run_cf(prev, prev_tot);
-}
-
-bool overlap_ok(const EngineArgs& a, bool f32) {
-  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T == kRowBlock && a.N % 4 == 0 &&
-         a.N <= 1024 && a.P % kChunk == 0 && a.P < (int64_t{1} << 29) && (a.pitch == 0 || a.pitch % 4 == 0);
 }
 
 // In-place forward normalisation of a stored [B][T][P] matrix (gbm.py:428-438).
@@ -901,7 +926,7 @@ size_t lds_bytes(int T, int N, bool cf) {
   size_t doubles = static_cast<size_t>(T);                       // lds_tot
   size_t work = static_cast<size_t>(kWaves) * kRowBlock;         // per-wave row partials
   if (cf) {
-    const size_t cfw = static_cast<size_t>(N > 4 * kThreads ? N : 4 * kThreads) + 3 * static_cast<size_t>(N);
+    const size_t cfw = static_cast<size_t>(cf_part_doubles(N)) + 3 * static_cast<size_t>(N);
     if (cfw > work) work = cfw;
   }
   const size_t bytes = (doubles + work) * sizeof(double);
@@ -979,54 +1004,20 @@ size_t workspace_bytes(int64_t B, int32_t T, int64_t P, bool all_rows) {
   return static_cast<size_t>(B) * W * (all_rows ? T : 1) * sizeof(double) + static_cast<size_t>(B + 16) * sizeof(uint32_t);
 }
 
-// Workgroups per CU for the overlap kernel: 2 (8 contracts per workgroup at C2; a third slot
-// would leave a partly filled last round).  SMC_OVERLAP_WGS_PER_CU overrides (tuning only; the
-// results do not depend on the grid).
-int overlap_wgs_per_cu() {
-  static int v = [] {
-    const char* e = getenv("SMC_OVERLAP_WGS_PER_CU");
-    const int x = e ? atoi(e) : 2;
-    return x >= 1 && x <= 8 ? x : 2;
+// Resident paths_kernel workgroups per CU (its ~42 VGPRs allow 4 x 512 threads); the
+// SMC_PATHS_WGS_PER_CU environment variable overrides (tuning only: results do not depend on it).
+int paths_wgs_per_cu() {
+  static const int v = [] {
+    const char* e = getenv("SMC_PATHS_WGS_PER_CU");
+    const int x = e ? atoi(e) : 4;
+    return x >= 1 && x <= 8 ? x : 4;
   }();
   return v;
 }
 
-template <bool LOG_EULER, bool HW, bool STORE_ALL>
-int32_t launch_overlap_k(const EngineArgs& a, hipStream_t stream) {
-  auto kernel = overlap_kernel<LOG_EULER, HW, STORE_ALL>;
-  const size_t lds = overlap_lds_bytes(a.N);
-  if (lds > 64 * 1024 &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          static_cast<int>(lds)) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(SMC_ERR_HIP, "overlap_kernel: cannot raise the dynamic LDS limit");
-  }
-  unsigned grid = 0;
-  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kOverlapThreads, lds, a.B, &grid)) return st;
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ==
-      hipSuccess && cus > 0) {
-    const int64_t cap = static_cast<int64_t>(overlap_wgs_per_cu()) * cus;
-    if (grid > cap) grid = static_cast<unsigned>(cap);
-  }
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kOverlapThreads), lds, stream, a);
-  return check_launch("overlap_kernel");
-}
-
-// Dynamic LDS of paths_kernel: its own need, or SMC_PATHS_LDS_KB (tuning: fewer resident
-// workgroups per CU).  The results do not depend on it.
-size_t paths_lds_bytes(size_t need) {
-  static const size_t pad = [] {
-    const char* e = getenv("SMC_PATHS_LDS_KB");
-    const long v = e ? atol(e) : 0;
-    return v > 0 && v <= 160 ? static_cast<size_t>(v) * 1024 : size_t{0};
-  }();
-  return pad > need ? pad : need;
-}
-
 template <bool LOG_EULER, bool HW, bool STRAIGHT, bool STORE_ALL>
 int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
-  const size_t lds1 = paths_lds_bytes(lds_bytes(a.T, a.N, false)), lds2 = lds_bytes(a.T, a.N, true);
+  const size_t lds1 = lds_bytes(a.T, a.N, false), lds2 = lds_bytes(a.T, a.N, true);
   auto k1 = paths_kernel<LOG_EULER, HW, STRAIGHT, STORE_ALL>;
   auto k2 = cf_kernel<float>;
   if ((lds1 > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(k1),
@@ -1038,22 +1029,66 @@ int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
     (void)hipGetLastError();
     return fail(SMC_ERR_HIP, "paths_kernel / cf_kernel: cannot raise the dynamic LDS limit");
   }
-  hipLaunchKernelGGL(k1, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds1, stream, a);
+  unsigned grid1 = static_cast<unsigned>(a.B);
+  if (STRAIGHT) {  // persistent: paths_wgs_per_cu() resident workgroups per CU
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+      (void)hipGetLastError();
+      return fail(SMC_ERR_HIP, "paths_kernel: device query failed");
+    }
+    const int64_t slots = static_cast<int64_t>(paths_wgs_per_cu()) * cus;
+    if (slots < a.B) grid1 = static_cast<unsigned>(slots);
+  }
+  hipLaunchKernelGGL(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
   if (int32_t st = check_launch("paths_kernel")) return st;
   hipLaunchKernelGGL(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
   return check_launch("cf_kernel");
 }
 
-// Training-shape kernel choice: 0 fused contract_kernel, 1 overlap_kernel, 2 paths + cf pair
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
+int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
+  auto kernel = resident_kernel<LOG_EULER, HW, STORE_ALL>;
+  const size_t lds = resident_lds_bytes(a.N);
+  if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "resident_kernel: cannot raise the dynamic LDS limit");
+  }
+  unsigned grid = 0;
+  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kResThreads, lds, a.B, &grid)) return st;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kResThreads), lds, stream, a);
+  return check_launch("resident_kernel");
+}
+
+// Training-shape kernel choice: 3 = resident_kernel where it applies (P <= 65,536), else the
+// paths_kernel + cf_kernel pair (2); 0 = the fused contract_kernel (tools/micro comparison builds)
 #ifndef SMC_TRAIN_MODE
-#define SMC_TRAIN_MODE 2
+#define SMC_TRAIN_MODE 3
 #endif
 
 template <typename Real>
 int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   if (a.B == 0) return SMC_OK;
   if constexpr (sizeof(Real) == 4) {
-    if (SMC_TRAIN_MODE == 2 && split_ok(a, true)) {
+    if (SMC_TRAIN_MODE == 3 && resident_ok(a, true)) {
+      const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+      const bool hw = (a.scheme & SMC_MATH_HW) != 0;
+      const bool sa = a.store == SMC_STORE_ALL;
+#define SMC_RES(LE, HWM, SA) \
+  if (log_euler == LE && hw == HWM && sa == SA) return launch_resident_k<LE, HWM, SA>(a, stream);
+      SMC_RES(true, true, true)
+      SMC_RES(true, true, false)
+      SMC_RES(true, false, true)
+      SMC_RES(true, false, false)
+      SMC_RES(false, true, true)
+      SMC_RES(false, true, false)
+      SMC_RES(false, false, true)
+      SMC_RES(false, false, false)
+#undef SMC_RES
+    }
+    if (SMC_TRAIN_MODE >= 2 && split_ok(a, true)) {
       const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
       const bool hw = (a.scheme & SMC_MATH_HW) != 0;
       const bool straight = a.T == kRowBlock && a.P % kChunk == 0;
@@ -1074,22 +1109,6 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
       SMC_SPLIT(false, false, false, true)
 #undef SMC_SPLIT
     }
-  }
-  if (SMC_TRAIN_MODE == 1 && overlap_ok(a, sizeof(Real) == 4)) {
-    const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
-    const bool hw = (a.scheme & SMC_MATH_HW) != 0;
-    const bool sa = a.store == SMC_STORE_ALL;
-#define SMC_OVERLAP(LE, HWM, SA) \
-  if (log_euler == LE && hw == HWM && sa == SA) return launch_overlap_k<LE, HWM, SA>(a, stream);
-    SMC_OVERLAP(true, true, true)
-    SMC_OVERLAP(true, true, false)
-    SMC_OVERLAP(true, false, true)
-    SMC_OVERLAP(true, false, false)
-    SMC_OVERLAP(false, true, true)
-    SMC_OVERLAP(false, true, false)
-    SMC_OVERLAP(false, false, true)
-    SMC_OVERLAP(false, false, false)
-#undef SMC_OVERLAP
   }
   if (a.slices < 1 || !a.simulate) a.slices = 1;
   if (a.slices > 1 && (!a.partials || !a.arrivals || !a.queues))
@@ -1248,8 +1267,8 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.pitch = path_pitch;
   a.slices = slices_for(n_paths, sliced != 0);
   a.store = SMC_STORE_ALL;
-  if (SMC_TRAIN_MODE == 2 && split_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "paths_kernel+cf_kernel";
-  if (SMC_TRAIN_MODE == 1 && overlap_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "overlap_kernel";
+  if (SMC_TRAIN_MODE == 3 && resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "resident_kernel";
+  if (SMC_TRAIN_MODE >= 2 && split_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "paths_kernel+cf_kernel";
   return a.slices > 1 ? "queue_kernel" : "contract_kernel";
 }
 

@@ -146,12 +146,15 @@ def test_path_pitch_is_an_odd_multiple_of_4k() -> None:
 
 
 def test_train_targets_kernel_choice() -> None:
-    """Which path/CF kernels smc_train_targets runs: the sliced queue kernel with a workspace; the
-    split pair paths_kernel + cf_kernel for f32 training (terminal-row sum parked in the scratch
+    """Which path/CF kernels smc_train_targets runs: the sliced queue kernel with a workspace;
+    resident_kernel for the f32 training shapes it covers (T = 16, 4096 | P <= 65,536, N | 4096,
+    N <= 1024); else the split pair paths_kernel + cf_kernel (terminal-row sum parked in the scratch
     row's padding, so it needs a padded pitch such as smc_path_pitch); contract_kernel otherwise."""
     L = _lib.lib()
     split = b"paths_kernel+cf_kernel"
-    assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 0) == split                 # C2
+    assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 0) == b"resident_kernel"    # C2
+    assert L.smc_train_targets_kernel(16, 256, 65536, 0, 0, 0) == b"resident_kernel"        # no pad needed
+    assert L.smc_train_targets_kernel(16, 2048, 65536, 0, 66560, 0) == split                 # N > 1024
     assert L.smc_train_targets_kernel(16, 1024, 262144, 0, L.smc_path_pitch(262144, 0), 0) == split  # C3
     assert L.smc_train_targets_kernel(16, 1024, 262144, 0, 0, 0) == b"contract_kernel"      # no padding
     assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 1) == b"queue_kernel"
@@ -159,6 +162,7 @@ def test_train_targets_kernel_choice() -> None:
     assert L.smc_train_targets_kernel(17, 256, 65536, 0, 66560, 0) == split                 # generic block
     assert L.smc_train_targets_kernel(16, 256, 65536, 1, 66560, 0) == b"contract_kernel"    # f64
     assert L.smc_train_targets_kernel(16, 6, 6144, 0, 6144, 0) == b"contract_kernel"        # pitch == P
+    assert L.smc_train_targets_kernel(16, 6, 6144, 0, 7168, 0) == split                     # N not | 4096
 
 
 def test_basket_entry_points_validate_before_any_device_work() -> None:

@@ -247,7 +247,8 @@ MANY_CONTRACT_CASES = [
 def test_multi_round_launches_match_oracle(oracle, golden, B, T, N, M, scheme, normalize, store) -> None:
     c = _contracts(oracle, golden, B, seed=7, skip=3)
     got, _, _ = _run_targets(c, T, N, M, scheme, normalize, "float32", store, ordinal0=9, with_rowsum=False)
-    kt, _ = oracle.kernel_targets(c, T, N, M, seed=7, ordinal0=9, scheme=scheme, normalize=bool(normalize))
+    kt, _ = oracle.kernel_targets(c, T, N, M, seed=7, ordinal0=9, scheme=scheme, normalize=bool(normalize),
+                                  wg=oracle.engine_wg(T, N, N * M))
     np.testing.assert_array_equal(got, kt)
     # padded pitch and chunked launches: same bits
     pitch = int(_L().smc_path_pitch(N * M, 0))
@@ -335,3 +336,35 @@ def test_hw_math_mode_within_fp32_tolerance(oracle, golden, scheme) -> None:
     _lib.check(_L().smc_normals(7, 3, 16, 4096, _lib.DTYPE_F32 | _lib.MATH_HW, _lib.ptr(z), None))
     torch.cuda.synchronize()
     np.testing.assert_allclose(z.cpu().numpy(), oracle.normals(7, 3, 16, 4096), rtol=0, atol=2e-5)
+
+
+RESIDENT_CASES = [
+    # (B, N, M, store): resident_kernel shapes (T = 16, 4096 | P <= 65,536, N | 4096, N <= 1024)
+    (300, 256, 256, _lib.STORE_ALL),      # C2 per-contract shape, > 1 contract on some workgroups
+    (40, 64, 64, _lib.STORE_ALL),         # one chunk (all terminal values in LDS), B < #CUs
+    (33, 1024, 16, _lib.STORE_TERMINAL),  # 4 chunks, G = 4, terminal-only scratch
+    (17, 4, 2048, _lib.STORE_ALL),        # N = 4: one column quad, G = 1024
+    (9, 512, 96, _lib.STORE_ALL),         # 12 chunks: 8 in LDS + 4 in registers
+]
+
+
+@pytest.mark.parametrize("B,N,M,store", RESIDENT_CASES)
+def test_resident_kernel_bit_exact(oracle, golden, B, N, M, store) -> None:
+    """resident_kernel (terminal rows kept on chip, no re-read): portable math bit-exact with the
+    kernel-mode oracle in 1024-lane order, hw math within 1e-5 of the reference-mode targets."""
+    P = N * M
+    pitch = int(_L().smc_path_pitch(P, 0))
+    assert _L().smc_train_targets_kernel(16, N, P, 0, pitch, 0) == b"resident_kernel"
+    assert oracle.engine_wg(16, N, P) == 1024
+    c = _contracts(oracle, golden, B, seed=42, skip=11)
+    got, _, _ = _run_targets(c, 16, N, M, 0, 1, "float32", store, ordinal0=21, with_rowsum=False, pitch=pitch)
+    kt, _ = oracle.kernel_targets(c, 16, N, M, seed=7, ordinal0=21, wg=1024)
+    np.testing.assert_array_equal(got, kt)
+    hw, _, _ = _run_targets(c, 16, N, M, 0, 1, "float32", store, ordinal0=21, with_rowsum=False, pitch=pitch,
+                            flags=_lib.MATH_HW)
+    want = oracle.training_targets(c, 16, N, M, seed=7, ordinal0=21)
+    assert _norm_rel(hw, want) < 1e-5
+    # contiguous rows (pitch = P) and launches of a few contracts: same bits
+    again, _, _ = _run_targets(c, 16, N, M, 0, 1, "float32", store, ordinal0=21, with_rowsum=False,
+                               chunk=max(1, B // 3))
+    np.testing.assert_array_equal(again, kt)

@@ -71,7 +71,8 @@ def test_portable_math_targets_bit_exact_and_match_reference(oracle, gbm_golden,
     got = train_targets(contracts, m, hw=False, padded=name != "c1")
     if m["dtype"] == "float32":
         kt, _ = oracle.kernel_targets(contracts, m["T"], m["N"], m["M"], seed=m["seed"], ordinal0=m["ordinal0"],
-                                      scheme=m["scheme"], normalize=m["normalize"])
+                                      scheme=m["scheme"], normalize=m["normalize"],
+                                      wg=oracle.engine_wg(m["T"], m["N"], m["N"] * m["M"]))
         np.testing.assert_array_equal(got, kt)
         assert per_contract_rel(got, want).max() < 5e-6
     else:
@@ -89,7 +90,7 @@ def test_c2_bench_instantiation_whole_rounds(oracle, gbm_golden) -> None:
     _, _, m = unpack(gbm_golden, "c2shape")
     assert (m["T"], m["N"], m["M"]) == (16, 256, 256) and m["ordinal0"] == 0
     kernel = _lib.lib().smc_train_targets_kernel(16, 256, 65536, _lib.DTYPE_F32, _lib.lib().smc_path_pitch(65536, 0), 0)
-    assert kernel in (b"overlap_kernel", b"contract_kernel")
+    assert kernel in (b"resident_kernel", b"paths_kernel+cf_kernel", b"contract_kernel")
     lo, hi = make_domain_bounds().arrays()
     contracts = oracle.sobol_contracts(7, 0, B, lo, hi)
     np.testing.assert_array_equal(contracts[:2], gbm_golden["c2shape_contracts"])
@@ -100,7 +101,7 @@ def test_c2_bench_instantiation_whole_rounds(oracle, gbm_golden) -> None:
     # portable math at the same instantiation: bit-exact with the kernel-mode restatement
     sub = contracts[:64]
     port = train_targets(sub, m, hw=False)
-    kt, _ = oracle.kernel_targets(sub, 16, 256, 256, seed=7, ordinal0=0)
+    kt, _ = oracle.kernel_targets(sub, 16, 256, 256, seed=7, ordinal0=0, wg=oracle.engine_wg(16, 256, 65536))
     np.testing.assert_array_equal(port, kt)
 
 
