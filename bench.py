@@ -35,16 +35,23 @@ CONFIGS = {
     "c1": (64, 16, 256, 4, [32], "C1: 64 contracts x 1024 paths (N=256 x M=4), T=16, 2-layer CVNN 6->32->256 fp32"),
     "c2": (4096, 16, 256, 256, [32, 32],
            "C2: 4096 contracts x 65536 paths (N=256 x M=256), T=16, 3-layer CVNN 6->32->32->256 fp32"),
-    # BASELINE configs[2] shapes; the CVNN stays fp32 (the reference accepts full precision only,
-    # gbm_trainer.py:679-682); 275 GB of paths per step run as equal launches through the scratch
+    # SURVEY 8(d) C2 "H=256 variant for MFMA": the same step with 256-wide hidden layers (267,264 params)
+    "c2h256": (4096, 16, 256, 256, [256, 256],
+               "C2/H=256: 4096 contracts x 65536 paths (N=256 x M=256), T=16, 3-layer CVNN 6->256->256->256 fp32"),
+    # BASELINE configs[2]: bf16 CVNN (bf16 MFMA operands, f32 master weights / Adam: an extension, the
+    # reference accepts full precision only, gbm_trainer.py:679-686); 275 GB of paths per step run as
+    # equal launches through the scratch
     "c3": (16384, 16, 1024, 256, [32, 32],
-           "C3: 16384 contracts x 262144 paths (N=1024 x M=256), T=16, 3-layer CVNN 6->32->32->1024 fp32"),
+           "C3: 16384 contracts x 262144 paths (N=1024 x M=256), T=16, 3-layer CVNN 6->32->32->1024 bf16 "
+           "(f32 master weights)"),
     # BASELINE configs[4] (per GPU): 4 correlated assets (Cholesky in LDS), equal-weight basket put
     "c5": (8192, 16, 256, 512, [32, 32],
            "C5: 8192 contracts x 131072 paths (N=256 x M=512), 4 correlated assets, T=16, basket put, "
            "3-layer CVNN 16->32->32->256 fp32"),
 }
 BASKET_ASSETS = {"c5": 4}
+NETWORK_COMPUTE = {"c3": "bf16"}  # default "auto": f32 on the f32 MFMA kernels
+MFMA_PEAK_TFLOPS = {"mfma_bf16": 2516.6, "mfma_f32": 157.3, "valu": 157.3}  # MI355X_MICROARCH.md, dense
 
 
 def parse() -> argparse.Namespace:
@@ -55,6 +62,10 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
     ap.add_argument("--math", default="hw", choices=["portable", "hw"])
+    ap.add_argument("--network", default=None, choices=["auto", "valu", "mfma", "bf16"],
+                    help="network kernels (default: bf16 for c3, auto otherwise)")
+    ap.add_argument("--overlap", default="on", choices=["on", "off"],
+                    help="MC part of step s+1 on its own stream beside step s's network part (pricer.overlap_mc)")
     ap.add_argument("--kernel-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU-baseline sample")
@@ -118,7 +129,7 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
         path = ("torch-cpu paths (f64 recursion, numpy default_rng normals per contract) + numpy.fft "
                 "(oracle/torch_cpu.py)")
     model = make_test_cvnn(n_inputs=contracts.shape[1], n_outputs=N, seed=123, dtype=torch.float32, device="cpu",
-                           hidden_layers=len(widths))
+                           hidden_layers=len(widths), hidden_width=widths[0])
     adam = torch.optim.Adam(model.parameters(), lr=1e-2)
     x = torch.tensor(contracts, dtype=torch.float32)
     tgt = torch.from_numpy(np.concatenate(tg))
@@ -205,13 +216,15 @@ def main() -> None:
     n_assets = BASKET_ASSETS.get(args.config, 0)
     n_inputs = 3 * n_assets + 4 if n_assets else 6
     model = make_test_cvnn(n_inputs=n_inputs, n_outputs=N, seed=123, dtype=torch.float32, device=dev,
-                           hidden_layers=len(widths))
+                           hidden_layers=len(widths), hidden_width=widths[0])
     cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
                                domain_bounds=make_domain_bounds())
     pricer = expect_success(GbmCVNNPricer.create(cfg))
     pricer.store_paths = args.store == "all"
     pricer.math_mode = args.math
     pricer.warmup_steps = max(1, min(2, args.warmup))
+    pricer.network_compute = args.network or NETWORK_COMPUTE.get(args.config, "auto")
+    pricer.overlap_mc = args.overlap == "on"
     if n_assets:
         from spectralmc_amd.basket import BasketConfig, use_basket_engine
 
@@ -292,11 +305,20 @@ def main() -> None:
             n1.record(stream)
         n1.synchronize()
         net_ms = n0.elapsed_time(n1) / args.kernel_iters
-        network = {"kernels": "forward_backward + reduce/Adam + finalize (csrc/cvnn.hip), VALU f32",
-                   "flops_per_step": flops, "ms": net_ms, "achieved": flops / (net_ms * 1e-3) / 1e12,
-                   "peak": 157.3, "unit": "TFLOP/s", "frac": flops / (net_ms * 1e-3) / 1e12 / 157.3,
-                   "note": "latency-bound small complex GEMMs; runs on its own stream beside the next "
-                           "step's contract kernel, so it adds ~0 to ms_per_step"}
+        kern = fused.kernels
+        peak = MFMA_PEAK_TFLOPS[kern]
+        desc_k = {"mfma_bf16": "pack + fb + wgrad (csrc/cvnn_mfma.hip, v_mfma_f32_16x16x32_bf16, bf16 operands, "
+                               "f32 accumulate / master weights) + reduce/Adam + finalize",
+                  "mfma_f32": "pack + fb + wgrad (csrc/cvnn_mfma.hip, v_mfma_f32_16x16x4_f32) + reduce/Adam + "
+                              "finalize",
+                  "valu": "forward_backward + reduce/Adam + finalize (csrc/cvnn.hip), VALU f32"}[kern]
+        network = {"kernels": desc_k, "compute": kern, "flops_per_step": flops, "ms": net_ms,
+                   "achieved": flops / (net_ms * 1e-3) / 1e12, "peak": peak, "unit": "TFLOP/s",
+                   "frac": flops / (net_ms * 1e-3) / 1e12 / peak,
+                   "peak_note": "dense MFMA peak of the operand type (bf16 2.52 PF; f32 MFMA = f32 VALU "
+                                "157.3 TF), MI355X_MICROARCH.md",
+                   "note": "small complex GEMMs (K = 12..512) plus the targets read; runs on its own stream "
+                           "beside the next step's path kernel"}
 
     # ---- measured HBM ceilings on this device (STREAM-style, 8 GiB buffers) --------------
     stream_gbs = {}
@@ -346,6 +368,8 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
+        "network_dtype": ({"mfma_bf16": "bf16 operands, f32 accumulate / master weights"}.get(network["compute"], "f32")
+                          if network else "f32 (torch-ROCm modules)"),
         "data": ("synthetic: Sobol basket contracts (seed 7, basket.default_basket_bounds), random-init CVNN (seed 123)"
                  if n_assets else
                  "synthetic: Sobol contracts (seed 7, make_domain_bounds defaults), random-init CVNN (seed 123)"),

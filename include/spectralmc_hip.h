@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 5
+#define SMC_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -215,6 +215,26 @@ int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t parti
 int32_t smc_adam_step(int32_t dtype, int64_t n_params, const void* grads, const smc_adam_args* adam,
                       void* stream);
 int64_t smc_adam_norm_partials(int64_t n_params);
+
+/* ---- the same network step on the matrix cores (csrc/cvnn_mfma.hip) ---------
+ * Each complex layer runs as real GEMMs of the interleaved (re, im) vectors on MFMA:
+ *   SMC_CVNN_MFMA_F32   f32 operands (v_mfma_f32_16x16x4_f32), the network's own precision;
+ *   SMC_CVNN_MFMA_BF16  bf16 operands rounded to nearest even, f32 accumulation, f32 master
+ *                       parameters / activations / loss / Adam (BASELINE configs[2] "bf16 CVNN";
+ *                       an extension: the reference asserts full precision, gbm_trainer.py:679-686).
+ * Parameters, inputs and targets are f32 / complex64.  The call writes per-segment partials
+ * [partial_blocks][n_params + 1] (gradients, loss last) that smc_cvnn_reduce_grads(SMC_DTYPE_F32,
+ * ...) sums in order, exactly as after smc_cvnn_forward_backward.  Shapes whose widths exceed the
+ * kernels' LDS plan return SMC_ERR_INVALID_SHAPE from the plan (callers keep the VALU kernels). */
+#define SMC_CVNN_MFMA_F32   1
+#define SMC_CVNN_MFMA_BF16  2
+int32_t smc_cvnn_mfma_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, int64_t batch,
+                           int64_t* partial_blocks, int64_t* workspace_bytes);
+int32_t smc_cvnn_mfma_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode,
+                                       const float* params, int64_t n_params, const float* input_re,
+                                       const float* input_im, const void* targets, int64_t batch,
+                                       float* partials, int64_t partial_blocks, void* workspace,
+                                       int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -34,7 +34,7 @@ STORE_TERMINAL = 1
 MATH_HW = 0x100
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 
@@ -67,6 +67,9 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_cvnn_reduce_grads": (_c_i32, [_c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
     "smc_adam_step": (_c_i32, [_c_i32, _c_i64, _c_vp, _c_vp, _c_vp]),
     "smc_adam_norm_partials": (_c_i64, [_c_i64]),
+    "smc_cvnn_mfma_plan": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
+    "smc_cvnn_mfma_forward_backward": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64,
+                                                _c_vp, _c_i64, _c_vp, _c_i64, _c_vp]),
     "smc_basket_train_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_i32, _c_u64, _c_vp, _c_i64,
                                           _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
     "smc_basket_resident_slots": (_c_i64, [_c_i32, _c_i32, _c_i32]),
@@ -74,6 +77,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
 
 CVNN_MAX_LAYERS = 8
 ACT_NONE, ACT_MODRELU, ACT_ZRELU = 0, 1, 2
+CVNN_MFMA_F32, CVNN_MFMA_BF16 = 1, 2
 
 
 class CvnnLayer(ctypes.Structure):

@@ -198,19 +198,26 @@ class BasketEngine:
     def set_position(self, sobol_index: int, ordinal: int) -> None:
         self.cursor.copy_(torch.tensor([sobol_index, ordinal], dtype=torch.int64), non_blocking=False)
 
-    def enqueue_step(self) -> StepBuffers:
+    def make_slot(self) -> StepBuffers:
+        """Another set of step outputs (see TrainingEngine.make_slot)."""
         b = self.buffers
+        return StepBuffers(contracts=torch.empty_like(b.contracts), real_in=torch.empty_like(b.real_in),
+                           imag_in=b.imag_in, targets=torch.empty_like(b.targets))
+
+    def enqueue_step(self, out: StepBuffers | None = None) -> StepBuffers:
+        b = out if out is not None else self.buffers
         offset = self.rank * self.B
         draw_device(self.tables, self.dim, self.cursor[0:1], offset, self.B, self.lower, self.upper, b.contracts,
                     b.real_in if self._f32_in else None)
         if not self._f32_in:
             b.real_in.copy_(b.contracts)
-        self.launch_targets(_lib.stream_handle(), _lib.ptr(self.cursor[1:2]), offset)
+        self.launch_targets(_lib.stream_handle(), _lib.ptr(self.cursor[1:2]), offset, b)
         self.cursor.add_(self.global_batch)
         return b
 
-    def launch_targets(self, stream: int | None, ordinal_ptr: int | None, ordinal0: int) -> None:
-        b = self.buffers
+    def launch_targets(self, stream: int | None, ordinal_ptr: int | None, ordinal0: int,
+                       b: StepBuffers | None = None) -> None:
+        b = b if b is not None else self.buffers
         _lib.check(_lib.lib().smc_basket_train_targets(
             _lib.ptr(b.contracts), self.B, self.A, self.T, self.N, self.M, self.cfg.mc_seed, ordinal_ptr, ordinal0,
             self._math, 1 if self.cfg.normalize else 0, self.store_mode, _lib.ptr(self._paths_buf), self.pitch,

@@ -1,0 +1,795 @@
+// Complex-valued MLP training step on the matrix cores (gfx950 MFMA).
+//
+// The same step as cvnn.hip (reference cvnn.py:65-210 ComplexLinear / modReLU / zReLU,
+// gbm_trainer.py:819-835 spectral MSE + backward), with every product a real GEMM on MFMA:
+//
+//   * a complex layer y = W z + b (W = A + iB, z = x + iy) is the real map of the interleaved
+//     vectors Z = (x0, y0, x1, y1, ...):  Wc[2j + a][2k + b] = [[A, -B], [B, A]]_{jk}[a][b],
+//     so U = Z Wc^T (features (u_j, v_j) interleaved, the complex64 layout of the targets),
+//     dZ = dU Wc, dWc = dU^T Z; dA = dWc[2j][2k] + dWc[2j+1][2k+1], dB = dWc[2j+1][2k] - dWc[2j][2k+1];
+//     the bias gradients are the extra "ones" column 2 ni of Z in the weight-gradient GEMM.
+//   * operand types (SMC_CVNN_MFMA_F32 / SMC_CVNN_MFMA_BF16):
+//       f32:  v_mfma_f32_16x16x4_f32   (exact f32 fma chains, the network's own dtype)
+//       bf16: v_mfma_f32_16x16x32_bf16 (bf16 operands rounded to nearest even, f32 accumulate;
+//             master parameters, activations, loss, Adam stay f32 — BASELINE configs[2] extension;
+//             the reference itself asserts full precision, gbm_trainer.py:679-686)
+//
+// Launches per step (all stream-ordered, no atomics, fixed reduction orders: bit-reproducible):
+//   pack_kernel       Wc [W_out][W_in] and Wc^T [W_in][W_out] of every layer from the f32 params
+//   fb_kernel         16 * RT batch rows per workgroup: forward through every layer (GEMM + bias +
+//                     activation epilogue, activations in LDS), loss and output gradient, then the
+//                     input-gradient GEMMs down the layers with the activation backward fused in
+//                     their epilogue.  Writes Z_l^T and dU_l^T ([feature][batch]) for the weight
+//                     gradients, modReLU-bias and loss partials per workgroup.
+//   wgrad_kernel      dWc_l = dU_l^T Z_l per (feature tile, column-tile group, batch segment), one wave
+//                     per item, K = the segment's batch rows; writes partials[segment][n_params + 1]
+//                     (weights, biases, modReLU biases, loss), which smc_cvnn_reduce_grads sums in order.
+//
+// MFMA fragments (MI355X / CDNA4): lane l = 16 g + c supplies 16 bytes of A row c and of B column c
+// at K offset g * KB / 4 of the K block; C/D: lane l holds rows 4 g .. 4 g + 3 of column c.  In the
+// f32 form the four instructions of a K block take element i of each lane's 4-vector, so a block
+// covers k = kb + 4 g + i for g, i in 0..3 on A and B alike.
+#include <cmath>
+
+#include "smc_internal.h"
+
+namespace smc {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kMaxL = SMC_CVNN_MAX_LAYERS;
+constexpr int kWgradTiles = 4;       // column tiles (16 wide) per weight-gradient item: 16 accumulators
+constexpr int kMaxSegments = 64;     // batch segments of the weight-gradient GEMMs
+constexpr int kSegmentRows = 64;     // minimum rows per segment
+constexpr int64_t kWgradItems = 4096;  // segments are added until the items reach this
+constexpr size_t kLdsCap = 156 * 1024;   // dynamic LDS of fb_kernel (160 KiB per CU, less its static LDS)
+constexpr size_t kLdsPair = 80 * 1024;   // two row tiles per workgroup only within this
+
+__host__ __device__ inline float bf16_round(float x) {
+  uint32_t u;
+  __builtin_memcpy(&u, &x, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) {
+    u |= 0x00400000u;  // quiet NaN
+  } else {
+    u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (torch's float -> bfloat16)
+  }
+  u &= 0xffff0000u;
+  float y;
+  __builtin_memcpy(&y, &u, 4);
+  return y;
+}
+
+__device__ __forceinline__ uint16_t bf16_bits(float x) { return static_cast<uint16_t>(__float_as_uint(bf16_round(x)) >> 16); }
+
+struct OpBf16 {
+  using T = uint16_t;
+  using V = bf16x8;
+  static constexpr int KB = 32;  // one v_mfma_f32_16x16x32_bf16 per K block
+  static __device__ __forceinline__ T cvt(float x) { return bf16_bits(x); }
+  static __device__ __forceinline__ V ld(const T* p) { return *reinterpret_cast<const V*>(p); }
+  static __device__ __forceinline__ f32x4 mmav(f32x4 acc, V a, V b) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x4 mma(f32x4 acc, const T* a, const T* b) {
+    const bf16x8 av = *reinterpret_cast<const bf16x8*>(a);
+    const bf16x8 bv = *reinterpret_cast<const bf16x8*>(b);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+  }
+  static __device__ __forceinline__ void store4(T* p, float a, float b, float c, float d) {
+    *reinterpret_cast<u16x4*>(p) = u16x4{cvt(a), cvt(b), cvt(c), cvt(d)};
+  }
+};
+
+struct OpF32 {
+  using T = float;
+  using V = f32x4;
+  static constexpr int KB = 16;  // four v_mfma_f32_16x16x4_f32 per K block
+  static __device__ __forceinline__ T cvt(float x) { return x; }
+  static __device__ __forceinline__ V ld(const T* p) { return *reinterpret_cast<const V*>(p); }
+  static __device__ __forceinline__ f32x4 mmav(f32x4 acc, V a, V b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], acc, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x4 mma(f32x4 acc, const T* a, const T* b) {
+    const f32x4 av = *reinterpret_cast<const f32x4*>(a);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(b);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bv[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bv[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bv[2], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bv[3], acc, 0, 0, 0);
+  }
+  static __device__ __forceinline__ void store4(T* p, float a, float b, float c, float d) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{a, b, c, d};
+  }
+};
+
+// Per-layer plan (host-computed).  W_in = roundup(2 ni, KB), W_out = roundup(2 no, KB).
+struct MLayer {
+  int32_t ni, no, act, win, wout, kx;  // kx = roundup(2 ni + 1, 16): rows of Z^T (ones row at 2 ni)
+  int64_t w_re, w_im, b_re, b_im, act_bias;
+  int64_t wc, wct;   // Op offsets: Wc [wout][win], Wc^T [win][wout]
+  int64_t zt, gt;    // Op offsets: Z^T [kx][bp], dU^T [wout][bp]
+  int64_t pre;       // f32 offset of the pre-activation [bp][2 no] (hidden layers with an activation), or -1
+  int64_t cpart;     // f32 offset of the modReLU-bias partials [nwg][no], or -1
+  int64_t items;     // weight-gradient items (waves) of this layer, all segments
+};
+
+struct MArgs {
+  int32_t n_layers;
+  MLayer layer[kMaxL];
+  int64_t batch, bp;
+  int32_t rows;      // batch rows per fb workgroup (16 RT)
+  int32_t nwg;       // fb workgroups = bp / rows
+  int32_t segs;      // batch segments of the weight gradients
+  int32_t zs, gs;    // LDS row strides (Op elements) of the activation and output-gradient buffers
+  int64_t n_params;
+  int64_t pack_elems;
+  const float* params;
+  const float* in_re;
+  const float* in_im;
+  const float* targets;   // [batch][N] complex64
+  void* opws;
+  float* fws;
+  double* lossp;          // [nwg]
+  float* partials;        // [segs][n_params + 1]
+};
+
+// ---- pack ------------------------------------------------------------------------------------
+template <class Op>
+__global__ __launch_bounds__(kThreads) void pack_kernel(MArgs a) {
+  using T = typename Op::T;
+  T* ws = static_cast<T*>(a.opws);
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < a.pack_elems;
+       e += static_cast<int64_t>(gridDim.x) * kThreads) {
+    int64_t r = e;
+    int l = 0;
+    while (r >= 2LL * a.layer[l].wout * a.layer[l].win) {
+      r -= 2LL * a.layer[l].wout * a.layer[l].win;
+      ++l;
+    }
+    const MLayer& ly = a.layer[l];
+    const int64_t n = static_cast<int64_t>(ly.wout) * ly.win;
+    const bool transposed = r >= n;
+    if (transposed) r -= n;
+    const int f = transposed ? static_cast<int>(r % ly.wout) : static_cast<int>(r / ly.win);
+    const int k = transposed ? static_cast<int>(r / ly.wout) : static_cast<int>(r % ly.win);
+    const int j = f >> 1, kk = k >> 1, ra = f & 1, rb = k & 1;
+    float v = 0.0f;
+    if (j < ly.no && kk < ly.ni) {
+      const float wa = a.params[ly.w_re + static_cast<int64_t>(j) * ly.ni + kk];
+      const float wb = a.params[ly.w_im + static_cast<int64_t>(j) * ly.ni + kk];
+      v = ra == rb ? wa : (ra == 0 ? -wb : wb);
+    }
+    ws[(transposed ? ly.wct : ly.wc) + (transposed ? k * static_cast<int64_t>(ly.wout) + f : f * static_cast<int64_t>(ly.win) + k)] = Op::cvt(v);
+  }
+}
+
+// ---- activations (f32; cvnn.hip / cvnn.py:149-210) --------------------------------------------
+struct Act {
+  // forward: (u, v) -> (ou, ov)
+  static __device__ __forceinline__ void fwd(int act, float c, float u, float v, float& ou, float& ov) {
+    if (act == SMC_ACT_MODRELU) {
+      const float m = sqrtf(u * u + v * v + 1e-9f);
+      const float t = m + c;
+      const float g = (t > 0.0f ? t : 0.0f) / m;
+      ou = g * u;
+      ov = g * v;
+    } else if (act == SMC_ACT_ZRELU) {
+      const bool keep = u >= 0.0f && v >= 0.0f;
+      ou = keep ? u : 0.0f;
+      ov = keep ? v : 0.0f;
+    } else {
+      ou = u;
+      ov = v;
+    }
+  }
+  // backward: output gradient (gr, gi) at pre-activation (u, v) -> (gu, gv); dc = d loss / d c share
+  static __device__ __forceinline__ void bwd(int act, float c, float u, float v, float gr, float gi, float& gu,
+                                             float& gv, float& dc) {
+    dc = 0.0f;
+    if (act == SMC_ACT_MODRELU) {
+      const float m = sqrtf(u * u + v * v + 1e-9f);
+      if (m + c > 0.0f) {
+        dc = (gr * u + gi * v) / m;
+        const float g = (m + c) / m;
+        const float k = -(gr * u + gi * v) * c / (m * m * m);
+        gu = gr * g + k * u;
+        gv = gi * g + k * v;
+      } else {
+        gu = gv = 0.0f;
+      }
+    } else if (act == SMC_ACT_ZRELU) {
+      const bool keep = u >= 0.0f && v >= 0.0f;
+      gu = keep ? gr : 0.0f;
+      gv = keep ? gi : 0.0f;
+    } else {
+      gu = gr;
+      gv = gi;
+    }
+  }
+};
+
+// Sum over the 16 batch columns of a C tile (lanes c = 0..15 of one row group g), fixed order.
+__device__ __forceinline__ float col_sum16(float x) {
+  x += __shfl_xor(x, 8, 64);
+  x += __shfl_xor(x, 4, 64);
+  x += __shfl_xor(x, 2, 64);
+  x += __shfl_xor(x, 1, 64);
+  return x;
+}
+
+// ---- tile GEMM: acc[rt] += A[16 rows at ap][k0, k1) . B[k0, k1)[16 columns of row tile rt at bp] ----
+// ap: this lane's A row (+ g KQ), from global memory (L2); bp: this lane's B row (+ g KQ) of row
+// tile 0 in LDS, row tiles ldb * 16 elements apart.  The A fragments of up to 8 K blocks are loaded
+// before their MFMAs, so their L2 latencies overlap.
+template <class Op, int RT>
+__device__ __forceinline__ void tile_gemm(f32x4* acc, const typename Op::T* ap, const typename Op::T* bp, int ldb,
+                                          int k0, int k1) {
+  using V = typename Op::V;
+  constexpr int KB = Op::KB;
+  for (int kb0 = k0; kb0 < k1; kb0 += 8 * KB) {
+    V av[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (kb0 + i * KB < k1) av[i] = Op::ld(ap + kb0 + i * KB);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (kb0 + i * KB < k1) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt] = Op::mmav(acc[rt], av[i], Op::ld(bp + rt * 16 * ldb + kb0 + i * KB));
+      }
+    }
+  }
+}
+
+constexpr int kFbThreads = 1024;
+constexpr int kFbWaves = kFbThreads / 64;
+
+// K split of a layer GEMM with `ntile` output tiles: waves take (tile, K part) items when the
+// tiles alone would leave waves idle; parts are added in order 0, 1, ... (bit-reproducible).
+__host__ __device__ inline int k_split(int ntile, int kdim, int kb) {
+  int ks = 1;
+  while (ntile * ks * 2 <= kFbWaves && kdim % (2 * ks * kb) == 0) ks *= 2;
+  return ks;
+}
+
+// All output tiles of one layer GEMM, then epi(tile, acc) for each; called by every wave.
+template <class Op, int RT, class Epi>
+__device__ __forceinline__ void layer_gemm(int ntile, int kdim, const typename Op::T* a0, int lda,
+                                           const typename Op::T* b0, int ldb, f32x4* scratch, Epi&& epi) {
+  constexpr int KQ = Op::KB / 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int ks = k_split(ntile, kdim, Op::KB);
+  if (ks == 1) {
+    for (int t = wave; t < ntile; t += kFbWaves) {
+      f32x4 acc[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      tile_gemm<Op, RT>(acc, a0 + static_cast<int64_t>(t * 16 + c) * lda + g * KQ, b0 + c * ldb + g * KQ, ldb, 0,
+                        kdim);
+      epi(t, acc);
+    }
+    return;
+  }
+  const int kc = kdim / ks;
+  const int t = wave / ks, part = wave % ks;
+  f32x4 acc[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) acc[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  if (t < ntile) {
+    tile_gemm<Op, RT>(acc, a0 + static_cast<int64_t>(t * 16 + c) * lda + g * KQ, b0 + c * ldb + g * KQ, ldb,
+                      part * kc, part * kc + kc);
+    if (part > 0) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) scratch[(wave * RT + rt) * 64 + lane] = acc[rt];
+    }
+  }
+  __syncthreads();
+  if (t < ntile && part == 0) {
+    for (int p = 1; p < ks; ++p) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] += scratch[((wave + p) * RT + rt) * 64 + lane];
+    }
+    epi(t, acc);
+  }
+}
+
+// ---- forward + backward over 16 RT batch rows ------------------------------------------------
+template <class Op, int RT>
+__global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
+  using T = typename Op::T;
+  constexpr int R = 16 * RT;
+  extern __shared__ __attribute__((aligned(16))) char net_lds[];
+  __shared__ MLayer layer[kMaxL];
+  __shared__ double red[kFbWaves];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, c = lane & 15;
+  if (tid < kMaxL) {
+#pragma unroll
+    for (int i = 0; i < kMaxL; ++i)
+      if (i == tid) layer[i] = a.layer[i];
+  }
+  __syncthreads();
+  const int L = a.n_layers;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int64_t bp = a.bp;
+  T* ws = static_cast<T*>(a.opws);
+  f32x4* scratch = reinterpret_cast<f32x4*>(net_lds);  // [kFbWaves][RT][64] split-K partials
+  T* zbuf[2];
+  zbuf[0] = reinterpret_cast<T*>(net_lds + kFbWaves * RT * 64 * sizeof(f32x4));
+  zbuf[1] = zbuf[0] + R * a.zs;
+  T* gb = zbuf[1] + R * a.zs;
+  const float* P = a.params;
+
+  // ---- layer-0 input: Z_0 (interleaved re, im) into LDS and Z_0^T (+ ones row) into the workspace
+  {
+    const MLayer& l0 = layer[0];
+    const int n0 = l0.ni;
+    auto in = [&](int64_t row, int k) -> float {
+      if (row >= a.batch || k >= 2 * n0) return 0.0f;
+      const int64_t i = row * n0 + (k >> 1);
+      return (k & 1) ? (a.in_im ? a.in_im[i] : 0.0f) : a.in_re[i];
+    };
+    for (int i = tid; i < R * l0.win; i += kFbThreads) {
+      const int r = i / l0.win, k = i - r * l0.win;
+      zbuf[0][r * a.zs + k] = Op::cvt(in(r0 + r, k));
+    }
+    for (int i = tid; i < l0.kx * R; i += kFbThreads) {
+      const int k = i / R, r = i - k * R;
+      ws[l0.zt + k * bp + r0 + r] = Op::cvt(k == 2 * n0 ? 1.0f : in(r0 + r, k));
+    }
+  }
+  __syncthreads();
+
+  // ---- forward through the hidden layers
+  int cur = 0;
+  for (int l = 0; l + 1 < L; ++l) {
+    const MLayer& ly = layer[l];
+    const MLayer& nx = layer[l + 1];
+    T* zout = zbuf[cur ^ 1];
+    layer_gemm<Op, RT>(ly.wout / 16, ly.win, ws + ly.wc, ly.win, zbuf[cur], a.zs, scratch, [&](int ft, f32x4* acc) {
+      const int f0 = ft * 16 + 4 * g;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = rt * 16 + c;
+        float o[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = (f0 >> 1) + h;
+          o[2 * h] = o[2 * h + 1] = 0.0f;
+          if (j < ly.no) {
+            float u = acc[rt][2 * h], v = acc[rt][2 * h + 1];
+            if (ly.b_re >= 0) u += P[ly.b_re + j];
+            if (ly.b_im >= 0) v += P[ly.b_im + j];
+            if (ly.pre >= 0) {
+              float* pre = a.fws + ly.pre + (r0 + r) * (2LL * ly.no) + 2 * j;
+              pre[0] = u;
+              pre[1] = v;
+            }
+            Act::fwd(ly.act, ly.act == SMC_ACT_MODRELU ? P[ly.act_bias + j] : 0.0f, u, v, o[2 * h], o[2 * h + 1]);
+          }
+        }
+        Op::store4(zout + r * a.zs + f0, o[0], o[1], o[2], o[3]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (f0 + i < 2 * ly.no) ws[nx.zt + (f0 + i) * bp + r0 + r] = Op::cvt(o[i]);
+      }
+    });
+    // Z^T rows 2 no .. kx of the next layer: the ones row, then zeros
+    for (int i = tid; i < (nx.kx - 2 * ly.no) * R; i += kFbThreads) {
+      const int k = 2 * ly.no + i / R, r = i % R;
+      ws[nx.zt + k * bp + r0 + r] = Op::cvt(k == 2 * ly.no ? 1.0f : 0.0f);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- last layer: prediction, loss, output gradient (+ its activation backward) into gb / dU^T
+  const float scale = 2.0f / static_cast<float>(static_cast<double>(a.batch) * layer[L - 1].no);
+  double loss = 0.0;
+  {
+    const MLayer& ly = layer[L - 1];
+    const int N = ly.no;
+    layer_gemm<Op, RT>(ly.wout / 16, ly.win, ws + ly.wc, ly.win, zbuf[cur], a.zs, scratch, [&](int ft, f32x4* acc) {
+      const int f0 = ft * 16 + 4 * g;
+      float dcs[2] = {0.0f, 0.0f};
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = rt * 16 + c;
+        const int64_t row = r0 + r;
+        float o[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = (f0 >> 1) + h;
+          o[2 * h] = o[2 * h + 1] = 0.0f;
+          if (j < N && row < a.batch) {
+            float u = acc[rt][2 * h], v = acc[rt][2 * h + 1];
+            if (ly.b_re >= 0) u += P[ly.b_re + j];
+            if (ly.b_im >= 0) v += P[ly.b_im + j];
+            const float cb = ly.act == SMC_ACT_MODRELU ? P[ly.act_bias + j] : 0.0f;
+            float pr, pi;
+            Act::fwd(ly.act, cb, u, v, pr, pi);
+            const float* t = a.targets + (row * N + j) * 2;
+            const float dr = pr - t[0], di = pi - t[1];
+            loss += static_cast<double>(dr * dr) + static_cast<double>(di * di);
+            float dc;
+            Act::bwd(ly.act, cb, u, v, scale * dr, scale * di, o[2 * h], o[2 * h + 1], dc);
+            dcs[h] += dc;
+          }
+        }
+        Op::store4(gb + r * a.gs + f0, o[0], o[1], o[2], o[3]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ws[ly.gt + (f0 + i) * bp + r0 + r] = Op::cvt(o[i]);
+      }
+      if (ly.cpart >= 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float s = col_sum16(dcs[h]);
+          const int j = (f0 >> 1) + h;
+          if (c == 0 && j < N) a.fws[ly.cpart + static_cast<int64_t>(blockIdx.x) * N + j] = s;
+        }
+      }
+    });
+  }
+  // workgroup loss partial, fixed order: wave butterfly, then waves in order
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) loss += __shfl_xor(loss, off, 64);
+  if (lane == 0) red[wave] = loss;
+  __syncthreads();  // also: gb complete, split-K scratch free
+  if (tid == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kFbWaves; ++w) t += red[w];
+    a.lossp[blockIdx.x] = t;
+  }
+
+  // ---- input gradients down the layers: dZ_l = dU_l Wc_l, then layer l-1's activation backward
+  const T* gsrc = gb;
+  int gstride = a.gs;
+  int dst = 0;
+  for (int l = L - 1; l >= 1; --l) {
+    const MLayer& ly = layer[l];
+    const MLayer& lp = layer[l - 1];
+    T* gdst = zbuf[dst];
+    layer_gemm<Op, RT>(ly.win / 16, ly.wout, ws + ly.wct, ly.wout, gsrc, gstride, scratch, [&](int it, f32x4* acc) {
+      const int f0 = it * 16 + 4 * g;
+      float dcs[2] = {0.0f, 0.0f};
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = rt * 16 + c;
+        float o[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = (f0 >> 1) + h;
+          o[2 * h] = o[2 * h + 1] = 0.0f;
+          if (j < lp.no) {
+            float u = 0.0f, v = 0.0f;
+            if (lp.pre >= 0) {
+              const float* pre = a.fws + lp.pre + (r0 + r) * (2LL * lp.no) + 2 * j;
+              u = pre[0];
+              v = pre[1];
+            }
+            const float cb = lp.act == SMC_ACT_MODRELU ? P[lp.act_bias + j] : 0.0f;
+            float dc;
+            Act::bwd(lp.act, cb, u, v, acc[rt][2 * h], acc[rt][2 * h + 1], o[2 * h], o[2 * h + 1], dc);
+            dcs[h] += dc;
+          }
+        }
+        Op::store4(gdst + r * a.zs + f0, o[0], o[1], o[2], o[3]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ws[lp.gt + (f0 + i) * bp + r0 + r] = Op::cvt(o[i]);
+      }
+      if (lp.cpart >= 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float s = col_sum16(dcs[h]);
+          const int j = (f0 >> 1) + h;
+          if (c == 0 && j < lp.no) a.fws[lp.cpart + static_cast<int64_t>(blockIdx.x) * lp.no + j] = s;
+        }
+      }
+    });
+    __syncthreads();
+    gsrc = gdst;
+    gstride = a.zs;
+    dst ^= 1;
+  }
+}
+
+// ---- weight gradients: one wave per (layer, feature tile, column-tile group, segment) ----------
+template <class Op>
+__global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
+  using T = typename Op::T;
+  constexpr int KQ = Op::KB / 4;
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  int64_t item = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  const T* ws = static_cast<const T*>(a.opws);
+  const int64_t stride = a.n_params + 1;
+  const int64_t seg_rows = a.bp / a.segs;
+  int l = 0;
+  while (l < a.n_layers && item >= a.layer[l].items) item -= a.layer[l].items, ++l;
+  if (l == a.n_layers) {
+    // bookkeeping items, one per segment: loss and modReLU-bias gradients of the segment's rows
+    if (item >= a.segs) return;
+    const int s = static_cast<int>(item);
+    const int w0 = static_cast<int>(s * (seg_rows / a.rows)), w1 = static_cast<int>((s + 1) * (seg_rows / a.rows));
+    float* part = a.partials + s * stride;
+    if (lane == 0) {
+      double t = 0.0;
+      for (int w = w0; w < w1; ++w) t += a.lossp[w];
+      part[a.n_params] = static_cast<float>(t / (static_cast<double>(a.batch) * a.layer[a.n_layers - 1].no));
+    }
+    for (int ll = 0; ll < a.n_layers; ++ll) {
+      const MLayer& ly = a.layer[ll];
+      if (ly.cpart < 0) continue;
+      for (int j = lane; j < ly.no; j += 64) {
+        double t = 0.0;
+        for (int w = w0; w < w1; ++w) t += a.fws[ly.cpart + static_cast<int64_t>(w) * ly.no + j];
+        part[ly.act_bias + j] = static_cast<float>(t);
+      }
+    }
+    return;
+  }
+  const MLayer& ly = a.layer[l];
+  const int ntile = ly.kx / 16;
+  const int ngroup = (ntile + kWgradTiles - 1) / kWgradTiles;
+  const int s = static_cast<int>(item % a.segs);
+  const int64_t rest = item / a.segs;
+  const int kg = static_cast<int>(rest % ngroup);
+  const int ft = static_cast<int>(rest / ngroup);
+  const int t0 = kg * kWgradTiles;
+  const int nt = ntile - t0 < kWgradTiles ? ntile - t0 : kWgradTiles;
+  f32x4 acc[kWgradTiles];
+#pragma unroll
+  for (int t = 0; t < kWgradTiles; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int64_t b0 = s * seg_rows;
+  const T* ap = ws + ly.gt + (ft * 16 + c) * a.bp + b0 + g * KQ;
+  const T* bp0 = ws + ly.zt + (t0 * 16 + c) * a.bp + b0 + g * KQ;
+  using V = typename Op::V;
+  for (int64_t kb = 0; kb < seg_rows; kb += 2 * Op::KB) {  // two K blocks' fragments in flight
+    const V a0 = Op::ld(ap + kb), a1 = Op::ld(ap + kb + Op::KB);
+    V b0[kWgradTiles], b1[kWgradTiles];
+#pragma unroll
+    for (int t = 0; t < kWgradTiles; ++t) {
+      if (t < nt) {
+        b0[t] = Op::ld(bp0 + t * 16 * a.bp + kb);
+        b1[t] = Op::ld(bp0 + t * 16 * a.bp + kb + Op::KB);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < kWgradTiles; ++t)
+      if (t < nt) acc[t] = Op::mmav(acc[t], a0, b0[t]);
+#pragma unroll
+    for (int t = 0; t < kWgradTiles; ++t)
+      if (t < nt) acc[t] = Op::mmav(acc[t], a1, b1[t]);
+  }
+  float* part = a.partials + s * stride;
+  const int fbase = ft * 16 + 4 * g;
+#pragma unroll
+  for (int t = 0; t < kWgradTiles; ++t) {
+    if (t < nt) {  // wave-uniform
+      float y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[i] = __shfl_xor(acc[t][i], 1, 64);
+      const int k = (t0 + t) * 16 + c;
+      if ((c & 1) == 0) {
+        const int kk = k >> 1;
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const int j = (fbase + i) >> 1;
+          if (j >= ly.no) continue;
+          if (kk < ly.ni) {
+            const int64_t w = static_cast<int64_t>(j) * ly.ni + kk;
+            part[ly.w_re + w] = acc[t][i] + y[i + 1];
+            part[ly.w_im + w] = acc[t][i + 1] - y[i];
+          } else if (kk == ly.ni) {  // the ones column: bias gradients
+            if (ly.b_re >= 0) part[ly.b_re + j] = acc[t][i];
+            if (ly.b_im >= 0) part[ly.b_im + j] = acc[t][i + 1];
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---- host plan ---------------------------------------------------------------------------------
+struct Plan {
+  MArgs a;
+  int rt;
+  size_t lds;
+  int64_t ws_bytes;
+  int64_t op_bytes, f32_off, f64_off;
+  unsigned fb_grid, pack_grid, wgrad_grid;
+};
+
+int64_t roundup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, int64_t batch, int64_t n_params,
+                  Plan* out) {
+  if (mode != SMC_CVNN_MFMA_F32 && mode != SMC_CVNN_MFMA_BF16)
+    return fail(SMC_ERR_INVALID_ARGUMENT, "cvnn mfma: mode must be SMC_CVNN_MFMA_F32 or SMC_CVNN_MFMA_BF16");
+  if (!layers || n_layers <= 0 || n_layers > kMaxL || batch <= 0)
+    return fail(SMC_ERR_INVALID_SHAPE, "cvnn mfma: 1..SMC_CVNN_MAX_LAYERS layers and a positive batch");
+  const bool bf16 = mode == SMC_CVNN_MFMA_BF16;
+  const int KB = bf16 ? OpBf16::KB : OpF32::KB;
+  const size_t es = bf16 ? 2 : 4;
+  Plan p{};
+  MArgs& a = p.a;
+  a.n_layers = n_layers;
+  a.batch = batch;
+  a.n_params = n_params;
+  int wmax = 0;
+  for (int l = 0; l < n_layers; ++l) {
+    const smc_cvnn_layer& s = layers[l];
+    if (s.in_features <= 0 || s.out_features <= 0 || (l > 0 && s.in_features != layers[l - 1].out_features))
+      return fail(SMC_ERR_INVALID_SHAPE, "cvnn mfma: inconsistent layer table");
+    MLayer& m = a.layer[l];
+    m.ni = s.in_features;
+    m.no = s.out_features;
+    m.act = s.activation;
+    m.win = static_cast<int32_t>(roundup(2 * m.ni, KB));
+    m.wout = static_cast<int32_t>(roundup(2 * m.no, KB));
+    m.kx = static_cast<int32_t>(roundup(2 * m.ni + 1, 16));
+    m.w_re = s.w_re;
+    m.w_im = s.w_im;
+    m.b_re = s.b_re;
+    m.b_im = s.b_im;
+    m.act_bias = s.act_bias;
+    wmax = m.win > wmax ? m.win : wmax;
+  }
+  const int wlast = a.layer[n_layers - 1].wout;
+  // LDS: split-K scratch [waves][RT][64] f32x4, two activation / gradient buffers [R][zs] and the last
+  // layer's output gradient [R][gs]; row strides are odd multiples of 16 bytes (conflict-free
+  // 16-byte fragment reads)
+  a.zs = static_cast<int32_t>(wmax + 16 / es);
+  a.gs = static_cast<int32_t>(wlast + 16 / es);
+  const size_t per16 = 16 * (2 * static_cast<size_t>(a.zs) + a.gs) * es + kFbWaves * 64 * 16;
+  if (per16 > kLdsCap) return fail(SMC_ERR_INVALID_SHAPE, "cvnn mfma: layer widths exceed the LDS budget");
+  p.rt = 2 * per16 <= kLdsPair && batch >= 4096 ? 2 : 1;
+  a.rows = 16 * p.rt;
+  p.lds = per16 * p.rt;
+  // batch segments of the weight gradients: powers of two, >= kSegmentRows rows each, until the
+  // (feature tile, column-tile group, segment) items fill the chip
+  int64_t tiles = 0;
+  for (int l = 0; l < n_layers; ++l) {
+    const int ntile = a.layer[l].kx / 16;
+    tiles += static_cast<int64_t>(a.layer[l].wout / 16) * ((ntile + kWgradTiles - 1) / kWgradTiles);
+  }
+  int segs = 1;
+  while (segs < kMaxSegments && batch / (2 * segs) >= kSegmentRows && tiles * 2 * segs <= kWgradItems) segs *= 2;
+  a.segs = segs;
+  const int64_t unit = roundup(a.rows, 2 * KB);  // powers of two: the rows and two K blocks divide it
+  a.bp = roundup(batch, unit * segs);
+  a.nwg = static_cast<int32_t>(a.bp / a.rows);
+  // workspace: Op region (packed weights, Z^T, dU^T), f32 region (pre-activations, modReLU partials), f64 (loss)
+  int64_t op = 0;
+  a.pack_elems = 0;
+  for (int l = 0; l < n_layers; ++l) {
+    MLayer& m = a.layer[l];
+    m.wc = op;
+    op += static_cast<int64_t>(m.wout) * m.win;
+    m.wct = op;
+    op += static_cast<int64_t>(m.wout) * m.win;
+    a.pack_elems += 2LL * m.wout * m.win;
+  }
+  for (int l = 0; l < n_layers; ++l) {
+    MLayer& m = a.layer[l];
+    op = roundup(op, 64);
+    m.zt = op;
+    op += static_cast<int64_t>(m.kx) * a.bp;
+    op = roundup(op, 64);
+    m.gt = op;
+    op += static_cast<int64_t>(m.wout) * a.bp;
+  }
+  p.op_bytes = roundup(op * static_cast<int64_t>(es), 256);
+  int64_t f = 0;
+  for (int l = 0; l < n_layers; ++l) {
+    MLayer& m = a.layer[l];
+    m.pre = -1;
+    m.cpart = -1;
+    if (l + 1 < n_layers && m.act != SMC_ACT_NONE) {
+      m.pre = f;
+      f = roundup(f + a.bp * 2 * m.no, 64);
+    }
+    if (m.act == SMC_ACT_MODRELU) {
+      m.cpart = f;
+      f = roundup(f + static_cast<int64_t>(a.nwg) * m.no, 64);
+    }
+    const int ntile = m.kx / 16;
+    m.items = static_cast<int64_t>(m.wout / 16) * ((ntile + kWgradTiles - 1) / kWgradTiles) * a.segs;
+  }
+  p.f32_off = p.op_bytes;
+  p.f64_off = roundup(p.f32_off + f * 4, 256);
+  p.ws_bytes = p.f64_off + static_cast<int64_t>(a.nwg) * 8;
+  int64_t items = a.segs;
+  for (int l = 0; l < n_layers; ++l) items += a.layer[l].items;
+  p.fb_grid = static_cast<unsigned>(a.nwg);
+  p.wgrad_grid = static_cast<unsigned>((items + kWaves - 1) / kWaves);
+  const int64_t pg = (a.pack_elems + kThreads - 1) / kThreads;
+  p.pack_grid = static_cast<unsigned>(pg < 2048 ? pg : 2048);
+  *out = p;
+  return SMC_OK;
+}
+
+template <class Op, int RT>
+int32_t launch_fb(const Plan& p, hipStream_t s) {
+  auto kernel = fb_kernel<Op, RT>;
+  if (p.lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          static_cast<int>(p.lds)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "cvnn fb_kernel: cannot raise the dynamic LDS limit");
+  }
+  hipLaunchKernelGGL(kernel, dim3(p.fb_grid), dim3(kFbThreads), p.lds, s, p.a);
+  return SMC_OK;
+}
+
+template <class Op>
+int32_t launch_all(const Plan& p, hipStream_t s) {
+  hipLaunchKernelGGL(pack_kernel<Op>, dim3(p.pack_grid), dim3(kThreads), 0, s, p.a);
+  if (int32_t rc = check_launch("cvnn pack_kernel")) return rc;
+  if (int32_t rc = p.rt == 2 ? launch_fb<Op, 2>(p, s) : launch_fb<Op, 1>(p, s)) return rc;
+  if (int32_t rc = check_launch("cvnn fb_kernel")) return rc;
+  hipLaunchKernelGGL(wgrad_kernel<Op>, dim3(p.wgrad_grid), dim3(kThreads), 0, s, p.a);
+  return check_launch("cvnn wgrad_kernel");
+}
+
+}  // namespace
+}  // namespace smc
+
+using namespace smc;
+
+#pragma GCC visibility push(default)
+extern "C" {
+
+int32_t smc_cvnn_mfma_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, int64_t batch,
+                           int64_t* partial_blocks, int64_t* workspace_bytes) {
+  if (!partial_blocks || !workspace_bytes) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_mfma_plan: null output");
+  Plan p;
+  const int32_t rc = make_plan(layers, n_layers, mode, batch, 0, &p);
+  if (rc != SMC_OK) return rc;
+  *partial_blocks = p.a.segs;
+  *workspace_bytes = p.ws_bytes;
+  return SMC_OK;
+}
+
+int32_t smc_cvnn_mfma_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode,
+                                       const float* params, int64_t n_params, const float* input_re,
+                                       const float* input_im, const void* targets, int64_t batch, float* partials,
+                                       int64_t partial_blocks, void* workspace, int64_t workspace_bytes,
+                                       void* stream) {
+  if (!params || !input_re || !targets || !partials || !workspace || n_params <= 0)
+    return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_mfma_forward_backward: bad argument");
+  for (int l = 0; layers && l < n_layers && l < kMaxL; ++l) {
+    const smc_cvnn_layer& s = layers[l];
+    const int64_t w = static_cast<int64_t>(s.in_features) * s.out_features;
+    bool ok = s.activation >= SMC_ACT_NONE && s.activation <= SMC_ACT_ZRELU && s.w_re >= 0 && s.w_im >= 0 &&
+              s.w_re + w <= n_params && s.w_im + w <= n_params;
+    for (int64_t o : {s.b_re, s.b_im}) ok = ok && (o < 0 || o + s.out_features <= n_params);
+    if (s.activation == SMC_ACT_MODRELU) ok = ok && s.act_bias >= 0 && s.act_bias + s.out_features <= n_params;
+    if (!ok) return fail(SMC_ERR_INVALID_SHAPE, "smc_cvnn_mfma_forward_backward: inconsistent layer table");
+  }
+  Plan p;
+  const int32_t rc = make_plan(layers, n_layers, mode, batch, n_params, &p);
+  if (rc != SMC_OK) return rc;
+  if (partial_blocks != p.a.segs) return fail(SMC_ERR_INVALID_SHAPE, "smc_cvnn_mfma_forward_backward: partial_blocks != plan");
+  if (workspace_bytes < p.ws_bytes) return fail(SMC_ERR_INVALID_SHAPE, "smc_cvnn_mfma_forward_backward: workspace too small");
+  MArgs& a = p.a;
+  a.params = params;
+  a.in_re = input_re;
+  a.in_im = input_im;
+  a.targets = static_cast<const float*>(targets);
+  a.opws = workspace;
+  a.fws = reinterpret_cast<float*>(static_cast<char*>(workspace) + p.f32_off);
+  a.lossp = reinterpret_cast<double*>(static_cast<char*>(workspace) + p.f64_off);
+  a.partials = partials;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  return mode == SMC_CVNN_MFMA_BF16 ? launch_all<OpBf16>(p, s) : launch_all<OpF32>(p, s);
+}
+
+}  // extern "C"
+#pragma GCC visibility pop

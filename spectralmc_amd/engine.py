@@ -123,23 +123,33 @@ class TrainingEngine:
         """Host -> device cursor (outside any captured region)."""
         self.cursor.copy_(torch.tensor([sobol_index, ordinal], dtype=torch.int64), non_blocking=False)
 
-    def enqueue_step(self) -> StepBuffers:
-        """Launch contracts + targets of the next step on the current stream, advance the cursor."""
-        stream = _lib.stream_handle()
+    def make_slot(self) -> StepBuffers:
+        """Another set of step outputs (contracts, CVNN input, targets) the step can write into
+        directly; the training session rotates through a few so the network part of step s reads
+        its own slot while steps s+1, s+2 are produced (no hand-off copy)."""
         b = self.buffers
+        return StepBuffers(contracts=torch.empty_like(b.contracts), real_in=torch.empty_like(b.real_in),
+                           imag_in=b.imag_in, targets=torch.empty_like(b.targets))
+
+    def enqueue_step(self, out: StepBuffers | None = None) -> StepBuffers:
+        """Launch contracts + targets of the next step on the current stream into ``out`` (default:
+        the engine's own buffers), advance the cursor."""
+        stream = _lib.stream_handle()
+        b = out if out is not None else self.buffers
         offset = self.rank * self.B
         draw_device(self.tables, self.dim, self.cursor[0:1], offset, self.B, self.lower, self.upper, b.contracts,
                     b.real_in if self._f32_in else None)
         if not self._f32_in:
             b.real_in.copy_(b.contracts)
-        self.launch_targets(stream, _lib.ptr(self.cursor[1:2]), offset)
+        self.launch_targets(stream, _lib.ptr(self.cursor[1:2]), offset, b)
         self.cursor.add_(self.global_batch)
         return b
 
-    def launch_targets(self, stream: int | None, ordinal_ptr: int | None, ordinal0: int) -> None:
-        """The fused path/CF kernel(s) for the current contracts (training needs only the
+    def launch_targets(self, stream: int | None, ordinal_ptr: int | None, ordinal0: int,
+                       b: StepBuffers | None = None) -> None:
+        """The fused path/CF kernel(s) for the contracts in ``b`` (training needs only the
         terminal row sum, so no rowsum buffer)."""
-        b = self.buffers
+        b = b if b is not None else self.buffers
         _lib.check(_lib.lib().smc_train_targets(
             _lib.ptr(b.contracts), self.B, self.T, self.N, self.M, self.seed, ordinal_ptr, ordinal0,
             self._scheme, self._norm, self._dtype_code, self.store_mode, _lib.ptr(self._paths_buf), self.pitch,

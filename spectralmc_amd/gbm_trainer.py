@@ -35,7 +35,7 @@ import torch
 from pydantic import BaseModel, ConfigDict, PositiveInt, ValidationError
 
 from . import _lib
-from .engine import TrainingEngine
+from .engine import StepBuffers, TrainingEngine
 from .errors.gbm import EngineFailure, NormalsUnavailable
 from .errors.sampler import SamplerValidationFailed, SequenceExhausted
 from .errors.trainer import (
@@ -218,13 +218,15 @@ class _StepProgram:
     """The per-step device program, split into a Monte-Carlo part and a network part so that
     the two can run on separate HIP streams (see TrainingSession):
 
-        mc()       Sobol draw + fused paths/targets launch into the engine buffers (+ cursor)
-        handoff()  copy the engine's CVNN input + targets into the network's own buffers
-        fwd_bwd()  CVNN forward, spectral MSE, backward into the flat [grads..., loss] buffer
+        mc(k)      Sobol draw + fused paths/targets launch into step slot k (+ cursor)
+        handoff(k) engines that cannot write a slot: copy their buffers into slot k
+        fwd_bwd(k) CVNN forward, spectral MSE, backward into the flat [grads..., loss] buffer
         reduce()   data-parallel mean of the flat buffer (one RCCL all-reduce)
         update()   Adam + post-step grad norm
 
     Each part runs eagerly or is recorded once into a hipGraph and replayed."""
+
+    SLOTS = 3
 
     def __init__(self, pricer: "GbmCVNNPricer", engine: TrainingEngine, adam: optim.Optimizer,
                  params: list[nn.Parameter], dp) -> None:
@@ -245,29 +247,40 @@ class _StepProgram:
         self.loss = torch.zeros((), dtype=params[0].dtype, device=dev)
         self.grad_norm = torch.zeros((), dtype=params[0].dtype, device=dev)
         eb = engine.buffers
-        # two network input slots: the hand-off of step s fills slot s % 2 while the network may
-        # still be reading slot (s - 1) % 2
-        self.real_in = [torch.empty_like(eb.real_in) for _ in range(2)]
+        # SLOTS step slots: step s's MC part writes slot s % SLOTS directly while the network parts
+        # of steps s-1, s-2 may still read theirs, so the MC stream never waits for a network part
+        # still queued behind the MC kernel (and no hand-off copy sits between MC launches)
+        self.direct = hasattr(engine, "make_slot")
+        self.slots = ([engine.make_slot() for _ in range(self.SLOTS)] if self.direct else
+                      [StepBuffers(contracts=torch.empty_like(eb.contracts), real_in=torch.empty_like(eb.real_in),
+                                   imag_in=eb.imag_in, targets=torch.empty_like(eb.targets))
+                       for _ in range(self.SLOTS)])
+        self.real_in = [b.real_in for b in self.slots]
         self.imag_in = eb.imag_in  # constant zeros
-        self.targets = [torch.empty_like(eb.targets) for _ in range(2)]
-        self.mc_graph: torch.cuda.CUDAGraph | None = None
+        self.targets = [b.targets for b in self.slots]
+        self.mc_graphs: list[torch.cuda.CUDAGraph] = []  # per slot
         self.nn_graphs: list[list[torch.cuda.CUDAGraph]] = []  # per slot
         # network half on the fused HIP kernels when the architecture allows (net.py)
         self.fused = None
         if getattr(pricer, "fused_network", False):
             from .net import FusedNetworkStep, UnsupportedNetwork
 
+            compute = getattr(pricer, "network_compute", "auto")
             try:
                 self.fused = FusedNetworkStep(pricer._cvnn, adam, params, self.flat, self.loss, self.grad_norm,
-                                              batch=eb.real_in.shape[0], fuse_adam=dp is None)
+                                              batch=eb.real_in.shape[0], fuse_adam=dp is None, compute=compute)
             except UnsupportedNetwork:
+                if compute in ("mfma", "bf16"):  # an explicit kernel request never degrades silently
+                    raise
                 self.fused = None
 
     # -- pieces -------------------------------------------------------------------------
-    def mc(self) -> None:
-        self.engine.enqueue_step()
+    def mc(self, slot: int) -> None:
+        self.engine.enqueue_step(self.slots[slot] if self.direct else None)
 
     def handoff(self, slot: int) -> None:
+        if self.direct:
+            return
         eb = self.engine.buffers
         self.real_in[slot].copy_(eb.real_in)
         self.targets[slot].copy_(eb.targets)
@@ -301,18 +314,23 @@ class _StepProgram:
     # -- eager / graph execution ------------------------------------------------------------
     @property
     def captured(self) -> bool:
-        return self.mc_graph is not None
+        return bool(self.mc_graphs)
 
     def capture(self, mc_stream: torch.cuda.Stream, nn_stream: torch.cuda.Stream) -> None:
-        """Record the MC part (own memory pool: it may replay concurrently with the network
-        graphs) and the network part (two graphs around the all-reduce when data-parallel)."""
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=mc_stream):
-            self.mc()
+        """Record the MC part per slot (own memory pool: it may replay concurrently with the
+        network graphs) and the network part per slot (two graphs around the all-reduce when
+        data-parallel).  Capturing launches nothing, so the device cursor does not move."""
+        graphs = []
+        mc_pool = torch.cuda.graph_pool_handle()
+        for slot in range(self.SLOTS):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=mc_pool, stream=mc_stream):
+                self.mc(slot)
+            graphs.append(g)
         pool = torch.cuda.graph_pool_handle()
         self.nn_graphs = []
         upd = None
-        for slot in range(2):
+        for slot in range(self.SLOTS):
             g1 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1, pool=pool, stream=nn_stream):
                 self.fwd_bwd(slot)
@@ -326,13 +344,13 @@ class _StepProgram:
                 with torch.cuda.graph(upd, pool=pool, stream=nn_stream):
                     self.update()
             self.nn_graphs.append([g1, upd])
-        self.mc_graph = g
+        self.mc_graphs = graphs
 
-    def run_mc(self) -> None:
-        if self.mc_graph is not None:
-            self.mc_graph.replay()
+    def run_mc(self, slot: int) -> None:
+        if self.mc_graphs:
+            self.mc_graphs[slot].replay()
         else:
-            self.mc()
+            self.mc(slot)
 
     def run_nn(self, slot: int) -> None:
         if not self.nn_graphs:
@@ -364,6 +382,10 @@ class GbmCVNNPricer:
     #: network forward/backward/Adam on the fused HIP kernels (csrc/cvnn.hip) when the CVNN is a
     #: ComplexLinear + modReLU/zReLU chain; False (or other architectures): torch-ROCm modules
     fused_network: bool = True
+    #: fused network kernels (net.FusedNetworkStep): "auto" (f32 on MFMA when the widths fit, else
+    #: VALU), "valu", "mfma", or "bf16" (bf16 MFMA operands, f32 master weights / Adam: the
+    #: BASELINE configs[2] extension; the reference asserts full precision, gbm_trainer.py:679-686)
+    network_compute: str = "auto"
 
     @staticmethod
     def create(cfg: GbmCVNNPricerConfig) -> Result["GbmCVNNPricer", GbmPricerError]:
@@ -724,9 +746,10 @@ class TrainingSession:
             self.mc_stream = self.stream
         self.stream.wait_stream(cur)
         self.mc_stream.wait_stream(cur)
-        self._handed = torch.cuda.Event()    # MC buffers copied to a network input slot
-        self._nn_done = [torch.cuda.Event(), torch.cuda.Event()]  # network finished with slot i
-        self._slot_used = [False, False]
+        K = _StepProgram.SLOTS
+        self._mc_done = [torch.cuda.Event() for _ in range(K)]  # step slot k written by the MC part
+        self._nn_done = [torch.cuda.Event() for _ in range(K)]  # network finished reading slot k
+        self._slot_used = [False] * K
         self._mc_pending = False             # the MC part of the next step is already enqueued
         self.mc_events: list[tuple[torch.cuda.Event, torch.cuda.Event]] | None = None
         self._closed = False
@@ -745,27 +768,19 @@ class TrainingSession:
             if self._mc_pending:  # the pending eager MC launch must finish before capture
                 self.mc_stream.synchronize()
             prog.capture(self.mc_stream, self.stream)
-        slot = self.steps % 2
+        K = _StepProgram.SLOTS
+        slot = self.steps % K
         with torch.cuda.stream(self.mc_stream):
             if not self._mc_pending:
-                prog.run_mc()
-            if self._slot_used[slot]:  # the network step two back must be done with this slot
-                self.mc_stream.wait_event(self._nn_done[slot])
+                self._enqueue_mc(slot)
             prog.handoff(slot)
-            self._handed.record(self.mc_stream)
+            self._mc_done[slot].record(self.mc_stream)
             self._mc_pending = False
             if prefetch_next and self.sobol_skip + 2 * self.global_batch <= MAX_POINTS:
-                if self.mc_events is not None:  # live timing of the MC part on its own stream
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(self.mc_stream)
-                    prog.run_mc()
-                    e1.record(self.mc_stream)
-                    self.mc_events.append((e0, e1))
-                else:
-                    prog.run_mc()
+                self._enqueue_mc((self.steps + 1) % K)
                 self._mc_pending = True
         with torch.cuda.stream(self.stream):
-            self.stream.wait_event(self._handed)
+            self.stream.wait_event(self._mc_done[slot])
             prog.run_nn(slot)
             self._nn_done[slot].record(self.stream)
             self._slot_used[slot] = True
@@ -774,6 +789,20 @@ class TrainingSession:
         self.global_step += 1
         self.pricer._mc_engine.advance(self.global_batch)
         return Success(self.global_step)
+
+    def _enqueue_mc(self, slot: int) -> None:
+        """MC part of a step into ``slot`` on the MC stream, once the network part that last read
+        the slot (SLOTS steps back) is done with it."""
+        if self._slot_used[slot]:
+            self.mc_stream.wait_event(self._nn_done[slot])
+        if self.mc_events is not None:  # live timing of the MC part on its own stream
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(self.mc_stream)
+            self.program.run_mc(slot)
+            e1.record(self.mc_stream)
+            self.mc_events.append((e0, e1))
+        else:
+            self.program.run_mc(slot)
 
     def sync(self) -> None:
         self.stream.synchronize()

@@ -1,10 +1,19 @@
 """Fused network half of the training step on the HIP kernels of csrc/cvnn.hip.
 
 ``FusedNetworkStep`` replaces the torch-ROCm forward / spectral-MSE / backward / Adam of
-``_torch_step`` (reference gbm_trainer.py:819-835) with three launches when the CVNN is a
+``_torch_step`` (reference gbm_trainer.py:819-835) with a handful of launches when the CVNN is a
 chain of ComplexLinear layers with optional modReLU / zReLU activations — the
 architectures ``cvnn_factory`` builds without batch norm or residual blocks.  Other models
 keep the torch path.
+
+Kernels (``compute``):
+  "auto"  f32 networks on the matrix cores (csrc/cvnn_mfma.hip, v_mfma_f32_16x16x4_f32) when the
+          widths fit its LDS plan, else the VALU kernels of csrc/cvnn.hip; f64 on the VALU kernels
+  "valu"  the VALU kernels (f32 / f64)
+  "mfma"  the f32 MFMA kernels (error if the shape does not fit)
+  "bf16"  bf16 operands on v_mfma_f32_16x16x32_bf16 with f32 accumulation and f32 master
+          parameters / Adam (BASELINE.json configs[2]; an extension of the reference, which
+          asserts full precision, gbm_trainer.py:679-686)
 
 State stays where torch expects it: the model's parameters and the Adam moments become views
 into flat device buffers (the kernels' layout), the Adam state dict keeps its keys
@@ -80,7 +89,7 @@ class FusedNetworkStep:
 
     def __init__(self, model: nn.Module, adam: torch.optim.Optimizer, params: list[nn.Parameter],
                  flat_grads: torch.Tensor, loss_out: torch.Tensor, grad_norm_out: torch.Tensor, batch: int,
-                 fuse_adam: bool) -> None:
+                 fuse_adam: bool, compute: str = "auto") -> None:
         if len(adam.param_groups) != 1:
             raise UnsupportedNetwork("one Adam parameter group expected")
         g = adam.param_groups[0]
@@ -98,8 +107,25 @@ class FusedNetworkStep:
         dev = params[0].device
         L = _lib.lib()
         self._layers = (_lib.CvnnLayer * len(self.table))(*self.table)
-        blocks = ctypes.c_int64()
-        _lib.check(L.smc_cvnn_plan(self._layers, len(self.table), self.dtype_code, batch, ctypes.byref(blocks)))
+        if compute not in ("auto", "valu", "mfma", "bf16"):
+            raise ValueError(f"compute must be auto / valu / mfma / bf16, not {compute!r}")
+        self.mode = 0  # 0: VALU kernels, else SMC_CVNN_MFMA_F32 / SMC_CVNN_MFMA_BF16
+        blocks, ws_bytes = ctypes.c_int64(), ctypes.c_int64()
+        if compute != "valu" and dtype == torch.float32:
+            mode = _lib.CVNN_MFMA_BF16 if compute == "bf16" else _lib.CVNN_MFMA_F32
+            st = L.smc_cvnn_mfma_plan(self._layers, len(self.table), mode, batch, ctypes.byref(blocks),
+                                      ctypes.byref(ws_bytes))
+            if st == _lib.SMC_OK:
+                self.mode = mode
+            elif compute != "auto":
+                raise UnsupportedNetwork(f"MFMA network kernels: {_lib.last_error()}")
+        elif compute in ("mfma", "bf16"):
+            raise UnsupportedNetwork(f"MFMA network kernels take f32 parameters, not {dtype}")
+        if self.mode:
+            self.workspace = torch.empty(ws_bytes.value, dtype=torch.uint8, device=dev)
+        else:
+            _lib.check(L.smc_cvnn_plan(self._layers, len(self.table), self.dtype_code, batch, ctypes.byref(blocks)))
+            self.workspace = None
         self.blocks = blocks.value
         self.partials = torch.empty((self.blocks, self.n + 1), dtype=dtype, device=dev)
         self.norm_partials = torch.empty(int(L.smc_adam_norm_partials(self.n)), dtype=torch.float64, device=dev)
@@ -141,14 +167,24 @@ class FusedNetworkStep:
         """Gradients + loss into the flat buffer (and, fused, the Adam step) on the current stream."""
         L = _lib.lib()
         stream = _lib.stream_handle()
-        _lib.check(L.smc_cvnn_forward_backward(self._layers, len(self.table), self.dtype_code,
-                                               _lib.ptr(self.params_flat), self.n, _lib.ptr(real_in),
-                                               _lib.ptr(imag_in) if imag_in is not None else None,
-                                               _lib.ptr(targets), self.batch, _lib.ptr(self.partials), self.blocks,
-                                               stream))
+        if self.mode:
+            _lib.check(L.smc_cvnn_mfma_forward_backward(
+                self._layers, len(self.table), self.mode, _lib.ptr(self.params_flat), self.n, _lib.ptr(real_in),
+                _lib.ptr(imag_in) if imag_in is not None else None, _lib.ptr(targets), self.batch,
+                _lib.ptr(self.partials), self.blocks, _lib.ptr(self.workspace), self.workspace.numel(), stream))
+        else:
+            _lib.check(L.smc_cvnn_forward_backward(self._layers, len(self.table), self.dtype_code,
+                                                   _lib.ptr(self.params_flat), self.n, _lib.ptr(real_in),
+                                                   _lib.ptr(imag_in) if imag_in is not None else None,
+                                                   _lib.ptr(targets), self.batch, _lib.ptr(self.partials),
+                                                   self.blocks, stream))
         _lib.check(L.smc_cvnn_reduce_grads(self.dtype_code, _lib.ptr(self.partials), self.blocks, self.n,
                                            _lib.ptr(self.grads),
                                            ctypes.byref(self.adam_args) if self.fuse_adam else None, stream))
+
+    @property
+    def kernels(self) -> str:
+        return {0: "valu", _lib.CVNN_MFMA_F32: "mfma_f32", _lib.CVNN_MFMA_BF16: "mfma_bf16"}[self.mode]
 
     def adam(self) -> None:
         """Adam + grad norm + loss copy from the (all-reduced) flat buffer."""

@@ -73,6 +73,9 @@ GBM_CASES = (
 )
 
 
+from bn_archs import BN_ARCHS  # noqa: E402  (the same builders construct this build's modules in the tests)
+
+
 def main() -> None:
     sys.dont_write_bytecode = True
     sys.path.insert(0, REF)
@@ -169,6 +172,40 @@ def main() -> None:
         out[f"cvnn_{name}_step_gradnorm"] = np.array(gn)
         for k, v in net.state_dict().items():
             out[f"cvnn_{name}_after__{k}"] = v.detach().numpy().copy()
+
+    # batch-norm / residual architectures (cvnn.py:213-480): train-mode forward, one _torch_step
+    # (batch statistics, running-stat updates, Adam) and the eval-mode forward after it
+    for name, make in BN_ARCHS.items():
+        with torch.random.fork_rng():
+            torch.manual_seed(321)
+            net = make(ref_cvnn)
+        for k, v in net.state_dict().items():
+            out[f"bn_{name}__{k}"] = v.detach().numpy().copy()
+        x_re = torch.tensor(contracts / contracts.max(axis=0), dtype=torch.float32)
+        x_im = torch.tensor(np.roll(contracts, 1, axis=1) / contracts.max(axis=0), dtype=torch.float32)
+        net.train()
+        with torch.no_grad():
+            yr, yi = net(x_re, x_im)
+        out[f"bn_{name}_fwd_re"], out[f"bn_{name}_fwd_im"] = yr.numpy(), yi.numpy()
+        n_out = yr.shape[1]
+        tgt = rng.normal(size=(contracts.shape[0], n_out)) + 1j * rng.normal(size=(contracts.shape[0], n_out))
+        out[f"bn_{name}_step_targets"] = tgt.astype(np.complex64)
+        targets = torch.tensor(out[f"bn_{name}_step_targets"])
+        adam = torch.optim.Adam(net.parameters(), lr=1e-2)
+        pr, pi = net(x_re, x_im)
+        loss = torch.nn.functional.mse_loss(pr, torch.real(targets)) + torch.nn.functional.mse_loss(
+            pi, torch.imag(targets))
+        adam.zero_grad(set_to_none=True)
+        loss.backward()
+        adam.step()
+        out[f"bn_{name}_step_loss"] = np.array(float(loss.item()))
+        out[f"bn_{name}_step_gradnorm"] = np.array(float(torch.nn.utils.clip_grad_norm_(net.parameters(), float("inf"))))
+        for k, v in net.state_dict().items():
+            out[f"bn_{name}_after__{k}"] = v.detach().numpy().copy()
+        net.eval()
+        with torch.no_grad():
+            er, ei = net(x_re, x_im)
+        out[f"bn_{name}_eval_re"], out[f"bn_{name}_eval_im"] = er.numpy(), ei.numpy()
 
     np.savez_compressed(OUT, **out)
     print(f"wrote {OUT}: {len(out)} arrays, {os.path.getsize(OUT)} bytes")

@@ -35,7 +35,8 @@ def test_library_exports_every_declared_symbol() -> None:
 INTEGRATION = os.path.join(os.path.dirname(HEADER), "..", "INTEGRATION.md")
 _CTYPES = {"c_int32": ctypes.c_int32, "c_int64": ctypes.c_int64, "c_uint64": ctypes.c_uint64,
            "c_void_p": ctypes.c_void_p, "c_char_p": ctypes.c_char_p, "None": None,
-           "ctypes.POINTER(c_void_p)": ctypes.POINTER(ctypes.c_void_p)}
+           "ctypes.POINTER(c_void_p)": ctypes.POINTER(ctypes.c_void_p),
+           "ctypes.POINTER(c_int64)": ctypes.POINTER(ctypes.c_int64)}
 
 
 def test_integration_doc_bindings_match_abi() -> None:

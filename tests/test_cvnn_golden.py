@@ -135,3 +135,49 @@ def test_build_model_leaves_caller_rng_untouched() -> None:
     before = torch.get_rng_state()
     make(123, [32], 128, torch.float32)
     assert torch.equal(before, torch.get_rng_state())
+
+
+@pytest.mark.parametrize("name", ["cov", "proj"])
+def test_batchnorm_residual_match_reference(golden, name) -> None:
+    """Covariance / naive complex batch norm and the residual block (reference cvnn.py:213-480),
+    built by the same builder over the reference's modules (tests/golden/bn_archs.py): initial
+    state bit-exact; train-mode forward (batch statistics), one _torch_step (loss, grad norm,
+    Adam update, running-statistic updates) and the eval-mode forward after it to f32 rounding."""
+    import spectralmc_amd.cvnn as ours
+    from tests.golden.bn_archs import BN_ARCHS
+
+    with torch.random.fork_rng():
+        torch.manual_seed(321)
+        net = BN_ARCHS[name](ours)
+    sd = net.state_dict()
+    keys = sorted(k.split("__", 1)[1] for k in golden if k.startswith(f"bn_{name}__"))
+    assert sorted(sd) == keys
+    for k in keys:
+        np.testing.assert_array_equal(sd[k].numpy(), golden[f"bn_{name}__{k}"], err_msg=k)
+    c = golden["sobol_s7_k0"]
+    x_re = torch.tensor(c / c.max(axis=0), dtype=torch.float32)
+    x_im = torch.tensor(np.roll(c, 1, axis=1) / c.max(axis=0), dtype=torch.float32)
+    net.train()
+    with torch.no_grad():
+        yr, yi = net(x_re, x_im)
+    np.testing.assert_allclose(yr.numpy(), golden[f"bn_{name}_fwd_re"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(yi.numpy(), golden[f"bn_{name}_fwd_im"], rtol=1e-5, atol=1e-6)
+    targets = torch.tensor(golden[f"bn_{name}_step_targets"])
+    adam = torch.optim.Adam(net.parameters(), lr=1e-2)
+    pr, pi = net(x_re, x_im)
+    loss = torch.nn.functional.mse_loss(pr, targets.real) + torch.nn.functional.mse_loss(pi, targets.imag)
+    adam.zero_grad(set_to_none=True)
+    loss.backward()
+    adam.step()
+    gn = float(torch.nn.utils.clip_grad_norm_(net.parameters(), float("inf")))
+    assert float(loss.detach()) == pytest.approx(float(golden[f"bn_{name}_step_loss"]), rel=1e-5)
+    assert gn == pytest.approx(float(golden[f"bn_{name}_step_gradnorm"]), rel=1e-4)
+    for k, v in net.state_dict().items():
+        ref = golden[f"bn_{name}_after__{k}"]
+        np.testing.assert_allclose(v.numpy(), ref, rtol=1e-5, atol=1e-6 * max(1.0, float(np.abs(ref).max())),
+                                   err_msg=k)
+    net.eval()
+    with torch.no_grad():
+        er, ei = net(x_re, x_im)
+    np.testing.assert_allclose(er.numpy(), golden[f"bn_{name}_eval_re"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(ei.numpy(), golden[f"bn_{name}_eval_im"], rtol=1e-4, atol=1e-5)

@@ -64,7 +64,7 @@ def _run(rank: int, world: int, outdir: str) -> None:
         buffers.contracts.copy_(torch.from_numpy(contracts))
         buffers.real_in.copy_(torch.from_numpy(contracts))
         buffers.targets.copy_(torch.from_numpy(targets))
-        slot = s % 2  # the session's alternating network input slots
+        slot = s % prog.SLOTS  # the session's rotating step slots (engines without slots: a hand-off copy)
         prog.handoff(slot)
         prog.run_nn(slot)  # TrainingSession's network half: fwd/bwd, all-reduce, Adam (eager here)
         losses.append(float(prog.loss))

@@ -1,0 +1,148 @@
+"""The network step on the matrix cores (csrc/cvnn_mfma.hip) against the oracle's explicit-precision
+restatement (oracle/cvnn_mixed.py, itself equal to torch autograd of _torch_step in f32,
+tests/test_cvnn_mixed_oracle.py):
+
+* SMC_CVNN_MFMA_F32: loss within 1e-5 rel, gradients within 1e-5 norm-relative (f32 summation
+  order is the only difference);
+* SMC_CVNN_MFMA_BF16: the same bf16 roundings as the restatement; a GPU f32 accumulation that lands
+  an intermediate on the other side of a bf16 rounding boundary moves that element by one bf16 ulp,
+  so loss within 1e-4 rel and gradients within 2e-3 norm-relative;
+* shapes: the C2 network (6 -> 32 -> 32 -> 256) and its H = 256 variant, the C3 network
+  (6 -> 32 -> 32 -> 1024), zReLU and a last-layer activation, ragged batches (row padding);
+* bit-identical reruns; the trainer's C3 session on the bf16 kernels.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.cvnn_mixed import cvnn_step
+from spectralmc_amd import _lib
+from spectralmc_amd.cvnn import ComplexLinear, ComplexSequential, modReLU, zReLU
+from spectralmc_amd.net import FusedNetworkStep
+from tests.helpers import make_test_cvnn
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def table_of(step: FusedNetworkStep) -> list[tuple[int, ...]]:
+    return [(t.in_features, t.out_features, t.activation, t.w_re, t.w_im, t.b_re, t.b_im, t.act_bias)
+            for t in step.table]
+
+
+def build(arch: str, n_out: int) -> torch.nn.Module:
+    if arch == "zrelu":
+        torch.manual_seed(5)
+        return ComplexSequential(ComplexLinear(6, 24), zReLU(), ComplexLinear(24, 40), modReLU(40),
+                                 ComplexLinear(40, n_out)).to(DEV)
+    if arch == "lastact":
+        torch.manual_seed(6)
+        return ComplexSequential(ComplexLinear(6, 32), modReLU(32), ComplexLinear(32, n_out), modReLU(n_out)).to(DEV)
+    width = 256 if arch == "h256" else 32
+    return make_test_cvnn(n_inputs=6, n_outputs=n_out, seed=123, dtype=torch.float32, device=DEV,
+                          hidden_layers=2, hidden_width=width)
+
+
+def data(B: int, n_out: int, seed: int = 11) -> tuple[torch.Tensor, torch.Tensor]:
+    g = torch.Generator().manual_seed(seed)
+    # contract-like inputs (positive, up to ~1e4 on the first features) and CF-magnitude targets
+    scale = torch.tensor([1e4, 2e4, 10.0, 0.2, 0.2, 2.0])
+    x = torch.rand((B, 6), generator=g) * scale
+    t = torch.complex(torch.randn((B, n_out), generator=g), torch.randn((B, n_out), generator=g)) * 1e3
+    return x, t
+
+
+def gpu_grads(model, compute: str, x: torch.Tensor, t: torch.Tensor) -> tuple[FusedNetworkStep, torch.Tensor]:
+    params = list(model.parameters())
+    adam = torch.optim.Adam(params, lr=1e-3)
+    n = sum(p.numel() for p in params)
+    flat = torch.zeros(n + 1, dtype=torch.float32, device=DEV)
+    loss = torch.zeros((), dtype=torch.float32, device=DEV)
+    gn = torch.zeros((), dtype=torch.float32, device=DEV)
+    step = FusedNetworkStep(model, adam, params, flat, loss, gn, x.shape[0], fuse_adam=False, compute=compute)
+    xd = x.to(DEV)
+    step.fwd_bwd(xd, torch.zeros_like(xd), t.to(DEV))
+    torch.cuda.synchronize()
+    return step, flat.cpu()
+
+
+CASES = [("c2", 256, 4096), ("c2", 256, 1000), ("c3", 1024, 2048), ("h256", 256, 4096), ("zrelu", 64, 21),
+         ("lastact", 96, 333)]
+
+
+@pytest.mark.parametrize("compute", ["mfma", "bf16"])
+@pytest.mark.parametrize("arch,n_out,B", CASES)
+def test_mfma_step_matches_oracle(compute, arch, n_out, B) -> None:
+    model = build(arch, n_out)
+    x, t = data(B, n_out)
+    params0 = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu().numpy()
+    step, flat = gpu_grads(model, compute, x, t)
+    assert step.kernels == ("mfma_bf16" if compute == "bf16" else "mfma_f32")
+    operand = "bf16" if compute == "bf16" else "f32"
+    loss, g = cvnn_step(table_of(step), params0, x.numpy(), None, t.numpy(), operand=operand)
+    got = flat[:-1].double().numpy()
+    rel = np.linalg.norm(got - g) / np.linalg.norm(g)
+    loss_rel = abs(float(flat[-1]) - loss) / loss
+    tol_g, tol_l = (2e-3, 1e-4) if compute == "bf16" else (1e-5, 1e-5)
+    assert loss_rel < tol_l, (loss_rel, rel)
+    assert rel < tol_g, (loss_rel, rel)
+    # every parameter group is resolved, not only the largest
+    off = 0
+    for p in model.parameters():
+        k = p.numel()
+        sl = slice(off, off + k)
+        gn = np.linalg.norm(g[sl])
+        if gn > 1e-3 * np.linalg.norm(g):
+            assert np.linalg.norm(got[sl] - g[sl]) / gn < 10 * tol_g
+        off += k
+
+
+@pytest.mark.parametrize("compute", ["mfma", "bf16"])
+def test_mfma_step_bit_reproducible(compute) -> None:
+    model = build("c3", 1024)
+    x, t = data(4096, 1024, seed=3)
+    _, a = gpu_grads(model, compute, x, t)
+    _, b = gpu_grads(model, compute, x, t)
+    assert torch.equal(a, b)
+
+
+def test_auto_uses_mfma_for_f32_and_valu_for_f64() -> None:
+    m32 = build("c2", 256)
+    s32, _ = gpu_grads(m32, "auto", *data(64, 256))
+    assert s32.kernels == "mfma_f32"
+    m64 = make_test_cvnn(n_inputs=6, n_outputs=64, seed=1, dtype=torch.float64, device=DEV, hidden_layers=1)
+    params = list(m64.parameters())
+    n = sum(p.numel() for p in params)
+    z = torch.zeros((), dtype=torch.float64, device=DEV)
+    s64 = FusedNetworkStep(m64, torch.optim.Adam(params), params, torch.zeros(n + 1, dtype=torch.float64, device=DEV),
+                           z, z.clone(), 16, fuse_adam=True, compute="auto")
+    assert s64.kernels == "valu"
+
+
+def test_c3_training_session_on_bf16_kernels() -> None:
+    """Two steps of the C3 shape (network 6 -> 32 -> 32 -> 1024 on bf16 MFMA, N = 1024) through
+    the trainer with a small batch: the session uses the bf16 kernels and the loss is finite and
+    equals the oracle step on the same targets."""
+    from spectralmc_amd.gbm_trainer import GbmCVNNPricer
+    from spectralmc_amd.models.numerical import Precision
+    from tests.helpers import (expect_success, make_black_scholes_config, make_domain_bounds, make_gbm_cvnn_config,
+                               make_simulation_params, make_training_config)
+
+    sp = make_simulation_params(timesteps=16, network_size=1024, batches_per_mc_run=4, threads_per_block=256,
+                                mc_seed=7, buffer_size=4, dtype=Precision.float32)
+    model = make_test_cvnn(n_inputs=6, n_outputs=1024, seed=123, dtype=torch.float32, device=DEV, hidden_layers=2)
+    cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                               domain_bounds=make_domain_bounds())
+    pricer = expect_success(GbmCVNNPricer.create(cfg))
+    pricer.network_compute = "bf16"
+    session = expect_success(pricer.open_session(make_training_config(num_batches=2, batch_size=64,
+                                                                      learning_rate=1e-2)))
+    assert session.program.fused is not None and session.program.fused.kernels == "mfma_bf16"
+    for _ in range(2):
+        expect_success(session.step())
+    final = session.close()
+    assert np.isfinite(final.loss)

@@ -39,6 +39,12 @@ for step in "$@"; do
     dp)      run dp 600 python -u -m pytest tests/test_gpu_dp.py -x -v --timeout 300 --timeout-method thread -rf ;;
     bench_c5) run bench_c5 600 python bench.py --config c5 --steps 10 --warmup 3 --kernel-iters 2 ;;
     prof_c5) cd /tmp && run prof_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv -- python "$ROOT/bench.py" --config c5 --steps 5 --warmup 2 --kernel-iters 1 --no-cpu-baseline; cd "$ROOT" ;;
+    bench_h256) run bench_h256 600 python bench.py --config c2h256 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    bench_seq) run bench_seq 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --overlap off ;;
+    prof_seq) cd /tmp && run prof_seq 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_seq" -o run --output-format csv -- python "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --overlap off; cd "$ROOT" ;;
+    bench_valu) run bench_valu 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --network valu ;;
+    bench_c3_f32) run bench_c3_f32 900 python bench.py --config c3 --steps 3 --warmup 2 --kernel-iters 1 --no-cpu-baseline --network mfma ;;
+    gputests_v) run gputests_v 1100 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider -rf ;;
     bench_c3) run bench_c3 900 python bench.py --config c3 --steps 3 --warmup 2 --kernel-iters 1 --no-cpu-baseline ;;
     prof)    cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; cd "$ROOT" ;;
     prof_default) cd /tmp && run prof_default 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_default" -o run --output-format csv -- python "$ROOT/bench.py"; cd "$ROOT" ;;
