@@ -66,6 +66,7 @@ def parse() -> argparse.Namespace:
                     help="network kernels (default: bf16 for c3, auto otherwise)")
     ap.add_argument("--overlap", default="on", choices=["on", "off"],
                     help="MC part of step s+1 on its own stream beside step s's network part (pricer.overlap_mc)")
+    ap.add_argument("--graphs", default="on", choices=["on", "off"], help="replay the step as hipGraphs")
     ap.add_argument("--kernel-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU-baseline sample")
@@ -222,7 +223,7 @@ def main() -> None:
     pricer = expect_success(GbmCVNNPricer.create(cfg))
     pricer.store_paths = args.store == "all"
     pricer.math_mode = args.math
-    pricer.warmup_steps = max(1, min(2, args.warmup))
+    pricer.warmup_steps = max(1, min(2, args.warmup)) if args.graphs == "on" else 0
     pricer.network_compute = args.network or NETWORK_COMPUTE.get(args.config, "auto")
     pricer.overlap_mc = args.overlap == "on"
     if n_assets:

@@ -27,6 +27,7 @@
 #pragma clang fp contract(off)
 
 #include "smc_internal.h"
+#include "smc_sobol.h"
 #include "smc_math.h"
 #include "smc_rng.h"
 
@@ -75,6 +76,18 @@ struct EngineArgs {
   double* partials;           // [B][slices][all_rows ? T : 1] slice row sums (slices > 1)
   uint32_t* arrivals;         // [B] arrival counters, zero between launches (slices > 1)
   uint32_t* queues;           // [16] queue_kernel work counters, zero between launches (slices > 1)
+  // fused training step (smc_train_step, resident_kernel only): each workgroup draws its own
+  // contracts' Sobol rows, and the last workgroup to finish advances the cursor
+  const uint32_t* sobol;      // table image (smc_sobol_export_tables) or NULL
+  int32_t sobol_dim;          // == 6 (BlackScholes.Inputs)
+  const double* lower;
+  const double* upper;
+  double* contracts_out;      // [B][6] f64
+  float* cvnn_out;            // [B][6] f32 CVNN input or NULL
+  int64_t* cursor;            // [2]: Sobol index, normal ordinal of the step's first contract
+  int64_t sobol_index0;       // Sobol index offset of contract 0 of this launch (rank * B)
+  int64_t advance;            // cursor[0..1] += advance after the launch
+  uint32_t* done;             // workgroups finished, zero between launches
 };
 
 #ifndef SMC_SLICE_CHUNKS
@@ -740,7 +753,7 @@ constexpr int kResRegChunks = kResMaxChunks - kResLdsChunks;
 constexpr size_t kResTermBytes = static_cast<size_t>(kResLdsChunks) * kResThreads * 16;  // 128 KiB
 
 size_t resident_lds_bytes(int N) {
-  return kResTermBytes + (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N)) * sizeof(double);
+  return kResTermBytes + (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 8) * sizeof(double);
 }
 
 template <bool LOG_EULER, bool HW, bool STORE_ALL>
@@ -762,10 +775,24 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   double* avg = wsum + kResWaves;         // [N]
   double* cs = avg + N;                   // [N]
   double* sn = cs + N;                    // [N]
+  double* row = sn + N;                   // [6] this contract's drawn Sobol row (fused step)
   for (int j = tid; j < N; j += kResThreads) math::twiddle(j, N, sn[j], cs[j]);
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
+  const int64_t sob0 = a.sobol ? a.cursor[0] + a.sobol_index0 : 0;
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    const Contract c = load_contract(a.contracts + b * 6);
+    Contract c;
+    if (a.sobol) {  // draw the contract (sobol_sampler.py:222-246) instead of a separate kernel
+      if (tid < 6) {
+        const double v = sobol_coord(a.sobol, a.sobol_dim, tid, static_cast<uint64_t>(sob0 + b), a.lower, a.upper);
+        row[tid] = v;
+        a.contracts_out[b * 6 + tid] = v;
+        if (a.cvnn_out) a.cvnn_out[b * 6 + tid] = static_cast<float>(v);
+      }
+      lds_barrier();
+      c = Contract{row[0], row[1], row[2], row[3], row[4], row[5]};
+    } else {
+      c = load_contract(a.contracts + b * 6);
+    }
     const Stepper<float, LOG_EULER, HW> step(c, kRowBlock);
     const float x0 = static_cast<float>(c.X0);
     float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * kRowBlock * pitch : b * pitch);
@@ -822,7 +849,16 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     }
     lds_barrier();
     fft_row<float, kResThreads, true>(avg, cs, sn, N, part, part + N, static_cast<float2*>(a.targets) + b * N);
-    lds_barrier();  // part (= term_lds) / avg / wsum are reused by the next contract
+    lds_barrier();  // part (= term_lds) / avg / wsum / row are reused by the next contract
+  }
+  if (a.done && tid == 0) {
+    // every workgroup read the cursor before it arrives here: the last one advances it
+    __threadfence();
+    if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
+      a.cursor[0] += a.advance;
+      a.cursor[1] += a.advance;
+      *a.done = 0u;
+    }
   }
 }
 
@@ -1137,6 +1173,13 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   return fail(SMC_ERR_INVALID_ARGUMENT, "engine: unsupported scheme / math mode");
 }
 
+__global__ void advance_cursor_kernel(int64_t* cursor, int64_t advance) {
+  if (threadIdx.x == 0) {
+    cursor[0] += advance;
+    cursor[1] += advance;
+  }
+}
+
 int32_t dispatch_engine(const EngineArgs& a, int32_t dtype, hipStream_t stream) {
   if (dtype == SMC_DTYPE_F32) return launch_engine<float>(a, stream);
   if (dtype == SMC_DTYPE_F64) return launch_engine<double>(a, stream);
@@ -1249,6 +1292,64 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
     if (int32_t st = dispatch_engine(a, dtype, as_stream(stream))) return st;
   }
   return SMC_OK;
+}
+
+int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const double* lower_dev, const double* upper_dev,
+                       int64_t* cursor_dev, int64_t index_offset, int64_t advance, double* contracts_dev,
+                       float* cvnn_input_dev, int64_t n_contracts, int32_t timesteps, int32_t network_size,
+                       int32_t batches_per_mc_run, uint64_t mc_seed, int32_t scheme, int32_t normalization,
+                       int32_t dtype, int32_t store_mode, void* paths_dev, int64_t path_pitch, int64_t chunk_contracts,
+                       void* targets_dev, uint32_t* counter_dev, void* stream) {
+  if (!sobol_tables_dev || !lower_dev || !upper_dev || !cursor_dev || !contracts_dev || !counter_dev)
+    return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_step: NULL buffer");
+  if (dim != 6) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_step: dim must be 6 (BlackScholes.Inputs)");
+  if (index_offset < 0 || advance < 0) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_step: negative offset");
+  const hipStream_t s = as_stream(stream);
+  const int64_t P = static_cast<int64_t>(network_size) * batches_per_mc_run;
+  EngineArgs a{};
+  a.B = n_contracts;
+  a.T = timesteps;
+  a.P = P;
+  a.N = network_size;
+  a.M = batches_per_mc_run;
+  a.seed = mc_seed;
+  a.ordinal_dev = cursor_dev + 1;
+  a.ordinal0 = index_offset;
+  a.scheme = scheme;
+  a.normalize = normalization != SMC_NORM_RAW;
+  a.store = store_mode;
+  a.simulate = 1;
+  a.paths = paths_dev;
+  a.targets = targets_dev;
+  a.pitch = path_pitch;
+  a.slices = 1;
+  const bool fused = SMC_TRAIN_MODE == 3 && dtype == SMC_DTYPE_F32 && n_contracts > 0 && chunk_contracts >= n_contracts &&
+                     valid_scheme(scheme) && (store_mode == SMC_STORE_ALL || store_mode == SMC_STORE_TERMINAL) &&
+                     paths_dev && targets_dev && network_size > 0 && batches_per_mc_run > 0 && resident_ok(a, true);
+  if (fused) {
+    a.contracts = contracts_dev;
+    a.sobol = sobol_tables_dev;
+    a.sobol_dim = dim;
+    a.lower = lower_dev;
+    a.upper = upper_dev;
+    a.contracts_out = contracts_dev;
+    a.cvnn_out = cvnn_input_dev;
+    a.cursor = cursor_dev;
+    a.sobol_index0 = index_offset;
+    a.advance = advance;
+    a.done = counter_dev;
+    return dispatch_engine(a, dtype, s);
+  }
+  // any other shape: the Sobol draw, the targets launch(es), then the cursor advance
+  if (int32_t st = smc_sobol_draw(sobol_tables_dev, dim, cursor_dev, index_offset, n_contracts, lower_dev, upper_dev,
+                                  contracts_dev, cvnn_input_dev, stream))
+    return st;
+  if (int32_t st = smc_train_targets(contracts_dev, n_contracts, timesteps, network_size, batches_per_mc_run, mc_seed,
+                                     cursor_dev + 1, index_offset, scheme, normalization, dtype, store_mode, paths_dev,
+                                     path_pitch, chunk_contracts, nullptr, targets_dev, nullptr, 0, stream))
+    return st;
+  hipLaunchKernelGGL(advance_cursor_kernel, dim3(1), dim3(64), 0, s, cursor_dev, advance);
+  return check_launch("advance_cursor_kernel");
 }
 
 int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, int64_t n_paths, int32_t all_rows) {

@@ -17,6 +17,7 @@
 #include <new>
 
 #include "smc_internal.h"
+#include "smc_sobol.h"
 #include "sobol_dirnums.h"
 
 #pragma clang fp contract(off)  // numpy rounds (upper - lower) * raw and + lower separately
@@ -159,20 +160,8 @@ __global__ void sobol_draw_kernel(const uint32_t* __restrict__ tables, int dim,
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t idx = static_cast<uint64_t>((index_dev ? *index_dev : 0) + index0 + i);
-  const uint64_t g = idx ^ (idx >> 1);
-  const uint32_t* sv = tables + dim;
   for (int d = 0; d < dim; ++d) {
-    uint32_t x = tables[d];
-    const uint32_t* svd = sv + d * SMC_SOBOL_BITS;
-#pragma unroll
-    for (int c = 0; c < SMC_SOBOL_BITS; ++c)
-      x ^= ((g >> c) & 1u) ? svd[c] : 0u;
-    const double raw = static_cast<double>(x) * 0x1p-30;
-    // numpy evaluates (upper - lower) * raw + lower with separate roundings: no FMA
-    // (the file-level `fp contract(off)` covers these operators; header intrinsics would not).
-    const double span = upper[d] - lower[d];
-    const double prod = span * raw;
-    const double val = lower[d] + prod;
+    const double val = smc::sobol_coord(tables, dim, d, idx, lower, upper);
     out[i * dim + d] = val;
     if (out_f32) out_f32[i * dim + d] = static_cast<float>(val);
   }

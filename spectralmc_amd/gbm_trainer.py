@@ -226,7 +226,7 @@ class _StepProgram:
 
     Each part runs eagerly or is recorded once into a hipGraph and replayed."""
 
-    SLOTS = 3
+    SLOTS = 4
 
     def __init__(self, pricer: "GbmCVNNPricer", engine: TrainingEngine, adam: optim.Optimizer,
                  params: list[nn.Parameter], dp) -> None:
@@ -248,8 +248,10 @@ class _StepProgram:
         self.grad_norm = torch.zeros((), dtype=params[0].dtype, device=dev)
         eb = engine.buffers
         # SLOTS step slots: step s's MC part writes slot s % SLOTS directly while the network parts
-        # of steps s-1, s-2 may still read theirs, so the MC stream never waits for a network part
-        # still queued behind the MC kernel (and no hand-off copy sits between MC launches)
+        # of earlier steps may still read theirs (no hand-off copy between MC launches).  A network
+        # part cannot run beside the path kernel (which holds every CU's registers), so its kernels
+        # run in the gaps between path kernels and one network part completes two path kernels
+        # after its own: with 4 slots the MC part never waits for a network part that just finished
         self.direct = hasattr(engine, "make_slot")
         self.slots = ([engine.make_slot() for _ in range(self.SLOTS)] if self.direct else
                       [StepBuffers(contracts=torch.empty_like(eb.contracts), real_in=torch.empty_like(eb.real_in),

@@ -55,6 +55,10 @@ def test_integration_doc_bindings_match_abi() -> None:
     for name, rt in restypes:
         assert _CTYPES[rt] == _lib.SIGNATURES[name][0], name
     assert {n for n, _ in argtypes} == {n for n, _ in restypes}
+    # every header line the stub cites declares the function it binds
+    header = open(HEADER).read().splitlines()
+    for name, line in re.findall(r"_lib\.(smc_\w+)\.argtypes[^#]*?#\s*spectralmc_hip\.h:(\d+)", text, flags=re.S):
+        assert f"{name}(" in header[int(line) - 1], (name, line)
     # every documented call passes as many arguments as the header declares
     calls = re.findall(r"_check\(_lib\.(smc_\w+)\((.*?)\)\)\n", code, flags=re.S)
     assert len(calls) >= 3

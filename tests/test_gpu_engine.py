@@ -368,3 +368,57 @@ def test_resident_kernel_bit_exact(oracle, golden, B, N, M, store) -> None:
     again, _, _ = _run_targets(c, 16, N, M, 0, 1, "float32", store, ordinal0=21, with_rowsum=False,
                                chunk=max(1, B // 3))
     np.testing.assert_array_equal(again, kt)
+
+
+# ------------------------------------------------------------------------------ fused step
+STEP_CASES = [  # (B, T, N, M, math, store): resident shapes (fused launch) and fallback shapes
+    (None, 16, 256, 256, _lib.MATH_HW, _lib.STORE_ALL),      # C2 per-contract shape, 2 rounds + 3
+    (37, 16, 64, 64, 0, _lib.STORE_TERMINAL),                # resident, portable math, terminal rows
+    (21, 16, 128, 1024, _lib.MATH_HW, _lib.STORE_ALL),       # P = 131,072: split pair fallback
+    (9, 5, 64, 4, 0, _lib.STORE_ALL),                        # T != 16: contract_kernel fallback
+]
+
+
+@pytest.mark.parametrize("B,T,N,M,math,store", STEP_CASES)
+def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store) -> None:
+    """smc_train_step (Sobol draw + targets + cursor advance; one resident_kernel launch where the
+    shape allows) is bit-identical to smc_sobol_draw + smc_train_targets + the cursor update, over
+    three consecutive steps of a rank-1-of-2 shard; the arrival counter is left at zero."""
+    L = _L()
+    if B is None:
+        B = 2 * torch.cuda.get_device_properties(0).multi_processor_count + 3
+    P = N * M
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
+    lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
+    hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
+    pitch = int(L.smc_path_pitch(P, 0))
+    shape = (B, T, pitch) if store == _lib.STORE_ALL else (B, pitch)
+    paths = torch.empty(shape, dtype=torch.float32, device=DEV)
+    scheme = _lib.SCHEME_LOG_EULER | math
+    offset, adv = B, 2 * B  # rank 1 of 2
+    cur_a = torch.tensor([100, 50], dtype=torch.int64, device=DEV)
+    cur_b = cur_a.clone()
+    counter = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for _ in range(3):
+        ca = torch.empty((B, 6), dtype=torch.float64, device=DEV)
+        fa = torch.empty((B, 6), dtype=torch.float32, device=DEV)
+        ta = torch.empty((B, N), dtype=torch.complex64, device=DEV)
+        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur_a), offset, adv,
+                                    _lib.ptr(ca), _lib.ptr(fa), B, T, N, M, 7, scheme, _lib.NORM_NORMALIZE,
+                                    _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, B, _lib.ptr(ta),
+                                    _lib.ptr(counter), None))
+        cb = torch.empty_like(ca)
+        fb = torch.empty_like(fa)
+        tb = torch.empty_like(ta)
+        draw_device(tables, 6, cur_b[0:1], offset, B, lo, hi, cb, fb)
+        _lib.check(L.smc_train_targets(_lib.ptr(cb), B, T, N, M, 7, _lib.ptr(cur_b[1:2]), offset, scheme,
+                                       _lib.NORM_NORMALIZE, _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, B, None,
+                                       _lib.ptr(tb), None, 0, None))
+        cur_b.add_(adv)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(ca.cpu().numpy(), cb.cpu().numpy())
+        np.testing.assert_array_equal(fa.cpu().numpy(), fb.cpu().numpy())
+        np.testing.assert_array_equal(ta.cpu().numpy(), tb.cpu().numpy())
+        assert cur_a.tolist() == cur_b.tolist()
+        assert int(counter.item()) == 0

@@ -42,6 +42,9 @@ for step in "$@"; do
     bench_h256) run bench_h256 600 python bench.py --config c2h256 --steps 20 --warmup 3 --no-cpu-baseline ;;
     bench_seq) run bench_seq 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --overlap off ;;
     prof_seq) cd /tmp && run prof_seq 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_seq" -o run --output-format csv -- python "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --overlap off; cd "$ROOT" ;;
+    bench_nograph) run bench_nograph 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --graphs off ;;
+    bench_seq_nograph) run bench_seq_nograph 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --graphs off --overlap off ;;
+    bench_q) run bench_q 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
     bench_valu) run bench_valu 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --network valu ;;
     bench_c3_f32) run bench_c3_f32 900 python bench.py --config c3 --steps 3 --warmup 2 --kernel-iters 1 --no-cpu-baseline --network mfma ;;
     gputests_v) run gputests_v 1100 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider -rf ;;
