@@ -46,7 +46,7 @@ constexpr int kMaxL = SMC_CVNN_MAX_LAYERS;
 constexpr int kWgradTiles = 4;       // column tiles (16 wide) per weight-gradient item: 16 accumulators
 constexpr int kMaxSegments = 64;     // batch segments of the weight-gradient GEMMs
 constexpr int kSegmentRows = 64;     // minimum rows per segment
-constexpr int64_t kWgradItems = 4096;  // segments are added until the items reach this
+constexpr int64_t kWgradItems = 8192;  // segments are added until the items reach this
 constexpr size_t kLdsCap = 156 * 1024;   // dynamic LDS of fb_kernel (160 KiB per CU, less its static LDS)
 constexpr size_t kLdsPair = 80 * 1024;   // two row tiles per workgroup only within this
 
@@ -116,7 +116,8 @@ struct MLayer {
   int64_t w_re, w_im, b_re, b_im, act_bias;
   int64_t wc, wct;   // Op offsets: Wc [wout][win], Wc^T [win][wout]
   int64_t zt, gt;    // Op offsets: Z^T [kx][bp], dU^T [wout][bp]
-  int64_t pre;       // f32 offset of the pre-activation [bp][2 no] (hidden layers with an activation), or -1
+  int64_t pre;       // f32 offset of the pre-activation [R][2 no] in the workgroup's LDS (hidden layers
+                     // with an activation), or -1
   int64_t cpart;     // f32 offset of the modReLU-bias partials [nwg][no], or -1
   int64_t items;     // weight-gradient items (waves) of this layer, all segments
 };
@@ -129,6 +130,7 @@ struct MArgs {
   int32_t nwg;       // fb workgroups = bp / rows
   int32_t segs;      // batch segments of the weight gradients
   int32_t zs, gs;    // LDS row strides (Op elements) of the activation and output-gradient buffers
+  int32_t pre_global;  // pre-activations in the f32 workspace [bp][2 no] instead of LDS [R][2 no]
   int64_t n_params;
   int64_t pack_elems;
   const float* params;
@@ -325,6 +327,7 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
   zbuf[0] = reinterpret_cast<T*>(net_lds + kFbWaves * RT * 64 * sizeof(f32x4));
   zbuf[1] = zbuf[0] + R * a.zs;
   T* gb = zbuf[1] + R * a.zs;
+  float* pre_lds = reinterpret_cast<float*>(gb + R * a.gs);  // 16-byte aligned: R * gs * sizeof(T) is
   const float* P = a.params;
 
   // ---- layer-0 input: Z_0 (interleaved re, im) into LDS and Z_0^T (+ ones row) into the workspace
@@ -368,7 +371,7 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
             if (ly.b_re >= 0) u += P[ly.b_re + j];
             if (ly.b_im >= 0) v += P[ly.b_im + j];
             if (ly.pre >= 0) {
-              float* pre = a.fws + ly.pre + (r0 + r) * (2LL * ly.no) + 2 * j;
+              float* pre = (a.pre_global ? a.fws + r0 * (2 * ly.no) : pre_lds) + ly.pre + r * (2 * ly.no) + 2 * j;
               pre[0] = u;
               pre[1] = v;
             }
@@ -470,7 +473,8 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
           if (j < lp.no) {
             float u = 0.0f, v = 0.0f;
             if (lp.pre >= 0) {
-              const float* pre = a.fws + lp.pre + (r0 + r) * (2LL * lp.no) + 2 * j;
+              const float* pre =
+                  (a.pre_global ? a.fws + r0 * (2 * lp.no) : pre_lds) + lp.pre + r * (2 * lp.no) + 2 * j;
               u = pre[0];
               v = pre[1];
             }
@@ -647,7 +651,15 @@ int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, 
   // 16-byte fragment reads)
   a.zs = static_cast<int32_t>(wmax + 16 / es);
   a.gs = static_cast<int32_t>(wlast + 16 / es);
-  const size_t per16 = 16 * (2 * static_cast<size_t>(a.zs) + a.gs) * es + kFbWaves * 64 * 16;
+  size_t pre_floats = 0;  // pre-activations of the hidden layers with an activation, per row
+  for (int l = 0; l + 1 < n_layers; ++l)
+    if (a.layer[l].act != SMC_ACT_NONE) pre_floats += 2 * static_cast<size_t>(a.layer[l].no);
+  size_t per16 = 16 * ((2 * static_cast<size_t>(a.zs) + a.gs) * es + pre_floats * 4) + kFbWaves * 64 * 16;
+  a.pre_global = 0;
+  if (per16 > kLdsCap) {  // pre-activations to the workspace instead
+    a.pre_global = 1;
+    per16 -= 16 * pre_floats * 4;
+  }
   if (per16 > kLdsCap) return fail(SMC_ERR_INVALID_SHAPE, "cvnn mfma: layer widths exceed the LDS budget");
   p.rt = 2 * per16 <= kLdsPair && batch >= 4096 ? 2 : 1;
   a.rows = 16 * p.rt;
@@ -686,14 +698,19 @@ int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, 
     op += static_cast<int64_t>(m.wout) * a.bp;
   }
   p.op_bytes = roundup(op * static_cast<int64_t>(es), 256);
-  int64_t f = 0;
+  int64_t f = 0, pre_off = 0;
   for (int l = 0; l < n_layers; ++l) {
     MLayer& m = a.layer[l];
     m.pre = -1;
     m.cpart = -1;
     if (l + 1 < n_layers && m.act != SMC_ACT_NONE) {
-      m.pre = f;
-      f = roundup(f + a.bp * 2 * m.no, 64);
+      if (a.pre_global) {
+        m.pre = f;
+        f = roundup(f + a.bp * 2 * m.no, 64);
+      } else {
+        m.pre = pre_off;
+        pre_off += static_cast<int64_t>(a.rows) * 2 * m.no;
+      }
     }
     if (m.act == SMC_ACT_MODRELU) {
       m.cpart = f;

@@ -261,6 +261,7 @@ class _StepProgram:
         self.imag_in = eb.imag_in  # constant zeros
         self.targets = [b.targets for b in self.slots]
         self.mc_graphs: list[torch.cuda.CUDAGraph] = []  # per slot
+        self.step_graphs: list[torch.cuda.CUDAGraph] = []  # per slot: MC + network (one stream)
         self.nn_graphs: list[list[torch.cuda.CUDAGraph]] = []  # per slot
         # network half on the fused HIP kernels when the architecture allows (net.py)
         self.fused = None
@@ -316,12 +317,26 @@ class _StepProgram:
     # -- eager / graph execution ------------------------------------------------------------
     @property
     def captured(self) -> bool:
-        return bool(self.mc_graphs)
+        return bool(self.mc_graphs or self.step_graphs)
 
     def capture(self, mc_stream: torch.cuda.Stream, nn_stream: torch.cuda.Stream) -> None:
         """Record the MC part per slot (own memory pool: it may replay concurrently with the
         network graphs) and the network part per slot (two graphs around the all-reduce when
-        data-parallel).  Capturing launches nothing, so the device cursor does not move."""
+        data-parallel).  On one stream without data parallelism the whole step (MC part, network
+        part, Adam) is one graph per slot.  Capturing launches nothing, so the device cursor does
+        not move."""
+        if mc_stream is nn_stream and self.dp is None:
+            pool = torch.cuda.graph_pool_handle()
+            self.step_graphs = []
+            for slot in range(self.SLOTS):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool, stream=mc_stream):
+                    self.mc(slot)
+                    self.handoff(slot)
+                    self.fwd_bwd(slot)
+                    self.update()
+                self.step_graphs.append(g)
+            return
         graphs = []
         mc_pool = torch.cuda.graph_pool_handle()
         for slot in range(self.SLOTS):
@@ -347,6 +362,15 @@ class _StepProgram:
                     self.update()
             self.nn_graphs.append([g1, upd])
         self.mc_graphs = graphs
+
+    def run_step(self, slot: int) -> None:
+        """The whole step on the current stream (one graph when captured on one stream)."""
+        if self.step_graphs:
+            self.step_graphs[slot].replay()
+            return
+        self.run_mc(slot)
+        self.handoff(slot)
+        self.run_nn(slot)
 
     def run_mc(self, slot: int) -> None:
         if self.mc_graphs:
@@ -772,6 +796,14 @@ class TrainingSession:
             prog.capture(self.mc_stream, self.stream)
         K = _StepProgram.SLOTS
         slot = self.steps % K
+        if self.stream is self.mc_stream and self.ctx is None:
+            with torch.cuda.stream(self.stream):  # sequential: one stream, one graph per step
+                prog.run_step(slot)
+            self.steps += 1
+            self.sobol_skip += self.global_batch
+            self.global_step += 1
+            self.pricer._mc_engine.advance(self.global_batch)
+            return Success(self.global_step)
         with torch.cuda.stream(self.mc_stream):
             if not self._mc_pending:
                 self._enqueue_mc(slot)
