@@ -43,10 +43,9 @@ typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxL = SMC_CVNN_MAX_LAYERS;
-constexpr int kWgradTiles = 4;       // column tiles (16 wide) per weight-gradient item: 16 accumulators
 constexpr int kMaxSegments = 64;     // batch segments of the weight-gradient GEMMs
-constexpr int kSegmentRows = 64;     // minimum rows per segment
-constexpr int64_t kWgradItems = 8192;  // segments are added until the items reach this
+constexpr int kSegmentRows = 256;    // minimum rows per segment
+constexpr int64_t kWgradBlocks = 2048;  // segments are added until the workgroups reach this
 constexpr size_t kLdsCap = 156 * 1024;   // dynamic LDS of fb_kernel (160 KiB per CU, less its static LDS)
 constexpr size_t kLdsPair = 80 * 1024;   // two row tiles per workgroup only within this
 
@@ -504,22 +503,38 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
   }
 }
 
-// ---- weight gradients: one wave per (layer, feature tile, column-tile group, segment) ----------
+// ---- weight gradients: one workgroup per (layer, 64 features, 64 columns, batch segment) ------
+// dWc block [64 f][64 k] = sum over the segment's rows of dU^T[f][row] Z^T[k][row]: both operands
+// staged through LDS in 64-row K stages (double-buffered, the next stage's global loads in flight
+// during the current stage's MFMAs); wave w computes the 32 x 32 quarter (w / 2, w % 2) as 2 x 2
+// tiles.  Workgroups past the tile blocks sum the loss and modReLU-bias partials of one segment
+// per wave.
+constexpr int kWgBlock = 64;  // output block edge
+constexpr int kWgStage = 64;  // batch rows per K stage (bf16; 32 for f32: the same 36 KiB of LDS)
+
 template <class Op>
 __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
   using T = typename Op::T;
-  constexpr int KQ = Op::KB / 4;
-  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  int64_t item = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  using V = typename Op::V;
+  constexpr int KB = Op::KB, KQ = KB / 4;
+  constexpr int ES = static_cast<int>(sizeof(T));
+  constexpr int KS = ES == 2 ? kWgStage : kWgStage / 2;  // batch rows per K stage
+  constexpr int LD = KS + 16 / ES;                       // LDS row stride (elements): odd multiple of 16 B
+  constexpr int PER = kWgBlock * KS / kThreads;          // elements each thread stages per operand
+  constexpr int NV = PER * ES / 16;                   // 16-byte loads per operand per thread
+  __shared__ __attribute__((aligned(16))) T stage[2][2][kWgBlock * LD];  // [buffer][A, B]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, c = lane & 15;
   const T* ws = static_cast<const T*>(a.opws);
   const int64_t stride = a.n_params + 1;
   const int64_t seg_rows = a.bp / a.segs;
+  int64_t item = blockIdx.x;
   int l = 0;
   while (l < a.n_layers && item >= a.layer[l].items) item -= a.layer[l].items, ++l;
   if (l == a.n_layers) {
-    // bookkeeping items, one per segment: loss and modReLU-bias gradients of the segment's rows
-    if (item >= a.segs) return;
-    const int s = static_cast<int>(item);
+    // bookkeeping: wave w of bookkeeping workgroup i sums segment 4 i + w
+    const int64_t sg = item * kWaves + wave;
+    if (sg >= a.segs) return;
+    const int s = static_cast<int>(sg);
     const int w0 = static_cast<int>(s * (seg_rows / a.rows)), w1 = static_cast<int>((s + 1) * (seg_rows / a.rows));
     float* part = a.partials + s * stride;
     if (lane == 0) {
@@ -539,60 +554,87 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
     return;
   }
   const MLayer& ly = a.layer[l];
-  const int ntile = ly.kx / 16;
-  const int ngroup = (ntile + kWgradTiles - 1) / kWgradTiles;
+  const int nfb = (ly.wout + kWgBlock - 1) / kWgBlock, nkb = (ly.kx + kWgBlock - 1) / kWgBlock;
   const int s = static_cast<int>(item % a.segs);
   const int64_t rest = item / a.segs;
-  const int kg = static_cast<int>(rest % ngroup);
-  const int ft = static_cast<int>(rest / ngroup);
-  const int t0 = kg * kWgradTiles;
-  const int nt = ntile - t0 < kWgradTiles ? ntile - t0 : kWgradTiles;
-  f32x4 acc[kWgradTiles];
-#pragma unroll
-  for (int t = 0; t < kWgradTiles; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int kblk = static_cast<int>(rest % nkb);
+  const int fblk = static_cast<int>(rest / nkb);
+  (void)nfb;
+  const int f_base = fblk * kWgBlock, k_base = kblk * kWgBlock;
   const int64_t b0 = s * seg_rows;
-  const T* ap = ws + ly.gt + (ft * 16 + c) * a.bp + b0 + g * KQ;
-  const T* bp0 = ws + ly.zt + (t0 * 16 + c) * a.bp + b0 + g * KQ;
-  using V = typename Op::V;
-  for (int64_t kb = 0; kb < seg_rows; kb += 2 * Op::KB) {  // two K blocks' fragments in flight
-    const V a0 = Op::ld(ap + kb), a1 = Op::ld(ap + kb + Op::KB);
-    V b0[kWgradTiles], b1[kWgradTiles];
+  // staging map: thread -> row tid / 4 of the block, elements (tid % 4) * 16 .. + 16 of the stage
+  const int srow = tid >> 2, scol = (tid & 3) * PER;
+  const bool a_ok = f_base + srow < ly.wout, b_ok = k_base + srow < ly.kx;
+  const T* ag = ws + ly.gt + (f_base + srow) * a.bp + b0 + scol;
+  const T* bg = ws + ly.zt + (k_base + srow) * a.bp + b0 + scol;
+  typedef float raw4 __attribute__((ext_vector_type(4)));
+  raw4 ra[NV], rb[NV];
+  auto fetch = [&](int64_t kb) {
 #pragma unroll
-    for (int t = 0; t < kWgradTiles; ++t) {
-      if (t < nt) {
-        b0[t] = Op::ld(bp0 + t * 16 * a.bp + kb);
-        b1[t] = Op::ld(bp0 + t * 16 * a.bp + kb + Op::KB);
-      }
+    for (int v = 0; v < NV; ++v) {
+      ra[v] = a_ok ? *reinterpret_cast<const raw4*>(ag + kb + v * (16 / ES)) : raw4{0.f, 0.f, 0.f, 0.f};
+      rb[v] = b_ok ? *reinterpret_cast<const raw4*>(bg + kb + v * (16 / ES)) : raw4{0.f, 0.f, 0.f, 0.f};
     }
+  };
+  auto put = [&](int buf) {
 #pragma unroll
-    for (int t = 0; t < kWgradTiles; ++t)
-      if (t < nt) acc[t] = Op::mmav(acc[t], a0, b0[t]);
+    for (int v = 0; v < NV; ++v) {
+      *reinterpret_cast<raw4*>(&stage[buf][0][srow * LD + scol + v * (16 / ES)]) = ra[v];
+      *reinterpret_cast<raw4*>(&stage[buf][1][srow * LD + scol + v * (16 / ES)]) = rb[v];
+    }
+  };
+  f32x4 acc[2][2];
 #pragma unroll
-    for (int t = 0; t < kWgradTiles; ++t)
-      if (t < nt) acc[t] = Op::mmav(acc[t], a1, b1[t]);
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nst = static_cast<int>(seg_rows / KS);
+  fetch(0);
+  put(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) fetch(static_cast<int64_t>(st + 1) * KS);
+#pragma unroll
+    for (int kb = 0; kb < KS; kb += KB) {
+      V af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[i] = Op::ld(&stage[buf][0][(wm * 32 + i * 16 + c) * LD + kb + g * KQ]);
+        bf[i] = Op::ld(&stage[buf][1][(wn * 32 + i * 16 + c) * LD + kb + g * KQ]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = Op::mmav(acc[i][j], af[i], bf[j]);
+    }
+    if (st + 1 < nst) put(buf ^ 1);
+    __syncthreads();
   }
   float* part = a.partials + s * stride;
-  const int fbase = ft * 16 + 4 * g;
 #pragma unroll
-  for (int t = 0; t < kWgradTiles; ++t) {
-    if (t < nt) {  // wave-uniform
+  for (int i = 0; i < 2; ++i) {
+    const int fbase = f_base + wm * 32 + i * 16 + 4 * g;
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
       float y[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) y[i] = __shfl_xor(acc[t][i], 1, 64);
-      const int k = (t0 + t) * 16 + c;
-      if ((c & 1) == 0) {
+      for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(acc[i][jt][r], 1, 64);
+      const int k = k_base + wn * 32 + jt * 16 + c;
+      if ((c & 1) == 0 && k < ly.kx) {
         const int kk = k >> 1;
 #pragma unroll
-        for (int i = 0; i < 4; i += 2) {
-          const int j = (fbase + i) >> 1;
+        for (int r = 0; r < 4; r += 2) {
+          const int j = (fbase + r) >> 1;
           if (j >= ly.no) continue;
           if (kk < ly.ni) {
             const int64_t w = static_cast<int64_t>(j) * ly.ni + kk;
-            part[ly.w_re + w] = acc[t][i] + y[i + 1];
-            part[ly.w_im + w] = acc[t][i + 1] - y[i];
+            part[ly.w_re + w] = acc[i][jt][r] + y[r + 1];
+            part[ly.w_im + w] = acc[i][jt][r + 1] - y[r];
           } else if (kk == ly.ni) {  // the ones column: bias gradients
-            if (ly.b_re >= 0) part[ly.b_re + j] = acc[t][i];
-            if (ly.b_im >= 0) part[ly.b_im + j] = acc[t][i + 1];
+            if (ly.b_re >= 0) part[ly.b_re + j] = acc[i][jt][r];
+            if (ly.b_im >= 0) part[ly.b_im + j] = acc[i][jt][r + 1];
           }
         }
       }
@@ -666,15 +708,13 @@ int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, 
   p.lds = per16 * p.rt;
   // batch segments of the weight gradients: powers of two, >= kSegmentRows rows each, until the
   // (feature tile, column-tile group, segment) items fill the chip
-  int64_t tiles = 0;
-  for (int l = 0; l < n_layers; ++l) {
-    const int ntile = a.layer[l].kx / 16;
-    tiles += static_cast<int64_t>(a.layer[l].wout / 16) * ((ntile + kWgradTiles - 1) / kWgradTiles);
-  }
+  int64_t blocks = 0;  // weight-gradient output blocks (64 x 64) of one segment
+  for (int l = 0; l < n_layers; ++l)
+    blocks += ((a.layer[l].wout + kWgBlock - 1) / kWgBlock) * static_cast<int64_t>((a.layer[l].kx + kWgBlock - 1) / kWgBlock);
   int segs = 1;
-  while (segs < kMaxSegments && batch / (2 * segs) >= kSegmentRows && tiles * 2 * segs <= kWgradItems) segs *= 2;
+  while (segs < kMaxSegments && batch / (2 * segs) >= kSegmentRows && blocks * 2 * segs <= kWgradBlocks) segs *= 2;
   a.segs = segs;
-  const int64_t unit = roundup(a.rows, 2 * KB);  // powers of two: the rows and two K blocks divide it
+  const int64_t unit = roundup(a.rows, kWgStage);  // powers of two: the rows and a K stage divide it
   a.bp = roundup(batch, unit * segs);
   a.nwg = static_cast<int32_t>(a.bp / a.rows);
   // workspace: Op region (packed weights, Z^T, dU^T), f32 region (pre-activations, modReLU partials), f64 (loss)
@@ -716,16 +756,15 @@ int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, 
       m.cpart = f;
       f = roundup(f + static_cast<int64_t>(a.nwg) * m.no, 64);
     }
-    const int ntile = m.kx / 16;
-    m.items = static_cast<int64_t>(m.wout / 16) * ((ntile + kWgradTiles - 1) / kWgradTiles) * a.segs;
+    m.items = ((m.wout + kWgBlock - 1) / kWgBlock) * static_cast<int64_t>((m.kx + kWgBlock - 1) / kWgBlock) * a.segs;
   }
   p.f32_off = p.op_bytes;
   p.f64_off = roundup(p.f32_off + f * 4, 256);
   p.ws_bytes = p.f64_off + static_cast<int64_t>(a.nwg) * 8;
-  int64_t items = a.segs;
+  int64_t items = (a.segs + kWaves - 1) / kWaves;  // bookkeeping workgroups (one segment per wave)
   for (int l = 0; l < n_layers; ++l) items += a.layer[l].items;
   p.fb_grid = static_cast<unsigned>(a.nwg);
-  p.wgrad_grid = static_cast<unsigned>((items + kWaves - 1) / kWaves);
+  p.wgrad_grid = static_cast<unsigned>(items);
   const int64_t pg = (a.pack_elems + kThreads - 1) / kThreads;
   p.pack_grid = static_cast<unsigned>(pg < 2048 ? pg : 2048);
   *out = p;
