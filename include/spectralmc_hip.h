@@ -170,7 +170,9 @@ int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t col
  * paths_dev: [chunk][A][T][pitch] f32 (SMC_STORE_ALL) or [chunk][A][pitch] (SMC_STORE_TERMINAL),
  * reused per launch of chunk_contracts; terminal_sum_dev (may be NULL): [B][A] f64 sums of the
  * terminal rows; targets_dev: [B][N] complex64.  math: 0 (portable, CPU-reproducible) or
- * SMC_MATH_HW.  Needs 1 <= A <= 8, N % 4 == 0, N <= 4096, N*M a multiple of 2048. */
+ * SMC_MATH_HW.  Needs 1 <= A <= 8, N % 4 == 0, N <= 4096, N*M a multiple of 2048.  With
+ * terminal_sum_dev each chunk is two launches (simulate + store + terminal sums, then the CF pass
+ * over the stored terminal rows), without it one fused launch; the targets are bit-identical. */
 int32_t smc_basket_train_targets(const double* contracts_dev, int64_t n_contracts, int32_t n_assets,
                                  int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
                                  uint64_t mc_seed, const int64_t* ordinal_dev, int64_t ordinal0,

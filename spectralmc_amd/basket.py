@@ -138,7 +138,8 @@ class BasketEngine:
     """Device buffers + launches of the basket Monte-Carlo side of one training step
     (the ``TrainingEngine`` interface)."""
 
-    kernel_name = "basket_kernel"
+    # the engine keeps the terminal sums, so each launch is the split pair (simulate, then CF)
+    kernel_name = "basket_kernel+basket_cf_kernel"
 
     def __init__(self, cfg: BasketConfig, batch_size: int, *, device: torch.device, sobol_skip: int = 0,
                  model_dtype: torch.dtype = torch.float32, rank: int = 0, world_size: int = 1,

@@ -77,14 +77,101 @@ __device__ void cholesky_equicorr(int A, double rho, double* L) {
     }
 }
 
-template <int A, bool HW>
+// Payoff + M-mean + DFT of contract b from its stored terminal rows and their sums tot[A] (in
+// LDS): the CF phase of basket_kernel, and all of basket_cf_kernel.
+template <int A>
+__device__ void basket_cf(const BasketArgs& a, int64_t b, const double* tot, double* part, double* avg,
+                          const double* cs, const double* sn) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x;
+  const int N = a.N, M = a.M;
+  const int64_t P = a.P;
+  const double* c = a.contracts + b * (3 * A + 4);
+  const double K = c[0], Tm = c[1], r = c[2];
+  const int64_t rows = a.store_all ? a.T : 1;
+  const float* cbase = a.paths + b * A * rows * a.pitch;
+  // payoff: per-asset forward scale, equal-weight basket, discounted put (f32, asset order)
+  const float Tf = static_cast<float>(Tm);
+  const float df = math::exp_any(static_cast<float>(-r) * Tf);
+  const float Kf = static_cast<float>(K);
+  const float wA = static_cast<float>(1.0 / A);
+  float sc[A];
+#pragma unroll
+  for (int i = 0; i < A; ++i) {
+    const float F = static_cast<float>(c[4 + i]) * math::exp_any(static_cast<float>(r - c[4 + A + i]) * Tf);
+    sc[i] = a.normalize ? F / static_cast<float>(tot[i] / static_cast<double>(P)) : 1.0f;
+  }
+  __amdgpu_buffer_rsrc_t rs[A];
+#pragma unroll
+  for (int i = 0; i < A; ++i) {
+    const float* trow = cbase + (i * rows + (rows - 1)) * a.pitch;
+    rs[i] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(trow), static_cast<short>(0), 0x7fffffff,
+                                              0x00020000);
+  }
+  // thread item (q, g): columns 4q..4q+3, batches m = g, g + G, ... (oracle_basket_kernel order)
+  const int cols = N / 4;
+  const int G = cols <= kBThreads ? kBThreads / cols : 1;
+  const int items = cols * G;
+  constexpr int kB = A <= 2 ? 8 : (A <= 4 ? 4 : 2);  // batches in flight per thread
+  for (int item = tid; item < items; item += kBThreads) {
+    const int q = item % cols, g = item / cols;
+    double sum[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int m0 = g; m0 < M; m0 += G * kB) {
+      v4f v[kB][A];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        const int m = m0 + u * G < M ? m0 + u * G : M - 1;
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+          v[u][i] = __builtin_amdgcn_raw_buffer_load_b128(rs[i], (m * N + 4 * q) * 4, 0, 16 /* sc1 */);
+      }
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        if (m0 + u * G < M) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float bs = 0.0f;
+#pragma unroll
+            for (int i = 0; i < A; ++i) bs = bs + v[u][i][e] * sc[i];
+            const float diff = Kf - bs * wA;
+            sum[e] += static_cast<double>(df * (diff > 0.0f ? diff : 0.0f));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[g * N + 4 * q + e] = sum[e];
+  }
+  __syncthreads();
+  for (int n = tid; n < N; n += kBThreads) {
+    double t2 = 0.0;
+    for (int g = 0; g < G; ++g) t2 += part[g * N + n];
+    avg[n] = t2 / static_cast<double>(M);
+  }
+  __syncthreads();
+  float2* out = a.targets + b * N;
+  for (int k = tid; k <= N / 2; k += kBThreads) {
+    double re = 0.0, im = 0.0;
+    int idx = 0;
+    for (int n = 0; n < N; ++n) {
+      re = fma(avg[n], cs[idx], re);
+      im = fma(-avg[n], sn[idx], im);
+      idx += k;
+      if (idx >= N) idx -= N;
+    }
+    out[k] = make_float2(static_cast<float>(re), static_cast<float>(im));
+    if (k != 0 && 2 * k != N) out[N - k] = make_float2(static_cast<float>(re), static_cast<float>(-im));
+  }
+}
+
+template <int A, bool HW, int MODE>  // MODE 0: simulate + CF, 1: simulate only (terminal sums out)
 __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kernel(BasketArgs a) {
   typedef float v4f __attribute__((ext_vector_type(4)));
   typedef float f2 __attribute__((ext_vector_type(2)));
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x;
-  const int T = a.T, N = a.N, M = a.M;
+  const int T = a.T, N = a.N;
   const int64_t P = a.P;
   double* Ld = lds;                          // [8][8]
   double* wsum = Ld + kMaxAssets * kMaxAssets;  // [kBWaves][A]
@@ -95,9 +182,10 @@ __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kerne
   double* sn = cs + N;
 
   const double* c = a.contracts + b * (3 * A + 4);
-  const double K = c[0], Tm = c[1], r = c[2], rho = c[3];
+  const double Tm = c[1], r = c[2], rho = c[3];
   if (tid == 0) cholesky_equicorr(A, rho, Ld);
-  for (int j = tid; j < N; j += kBThreads) math::twiddle(j, N, sn[j], cs[j]);
+  if (MODE == 0)
+    for (int j = tid; j < N; j += kBThreads) math::twiddle(j, N, sn[j], cs[j]);
   __syncthreads();
 
   // per-asset log2-unit coefficients (Stepper of gbm.hip); HW normals come out / sqrt(2 ln 2)
@@ -188,85 +276,30 @@ __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kerne
     tot[tid] = sum;
     if (a.terminal_sum) a.terminal_sum[b * A + tid] = sum;
   }
+  if constexpr (MODE == 1) return;  // basket_cf_kernel takes it from the stored rows and sums
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's terminal-row stores
   __syncthreads();
-#if defined(SMC_EXPERIMENT_NO_CF)  // tools/micro decomposition builds only
-  return;
-#endif
-
-  // payoff: per-asset forward scale, equal-weight basket, discounted put (f32, asset order)
-  const float Tf = static_cast<float>(Tm);
-  const float df = math::exp_any(static_cast<float>(-r) * Tf);
-  const float Kf = static_cast<float>(K);
-  const float wA = static_cast<float>(1.0 / A);
-  float sc[A];
-#pragma unroll
-  for (int i = 0; i < A; ++i) {
-    const float F = static_cast<float>(c[4 + i]) * math::exp_any(static_cast<float>(r - c[4 + A + i]) * Tf);
-    sc[i] = a.normalize ? F / static_cast<float>(tot[i] / static_cast<double>(P)) : 1.0f;
-  }
-  __amdgpu_buffer_rsrc_t rs[A];
-#pragma unroll
-  for (int i = 0; i < A; ++i) {
-    const float* trow = cbase + (i * rows + (rows - 1)) * pitch;
-    rs[i] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(trow), static_cast<short>(0), 0x7fffffff,
-                                              0x00020000);
-  }
-  // thread item (q, g): columns 4q..4q+3, batches m = g, g + G, ... (oracle_basket_kernel order)
-  const int cols = N / 4;
-  const int G = cols <= kBThreads ? kBThreads / cols : 1;
-  const int items = cols * G;
-  constexpr int kB = A <= 2 ? 8 : (A <= 4 ? 4 : 2);  // batches in flight per thread
-  for (int item = tid; item < items; item += kBThreads) {
-    const int q = item % cols, g = item / cols;
-    double sum[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int m0 = g; m0 < M; m0 += G * kB) {
-      v4f v[kB][A];
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        const int m = m0 + u * G < M ? m0 + u * G : M - 1;
-#pragma unroll
-        for (int i = 0; i < A; ++i)
-          v[u][i] = __builtin_amdgcn_raw_buffer_load_b128(rs[i], (m * N + 4 * q) * 4, 0, 16 /* sc1 */);
-      }
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        if (m0 + u * G < M) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float bs = 0.0f;
-#pragma unroll
-            for (int i = 0; i < A; ++i) bs = bs + v[u][i][e] * sc[i];
-            const float diff = Kf - bs * wA;
-            sum[e] += static_cast<double>(df * (diff > 0.0f ? diff : 0.0f));
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) part[g * N + 4 * q + e] = sum[e];
-  }
-  __syncthreads();
-  for (int n = tid; n < N; n += kBThreads) {
-    double t2 = 0.0;
-    for (int g = 0; g < G; ++g) t2 += part[g * N + n];
-    avg[n] = t2 / static_cast<double>(M);
-  }
-  __syncthreads();
-  float2* out = a.targets + b * N;
-  for (int k = tid; k <= N / 2; k += kBThreads) {
-    double re = 0.0, im = 0.0;
-    int idx = 0;
-    for (int n = 0; n < N; ++n) {
-      re = fma(avg[n], cs[idx], re);
-      im = fma(-avg[n], sn[idx], im);
-      idx += k;
-      if (idx >= N) idx -= N;
-    }
-    out[k] = make_float2(static_cast<float>(re), static_cast<float>(im));
-    if (k != 0 && 2 * k != N) out[N - k] = make_float2(static_cast<float>(re), static_cast<float>(-im));
-  }
+  basket_cf<A>(a, b, tot, part, avg, cs, sn);
 }
+
+// One workgroup per contract: the CF phase from the stored terminal rows and terminal sums
+// (a separate pass after basket_kernel<MODE 1>: bit-identical to the fused kernel).
+template <int A>
+__global__ __launch_bounds__(kBThreads) void basket_cf_kernel(BasketArgs a) {
+  extern __shared__ double lds[];
+  const int N = a.N;
+  const int64_t b = blockIdx.x;
+  double* tot = lds;                         // [A]
+  double* part = tot + kMaxAssets;           // [max(4 kBThreads, N)]
+  double* avg = part + (N > 4 * kBThreads ? N : 4 * kBThreads);  // [N]
+  double* cs = avg + N;
+  double* sn = cs + N;
+  for (int j = threadIdx.x; j < N; j += kBThreads) math::twiddle(j, N, sn[j], cs[j]);
+  if (threadIdx.x < A) tot[threadIdx.x] = a.terminal_sum[b * A + threadIdx.x];
+  __syncthreads();
+  basket_cf<A>(a, b, tot, part, avg, cs, sn);
+}
+
 
 size_t basket_lds_bytes(int A, int N) {
   const size_t part = static_cast<size_t>(N > 4 * kBThreads ? N : 4 * kBThreads);
@@ -274,9 +307,21 @@ size_t basket_lds_bytes(int A, int N) {
          sizeof(double);
 }
 
+size_t basket_cf_lds_bytes(int N) {
+  const size_t part = static_cast<size_t>(N > 4 * kBThreads ? N : 4 * kBThreads);
+  return (kMaxAssets + part + 3 * static_cast<size_t>(N)) * sizeof(double);
+}
+
+// Split (basket_kernel<1> then basket_cf_kernel) when the caller keeps the terminal sums: the CF
+// re-read then streams at full read bandwidth instead of stalling each workgroup's store queue
+// (as the single-asset paths_kernel + cf_kernel pair; SMC_BASKET_SPLIT=0 builds keep the fused kernel)
+#ifndef SMC_BASKET_SPLIT
+#define SMC_BASKET_SPLIT 1
+#endif
+
 template <int A, bool HW>
 const void* basket_kernel_ptr() {
-  return reinterpret_cast<const void*>(basket_kernel<A, HW>);
+  return reinterpret_cast<const void*>(basket_kernel<A, HW, SMC_BASKET_SPLIT ? 1 : 0>);
 }
 
 // Workgroups of the kernel launched for <A, HW, N> resident on the current device (occupancy x CUs).
@@ -295,10 +340,10 @@ int64_t basket_slots_k(int N) {
   return static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
 }
 
-template <int A, bool HW>
-int32_t launch_basket_k(const BasketArgs& a, hipStream_t stream) {
+template <int A, bool HW, int MODE>
+int32_t launch_basket_mode(const BasketArgs& a, hipStream_t stream) {
   const size_t lds = basket_lds_bytes(A, a.N);
-  auto kernel = basket_kernel<A, HW>;
+  auto kernel = basket_kernel<A, HW, MODE>;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                           static_cast<int>(lds)) != hipSuccess) {
@@ -307,6 +352,22 @@ int32_t launch_basket_k(const BasketArgs& a, hipStream_t stream) {
   }
   hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(kBThreads), lds, stream, a);
   return check_launch("basket_kernel");
+}
+
+template <int A, bool HW>
+int32_t launch_basket_k(const BasketArgs& a, hipStream_t stream) {
+  if (!SMC_BASKET_SPLIT || !a.terminal_sum) return launch_basket_mode<A, HW, 0>(a, stream);
+  if (int32_t st = launch_basket_mode<A, HW, 1>(a, stream)) return st;
+  const size_t lds = basket_cf_lds_bytes(a.N);
+  auto cf = basket_cf_kernel<A>;
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(cf), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "basket_cf_kernel: cannot raise the dynamic LDS limit");
+  }
+  hipLaunchKernelGGL(cf, dim3(static_cast<unsigned>(a.B)), dim3(kBThreads), lds, stream, a);
+  return check_launch("basket_cf_kernel");
 }
 
 template <bool HW>
