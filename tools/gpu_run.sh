@@ -55,6 +55,8 @@ for step in "$@"; do
     pmc_c5_sq) cd /tmp && run pmc_c5_sq 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_c5_sq" -o run --output-format csv -- python "$ROOT/tools/kprof_basket.py"; cd "$ROOT" ;;
     pmc_c5_write) cd /tmp && run pmc_c5_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_c5_write" -o run --output-format csv -- python "$ROOT/tools/kprof_basket.py"; cd "$ROOT" ;;
     pmc_c5_fetch) cd /tmp && run pmc_c5_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_c5_fetch" -o run --output-format csv -- python "$ROOT/tools/kprof_basket.py"; cd "$ROOT" ;;
+    pmc_c3_write) cd /tmp && run pmc_c3_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_c3_write" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced --B 2048 --N 1024 --M 256 --iters 3; cd "$ROOT" ;;
+    pmc_c3_fetch) cd /tmp && run pmc_c3_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_c3_fetch" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced --B 2048 --N 1024 --M 256 --iters 3; cd "$ROOT" ;;
     pmc_c2_write) cd /tmp && run pmc_c2_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_c2_write" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
     pmc_c2_fetch) cd /tmp && run pmc_c2_fetch 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_c2_fetch" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
     pmc_hw_all)  cd /tmp && run pmc_hw_all 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_hw_all" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
