@@ -164,18 +164,14 @@ __device__ void basket_cf(const BasketArgs& a, int64_t b, const double* tot, dou
   }
 }
 
-// MODE 0: simulate + CF, one workgroup per contract; 1: simulate only (terminal sums out), and
-// persistent: the resident workgroups run contracts blockIdx.x, + gridDim.x, ... back to back.
-// STRAIGHT (T == 16, every row stored): the time loop is unrolled with unconditional row stores.
-template <int A, bool HW, int MODE, bool STRAIGHT = false>
+template <int A, bool HW, int MODE>  // MODE 0: simulate + CF, 1: simulate only (terminal sums out)
 __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kernel(BasketArgs a) {
   typedef float v4f __attribute__((ext_vector_type(4)));
   typedef float f2 __attribute__((ext_vector_type(2)));
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int64_t b = blockIdx.x; b < a.B; b += (MODE == 1 ? gridDim.x : a.B)) {
-  const int T = STRAIGHT ? 16 : a.T, N = a.N;
-  constexpr int kTimeUnroll = STRAIGHT ? 16 : 1;
+  const int64_t b = blockIdx.x;
+  const int T = a.T, N = a.N;
   const int64_t P = a.P;
   double* Ld = lds;                          // [8][8]
   double* wsum = Ld + kMaxAssets * kMaxAssets;  // [kBWaves][A]
@@ -187,7 +183,6 @@ __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kerne
 
   const double* c = a.contracts + b * (3 * A + 4);
   const double Tm = c[1], r = c[2], rho = c[3];
-  if (MODE == 1 && b != blockIdx.x) __syncthreads();  // previous contract's Ld / wsum reads are done
   if (tid == 0) cholesky_equicorr(A, rho, Ld);
   if (MODE == 0)
     for (int j = tid; j < N; j += kBThreads) math::twiddle(j, N, sn[j], cs[j]);
@@ -212,7 +207,7 @@ __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kerne
 
   const uint64_t ordinal = static_cast<uint64_t>((a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0 + b);
   const int64_t pitch = a.pitch;
-  const int64_t rows = STRAIGHT || a.store_all ? T : 1;
+  const int64_t rows = a.store_all ? T : 1;
   float* cbase = a.paths + b * A * rows * pitch;
   const uint32_t lane_off = static_cast<uint32_t>(kBPaths * sizeof(float)) * tid;
   double acc[A];
@@ -226,7 +221,6 @@ __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kerne
     for (int i = 0; i < A; ++i)
 #pragma unroll
       for (int j = 0; j < kBPaths; ++j) x[i][j] = x0[i];
-#pragma unroll kTimeUnroll
     for (int t = 0; t < T; ++t) {
       // path pairs (j, j + 1): draws in path order, then the correlation and the step as packed
       // f32 ops (v_pk_fma_f32 / v_pk_mul_f32; same IEEE results as the scalar ops)
@@ -250,8 +244,8 @@ __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kerne
           x[i][j + 1] = xv.y;
         }
       }
-      if (STRAIGHT || a.store_all || t == T - 1) {
-        const int64_t row = STRAIGHT || a.store_all ? t : 0;
+      if (a.store_all || t == T - 1) {
+        const int64_t row = a.store_all ? t : 0;
 #pragma unroll
         for (int i = 0; i < A; ++i) {
           const v4f v = {x[i][0], x[i][1], x[i][2], x[i][3]};
@@ -282,11 +276,10 @@ __global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kerne
     tot[tid] = sum;
     if (a.terminal_sum) a.terminal_sum[b * A + tid] = sum;
   }
-  if constexpr (MODE == 1) continue;  // basket_cf_kernel takes it from the stored rows and sums
+  if constexpr (MODE == 1) return;  // basket_cf_kernel takes it from the stored rows and sums
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's terminal-row stores
   __syncthreads();
   basket_cf<A>(a, b, tot, part, avg, cs, sn);
-  }
 }
 
 // One workgroup per contract: the CF phase from the stored terminal rows and terminal sums
@@ -328,7 +321,7 @@ size_t basket_cf_lds_bytes(int N) {
 
 template <int A, bool HW>
 const void* basket_kernel_ptr() {
-  return reinterpret_cast<const void*>(basket_kernel<A, HW, SMC_BASKET_SPLIT ? 1 : 0, SMC_BASKET_SPLIT != 0>);
+  return reinterpret_cast<const void*>(basket_kernel<A, HW, SMC_BASKET_SPLIT ? 1 : 0>);
 }
 
 // Workgroups of the kernel launched for <A, HW, N> resident on the current device (occupancy x CUs).
@@ -347,38 +340,24 @@ int64_t basket_slots_k(int N) {
   return static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
 }
 
-template <int A, bool HW, int MODE, bool STRAIGHT>
+template <int A, bool HW, int MODE>
 int32_t launch_basket_mode(const BasketArgs& a, hipStream_t stream) {
   const size_t lds = basket_lds_bytes(A, a.N);
-  auto kernel = basket_kernel<A, HW, MODE, STRAIGHT>;
+  auto kernel = basket_kernel<A, HW, MODE>;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                           static_cast<int>(lds)) != hipSuccess) {
     (void)hipGetLastError();
     return fail(SMC_ERR_HIP, "basket_kernel: cannot raise the dynamic LDS limit");
   }
-  unsigned grid = static_cast<unsigned>(a.B);
-  if (MODE == 1) {  // persistent: one round of resident workgroups
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kernel), kBThreads, lds) !=
-            hipSuccess) {
-      (void)hipGetLastError();
-      return fail(SMC_ERR_HIP, "basket_kernel: occupancy query failed");
-    }
-    const int64_t slots = static_cast<int64_t>(per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
-    if (slots < a.B) grid = static_cast<unsigned>(slots);
-  }
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBThreads), lds, stream, a);
+  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(kBThreads), lds, stream, a);
   return check_launch("basket_kernel");
 }
 
 template <int A, bool HW>
 int32_t launch_basket_k(const BasketArgs& a, hipStream_t stream) {
-  if (!SMC_BASKET_SPLIT || !a.terminal_sum) return launch_basket_mode<A, HW, 0, false>(a, stream);
-  const int32_t st = a.T == 16 && a.store_all ? launch_basket_mode<A, HW, 1, true>(a, stream)
-                                              : launch_basket_mode<A, HW, 1, false>(a, stream);
-  if (st) return st;
+  if (!SMC_BASKET_SPLIT || !a.terminal_sum) return launch_basket_mode<A, HW, 0>(a, stream);
+  if (int32_t st = launch_basket_mode<A, HW, 1>(a, stream)) return st;
   const size_t lds = basket_cf_lds_bytes(a.N);
   auto cf = basket_cf_kernel<A>;
   if (lds > 64 * 1024 &&

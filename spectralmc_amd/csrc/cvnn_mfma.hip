@@ -69,7 +69,6 @@ struct OpBf16 {
   using T = uint16_t;
   using V = bf16x8;
   static constexpr int KB = 32;  // one v_mfma_f32_16x16x32_bf16 per K block
-  static constexpr int BATCH = 8;  // A fragments (K blocks) in flight per tile GEMM batch
   static __device__ __forceinline__ T cvt(float x) { return bf16_bits(x); }
   static __device__ __forceinline__ V ld(const T* p) { return *reinterpret_cast<const V*>(p); }
   static __device__ __forceinline__ f32x4 mmav(f32x4 acc, V a, V b) {
@@ -89,7 +88,6 @@ struct OpF32 {
   using T = float;
   using V = f32x4;
   static constexpr int KB = 16;  // four v_mfma_f32_16x16x4_f32 per K block
-  static constexpr int BATCH = 4;  // A fragments (K blocks) in flight per tile GEMM batch
   static __device__ __forceinline__ T cvt(float x) { return x; }
   static __device__ __forceinline__ V ld(const T* p) { return *reinterpret_cast<const V*>(p); }
   static __device__ __forceinline__ f32x4 mmav(f32x4 acc, V a, V b) {
@@ -230,26 +228,20 @@ __device__ __forceinline__ float col_sum16(float x) {
 
 // ---- tile GEMM: acc[rt] += A[16 rows at ap][k0, k1) . B[k0, k1)[16 columns of row tile rt at bp] ----
 // ap: this lane's A row (+ g KQ), from global memory (L2); bp: this lane's B row (+ g KQ) of row
-// tile 0 in LDS, row tiles ldb * 16 elements apart.  A fragments come in batches of up to 8 K
-// blocks (their L2 latencies overlap); the first batch is loaded by the caller ahead of time
-// (load_batch), so it is in flight across the previous tile's epilogue or the previous layer's
-// barrier.
-template <class Op>
-__device__ __forceinline__ void load_batch(typename Op::V* av, const typename Op::T* ap, int k0, int k1) {
-  constexpr int KB = Op::KB;
-#pragma unroll
-  for (int i = 0; i < Op::BATCH; ++i)
-    if (k0 + i * KB < k1) av[i] = Op::ld(ap + k0 + i * KB);
-}
-
+// tile 0 in LDS, row tiles ldb * 16 elements apart.  The A fragments of up to 8 K blocks are loaded
+// before their MFMAs, so their L2 latencies overlap.
 template <class Op, int RT>
-__device__ __forceinline__ void tile_gemm(f32x4* acc, typename Op::V* av, const typename Op::T* ap,
-                                          const typename Op::T* bp, int ldb, int k0, int k1) {
+__device__ __forceinline__ void tile_gemm(f32x4* acc, const typename Op::T* ap, const typename Op::T* bp, int ldb,
+                                          int k0, int k1) {
+  using V = typename Op::V;
   constexpr int KB = Op::KB;
-  for (int kb0 = k0; kb0 < k1; kb0 += Op::BATCH * KB) {
-    if (kb0 != k0) load_batch<Op>(av, ap, kb0, k1);
+  for (int kb0 = k0; kb0 < k1; kb0 += 8 * KB) {
+    V av[8];
 #pragma unroll
-    for (int i = 0; i < Op::BATCH; ++i) {
+    for (int i = 0; i < 8; ++i)
+      if (kb0 + i * KB < k1) av[i] = Op::ld(ap + kb0 + i * KB);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
       if (kb0 + i * KB < k1) {
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) acc[rt] = Op::mmav(acc[rt], av[i], Op::ld(bp + rt * 16 * ldb + kb0 + i * KB));
@@ -258,7 +250,7 @@ __device__ __forceinline__ void tile_gemm(f32x4* acc, typename Op::V* av, const 
   }
 }
 
-constexpr int kFbThreads = 512;
+constexpr int kFbThreads = 1024;
 constexpr int kFbWaves = kFbThreads / 64;
 
 // K split of a layer GEMM with `ntile` output tiles: waves take (tile, K part) items when the
@@ -269,48 +261,20 @@ __host__ __device__ inline int k_split(int ntile, int kdim, int kb) {
   return ks;
 }
 
-// The A operand of one layer GEMM: `ntile` output tiles of 16 rows, K = kdim, rows lda apart.
-template <class Op>
-struct Gemm {
-  int ntile, kdim;
-  const typename Op::T* a0;
-  int lda;
-};
-
-// This wave's first A batch of g (its first work item), into av; g.ntile == 0: nothing follows.
-template <class Op>
-__device__ __forceinline__ void prefetch_first(const Gemm<Op>& gm, typename Op::V* av) {
-  const Gemm<Op>* g = &gm;
-  constexpr int KQ = Op::KB / 4;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, gq = lane >> 4, c = lane & 15;
-  const int ks = k_split(g->ntile, g->kdim, Op::KB);
-  const int t = ks == 1 ? wave : wave / ks;
-  if (t >= g->ntile) return;
-  const int kc = g->kdim / ks, k0 = ks == 1 ? 0 : (wave % ks) * kc;
-  load_batch<Op>(av, g->a0 + static_cast<int64_t>(t * 16 + c) * g->lda + gq * KQ, k0, k0 + kc);
-}
-
-// All output tiles of one layer GEMM, then epi(tile, acc) for each; called by every wave.  av holds
-// this wave's first A batch of `cur` on entry and of `next` on exit.
+// All output tiles of one layer GEMM, then epi(tile, acc) for each; called by every wave.
 template <class Op, int RT, class Epi>
-__device__ __forceinline__ void layer_gemm(const Gemm<Op>& cur, const Gemm<Op>& next, typename Op::V* av,
+__device__ __forceinline__ void layer_gemm(int ntile, int kdim, const typename Op::T* a0, int lda,
                                            const typename Op::T* b0, int ldb, f32x4* scratch, Epi&& epi) {
   constexpr int KQ = Op::KB / 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
-  const int ntile = cur.ntile, kdim = cur.kdim;
-  auto arow = [&](int t) { return cur.a0 + static_cast<int64_t>(t * 16 + c) * cur.lda + g * KQ; };
   const int ks = k_split(ntile, kdim, Op::KB);
   if (ks == 1) {
-    if (wave >= ntile) prefetch_first<Op>(next, av);
     for (int t = wave; t < ntile; t += kFbWaves) {
       f32x4 acc[RT];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) acc[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      tile_gemm<Op, RT>(acc, av, arow(t), b0 + c * ldb + g * KQ, ldb, 0, kdim);
-      if (t + kFbWaves < ntile)
-        load_batch<Op>(av, arow(t + kFbWaves), 0, kdim);
-      else
-        prefetch_first<Op>(next, av);
+      tile_gemm<Op, RT>(acc, a0 + static_cast<int64_t>(t * 16 + c) * lda + g * KQ, b0 + c * ldb + g * KQ, ldb, 0,
+                        kdim);
       epi(t, acc);
     }
     return;
@@ -321,13 +285,13 @@ __device__ __forceinline__ void layer_gemm(const Gemm<Op>& cur, const Gemm<Op>& 
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) acc[rt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   if (t < ntile) {
-    tile_gemm<Op, RT>(acc, av, arow(t), b0 + c * ldb + g * KQ, ldb, part * kc, part * kc + kc);
+    tile_gemm<Op, RT>(acc, a0 + static_cast<int64_t>(t * 16 + c) * lda + g * KQ, b0 + c * ldb + g * KQ, ldb,
+                      part * kc, part * kc + kc);
     if (part > 0) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) scratch[(wave * RT + rt) * 64 + lane] = acc[rt];
     }
   }
-  prefetch_first<Op>(next, av);
   __syncthreads();
   if (t < ntile && part == 0) {
     for (int p = 1; p < ks; ++p) {
@@ -358,18 +322,12 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
   const int64_t bp = a.bp;
   T* ws = static_cast<T*>(a.opws);
   f32x4* scratch = reinterpret_cast<f32x4*>(net_lds);  // [kFbWaves][RT][64] split-K partials
-  T* const z0 = reinterpret_cast<T*>(net_lds + kFbWaves * RT * 64 * sizeof(f32x4));
-  T* const z1 = z0 + R * a.zs;  // activation / gradient ping-pong buffers (selected, never indexed)
-  T* gb = z1 + R * a.zs;
+  T* zbuf[2];
+  zbuf[0] = reinterpret_cast<T*>(net_lds + kFbWaves * RT * 64 * sizeof(f32x4));
+  zbuf[1] = zbuf[0] + R * a.zs;
+  T* gb = zbuf[1] + R * a.zs;
   float* pre_lds = reinterpret_cast<float*>(gb + R * a.gs);  // 16-byte aligned: R * gs * sizeof(T) is
   const float* P = a.params;
-
-  // this wave's first A batch of the next layer GEMM, in flight ahead of its barrier
-  typename Op::V av[Op::BATCH];
-  {
-    const Gemm<Op> g0{layer[0].wout / 16, layer[0].win, ws + layer[0].wc, layer[0].win};
-    prefetch_first<Op>(g0, av);
-  }
 
   // ---- layer-0 input: Z_0 (interleaved re, im) into LDS and Z_0^T (+ ones row) into the workspace
   {
@@ -382,7 +340,7 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
     };
     for (int i = tid; i < R * l0.win; i += kFbThreads) {
       const int r = i / l0.win, k = i - r * l0.win;
-      z0[r * a.zs + k] = Op::cvt(in(r0 + r, k));
+      zbuf[0][r * a.zs + k] = Op::cvt(in(r0 + r, k));
     }
     for (int i = tid; i < l0.kx * R; i += kFbThreads) {
       const int k = i / R, r = i - k * R;
@@ -396,11 +354,8 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
   for (int l = 0; l + 1 < L; ++l) {
     const MLayer& ly = layer[l];
     const MLayer& nx = layer[l + 1];
-    T* zout = cur ? z0 : z1;
-    const T* zin = cur ? z1 : z0;
-    const Gemm<Op> gc{ly.wout / 16, ly.win, ws + ly.wc, ly.win};
-    const Gemm<Op> gn{nx.wout / 16, nx.win, ws + nx.wc, nx.win};
-    layer_gemm<Op, RT>(gc, gn, av, zin, a.zs, scratch, [&](int ft, f32x4* acc) {
+    T* zout = zbuf[cur ^ 1];
+    layer_gemm<Op, RT>(ly.wout / 16, ly.win, ws + ly.wc, ly.win, zbuf[cur], a.zs, scratch, [&](int ft, f32x4* acc) {
       const int f0 = ft * 16 + 4 * g;
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
@@ -443,9 +398,7 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
   {
     const MLayer& ly = layer[L - 1];
     const int N = ly.no;
-    const Gemm<Op> gc{ly.wout / 16, ly.win, ws + ly.wc, ly.win};
-    const Gemm<Op> gn{L > 1 ? ly.win / 16 : 0, ly.wout, ws + ly.wct, ly.wout};  // the first input-gradient GEMM
-    layer_gemm<Op, RT>(gc, gn, av, cur ? z1 : z0, a.zs, scratch, [&](int ft, f32x4* acc) {
+    layer_gemm<Op, RT>(ly.wout / 16, ly.win, ws + ly.wc, ly.win, zbuf[cur], a.zs, scratch, [&](int ft, f32x4* acc) {
       const int f0 = ft * 16 + 4 * g;
       float dcs[2] = {0.0f, 0.0f};
 #pragma unroll
@@ -504,10 +457,8 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
   for (int l = L - 1; l >= 1; --l) {
     const MLayer& ly = layer[l];
     const MLayer& lp = layer[l - 1];
-    T* gdst = dst ? z1 : z0;
-    const Gemm<Op> gc{ly.win / 16, ly.wout, ws + ly.wct, ly.wout};
-    const Gemm<Op> gn{l > 1 ? lp.win / 16 : 0, lp.wout, ws + lp.wct, lp.wout};
-    layer_gemm<Op, RT>(gc, gn, av, gsrc, gstride, scratch, [&](int it, f32x4* acc) {
+    T* gdst = zbuf[dst];
+    layer_gemm<Op, RT>(ly.win / 16, ly.wout, ws + ly.wct, ly.wout, gsrc, gstride, scratch, [&](int it, f32x4* acc) {
       const int f0 = it * 16 + 4 * g;
       float dcs[2] = {0.0f, 0.0f};
 #pragma unroll
