@@ -819,6 +819,10 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     const double w = wave_sum(acc[0]);
     if (lane == 0) wsum[wave] = w;
     lds_barrier();
+#if defined(SMC_RESIDENT_NO_CF)  // tools/micro decomposition builds only: no payoff / M-mean / FFT
+    lds_barrier();
+    continue;
+#endif
     double tot = 0.0;
     for (int k = 0; k < kResWaves; ++k) tot += wsum[k];
     const Payoff<float> pay(a, c, tot);

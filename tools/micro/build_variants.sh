@@ -9,7 +9,7 @@ for spec in "$@"; do
   flags=${spec#*:}
   [ "$flags" = "$spec" ] && flags=""
   mkdir -p "build/v_$name"
-  for src in capi sobol gbm cvnn basket; do
+  for src in capi sobol gbm cvnn cvnn_mfma basket; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -munsafe-fp-atomics \
       $flags -c $src.hip -o "build/v_$name/$src.o" &
   done
