@@ -264,7 +264,12 @@ def main() -> None:
         b = eng.buffers
 
         def run_kernel() -> None:
-            eng.launch_targets(_lib.stream_handle(stream), None, 0)
+            # the launch(es) the training step makes: smc_train_step (Sobol draw, targets and cursor
+            # update fused into the resident kernel) where the engine uses it, else the targets call
+            if getattr(eng, "_uses_train_step", False):
+                eng.enqueue_step()
+            else:
+                eng.launch_targets(_lib.stream_handle(stream), None, 0)
 
         run_kernel()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

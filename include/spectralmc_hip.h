@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 7
+#define SMC_ABI_VERSION 8
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -133,19 +133,32 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
 /* One Monte-Carlo step of the training loop (sobol_sampler.py:222-246 + gbm_trainer.py:1546-1556):
  * the Sobol draw of the step's contracts (point i = sequence index cursor_dev[0] + index_offset + i,
  * scaled as smc_sobol_draw, into contracts_dev [B][6] f64 and cvnn_input_dev [B][6] f32 or NULL),
- * the targets exactly as smc_train_targets with ordinal_dev = cursor_dev + 1, ordinal0 = index_offset
- * (no row sums, no workspace), then cursor_dev[0..1] += advance.  Where the resident kernel takes
- * the shape (f32, T = 16, P <= 65,536, one chunk) all of it is ONE launch: each workgroup draws the
- * rows of its own contracts and the last workgroup to finish advances the cursor, counting arrivals
- * in counter_dev (one u32, zero-filled before the first call; the call leaves it zero).  Other
- * shapes run the three steps as separate launches.  Results are bit-identical either way. */
+ * the targets with ordinal_dev = cursor_dev + 1, ordinal0 = index_offset, then
+ * cursor_dev[0..1] += advance.  Where the resident kernel takes the shape (f32, T = 16, P a
+ * multiple of 4096 up to 8 x 65,536, N | 4096) each chunk of contracts is ONE launch: each
+ * workgroup draws the rows of its own contracts and the last workgroup of the last chunk advances
+ * the cursor.  P <= 65,536: one workgroup per contract, targets bit-identical to
+ * smc_sobol_draw + smc_train_targets (no workspace) + the cursor update.  P > 65,536 (C3): W =
+ * P / 65,536 co-resident workgroups per contract exchange their terminal and column sums through
+ * the sync area; the f64 sums are added in slice order (oracle kernel mode, slices = W).  Other
+ * shapes run the three steps as separate launches, bit-identical to the separate calls.
+ * sync_dev: smc_train_step_sync_bytes(...) bytes, zero-filled before the first call (every call
+ * leaves it zeroed). */
 int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const double* lower_dev,
                        const double* upper_dev, int64_t* cursor_dev, int64_t index_offset, int64_t advance,
                        double* contracts_dev, float* cvnn_input_dev, int64_t n_contracts, int32_t timesteps,
                        int32_t network_size, int32_t batches_per_mc_run, uint64_t mc_seed, int32_t scheme,
                        int32_t normalization, int32_t dtype, int32_t store_mode, void* paths_dev,
-                       int64_t path_pitch, int64_t chunk_contracts, void* targets_dev, uint32_t* counter_dev,
-                       void* stream);
+                       int64_t path_pitch, int64_t chunk_contracts, void* targets_dev, void* sync_dev,
+                       int64_t sync_bytes, void* stream);
+/* Bytes of smc_train_step's sync area for this shape on the current device (4 for whole-contract
+ * shapes; -1 if the device query fails). */
+int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
+                                  int32_t dtype, int64_t path_pitch);
+/* Name of the kernel smc_train_step launches for this shape ("resident_kernel",
+ * "resident_kernel(sliced)", or smc_train_targets_kernel's name).  Static string. */
+const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
+                                  int32_t dtype, int64_t path_pitch);
 /* Workspace bytes smc_train_targets needs for sliced contracts (0: P too small to slice). */
 int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, int64_t n_paths,
                                    int32_t all_rows);

@@ -467,9 +467,15 @@ static void fft_real(const double* avg, const double* cs, const double* sn, int 
 }
 
 /* targets: [B][N] interleaved complex64 (re, im) */
+/* slices: workgroups per contract of the sliced resident_kernel (gbm.hip, smc_train_step with
+ * P > 65,536): slice s holds batch rows [s M/slices, (s+1) M/slices); its items sum only those rows,
+ * its column sums add the G groups in order from 0.0, and the M-mean adds the slices' column sums
+ * in slice order from 0.0.  slices = 1 is the whole-contract order (0.0 + x == x). */
 void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, int32_t normalize, int32_t wg,
-                      const float* terminal, const double* terminal_sum, float* targets) {
+                      int32_t slices, const float* terminal, const double* terminal_sum, float* targets) {
   const int lanes = wg > 0 ? wg : K_THREADS;  /* G = lanes / column quads (resident_kernel: 4096 / N) */
+  const int W = slices > 1 ? slices : 1;
+  const int Ms = M / W;
   const int64_t P = (int64_t)N * M;
   /* gbm.hip cf_targets_contract: with N % 4 == 0 a thread owns 4 adjacent columns (16-B loads),
    * so the m-groups per column are counted over N/4 column quads */
@@ -491,22 +497,27 @@ void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, 
     const float s = normalize ? F / (float)(terminal_sum[b] / (double)P) : 1.0f;
     const float K = (float)c[1];
     const float* row = terminal + b * P;
-    for (int item = 0; item < items; ++item) {
-      const int n = item % N, g = item / N;
-      double sum = 0.0;
-      for (int m = g; m < M; m += G) {
-        const float xs = row[(int64_t)m * N + n] * s;
-        const float diff = K - xs;
-        const float pay = df * (diff > 0.0f ? diff : 0.0f);
-        sum += (double)pay;
+    for (int n = 0; n < N; ++n) avg[n] = 0.0;
+    for (int sl = 0; sl < W; ++sl) {
+      const int m0 = sl * Ms, m1 = sl + 1 == W ? M : (sl + 1) * Ms;
+      for (int item = 0; item < items; ++item) {
+        const int n = item % N, g = item / N;
+        double sum = 0.0;
+        for (int m = m0 + g; m < m1; m += G) {
+          const float xs = row[(int64_t)m * N + n] * s;
+          const float diff = K - xs;
+          const float pay = df * (diff > 0.0f ? diff : 0.0f);
+          sum += (double)pay;
+        }
+        part[item] = sum;
       }
-      part[item] = sum;
+      for (int n = 0; n < N; ++n) {
+        double col = 0.0;
+        for (int g = 0; g < G; ++g) col += part[g * N + n];
+        avg[n] += col; /* slices in order from 0.0 */
+      }
     }
-    for (int n = 0; n < N; ++n) {
-      double tot = 0.0;
-      for (int g = 0; g < G; ++g) tot += part[g * N + n];
-      avg[n] = tot / (double)M;
-    }
+    for (int n = 0; n < N; ++n) avg[n] = avg[n] / (double)M;
     float* out = targets + 2 * b * N;
     if (use_fft(N)) {
       fft_real(avg, cs, sn, N, xr, xi);

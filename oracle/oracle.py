@@ -63,8 +63,8 @@ def lib() -> ctypes.CDLL:
                                           ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_kernel_cf.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
-                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
-                                       ctypes.c_void_p]
+                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_basket_kernel.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64,
                                            ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -200,28 +200,30 @@ SLICE_PATHS = 8192
 
 def kernel_paths(contracts: np.ndarray, timesteps: int, n_paths: int, seed: int, ordinal0: int = 0,
                  scheme: int = 0, want_paths: bool = False, sliced: bool = False,
-                 wg: int = 512) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
+                 wg: int = 512, slices: int = 1) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
     """f32 KERNEL mode: exact restatement of the HIP engine (paths, terminal, rowsum in its order).
     sliced: row sums in the sliced-contract order (engine with a workspace); wg: lanes of the
-    engine workgroup whose reduction order to follow (1024 = resident_kernel)."""
+    engine workgroup whose reduction order to follow (1024 = resident_kernel); slices: workgroups
+    per contract of the sliced resident_kernel (slices of n_paths / slices paths, added in order)."""
     contracts = np.ascontiguousarray(contracts, dtype=np.float64)
     B = contracts.shape[0]
     paths = np.empty((B, timesteps, n_paths), dtype=np.float32) if want_paths else None
     terminal = np.empty((B, n_paths), dtype=np.float32)
     rowsum = np.empty((B, timesteps), dtype=np.float64)
+    span = SLICE_PATHS if sliced else (n_paths // slices if slices > 1 else 0)
     lib().oracle_kernel_paths(_ptr(contracts), B, timesteps, n_paths, seed, ordinal0, scheme,
-                              SLICE_PATHS if sliced else 0, wg, _ptr(paths), _ptr(terminal), _ptr(rowsum))
+                              span, wg, _ptr(paths), _ptr(terminal), _ptr(rowsum))
     return paths, terminal, rowsum
 
 
 def kernel_cf(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndarray, network_size: int,
-              batches: int, normalize: bool = True, wg: int = 512) -> np.ndarray:
+              batches: int, normalize: bool = True, wg: int = 512, slices: int = 1) -> np.ndarray:
     contracts = np.ascontiguousarray(contracts, dtype=np.float64)
     terminal = np.ascontiguousarray(terminal, dtype=np.float32)
     terminal_sum = np.ascontiguousarray(terminal_sum, dtype=np.float64)
     out = np.empty((contracts.shape[0], network_size), dtype=np.complex64)
     lib().oracle_kernel_cf(_ptr(contracts), contracts.shape[0], network_size, batches, int(normalize), wg,
-                           _ptr(terminal), _ptr(terminal_sum), _ptr(out))
+                           slices, _ptr(terminal), _ptr(terminal_sum), _ptr(out))
     return out
 
 
@@ -236,14 +238,28 @@ def engine_wg(timesteps: int, network_size: int, n_paths: int, with_rowsum: bool
     return 1024 if ok else 512
 
 
+def train_step_order(timesteps: int, network_size: int, n_paths: int) -> tuple[int, int]:
+    """(wg, slices) of the f32 resident launch smc_train_step makes for this shape (gbm.hip
+    resident_slices / resident_ok: W = the fewest power-of-two slices of <= 65,536 paths, W <= 8),
+    or (engine_wg(...), 1) where it falls back to the separate draw + smc_train_targets calls."""
+    N, P = network_size, n_paths
+    W = 1
+    while W < 8 and P > W * 65536:
+        W *= 2
+    ok = (timesteps == 16 and P % (W * 4096) == 0 and P // (W * 4096) <= 16 and 4 <= N <= 1024
+          and 4096 % N == 0)
+    return (1024, W) if ok else (engine_wg(timesteps, N, P), 1)
+
+
 def kernel_targets(contracts: np.ndarray, timesteps: int, network_size: int, batches: int, seed: int,
                    ordinal0: int = 0, scheme: int = 0, normalize: bool = True,
-                   sliced: bool = False, wg: int = 512) -> tuple[np.ndarray, np.ndarray]:
+                   sliced: bool = False, wg: int = 512, slices: int = 1) -> tuple[np.ndarray, np.ndarray]:
     """(targets [B,N] complex64, rowsum [B,T]) exactly as the f32 HIP engine computes them
-    (wg: engine_wg(...) of the launch)."""
+    (wg: engine_wg(...) of the launch; slices: train_step_order(...) for smc_train_step)."""
     _, terminal, rowsum = kernel_paths(contracts, timesteps, network_size * batches, seed, ordinal0, scheme,
-                                       sliced=sliced, wg=wg)
-    return kernel_cf(contracts, terminal, rowsum[:, -1], network_size, batches, normalize, wg=wg), rowsum
+                                       sliced=sliced, wg=wg, slices=slices)
+    return kernel_cf(contracts, terminal, rowsum[:, -1], network_size, batches, normalize, wg=wg,
+                     slices=slices), rowsum
 
 
 # --------------------------------------------------------------------------- basket (extension)

@@ -34,7 +34,7 @@ STORE_TERMINAL = 1
 MATH_HW = 0x100
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 
@@ -59,7 +59,9 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
                                    _c_vp]),
     "smc_train_step": (_c_i32, [_c_vp, _c_i32, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_i64, _c_i32, _c_i32,
                                 _c_i32, _c_u64, _c_i32, _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp,
-                                _c_vp]),
+                                _c_i64, _c_vp]),
+    "smc_train_step_sync_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i64]),
+    "smc_train_step_kernel": (ctypes.c_char_p, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i64]),
     "smc_engine_workspace_bytes": (_c_i64, [_c_i64, _c_i32, _c_i64, _c_i32]),
     "smc_train_targets_kernel": (ctypes.c_char_p, [_c_i32, _c_i32, _c_i64, _c_i32, _c_i64, _c_i32]),
     "smc_path_pitch": (_c_i64, [_c_i64, _c_i32]),

@@ -88,6 +88,14 @@ struct EngineArgs {
   int64_t sobol_index0;       // Sobol index offset of contract 0 of this launch (rank * B)
   int64_t advance;            // cursor[0..1] += advance after the launch
   uint32_t* done;             // workgroups finished, zero between launches
+  // sliced resident_kernel (smc_train_step, P > 65,536): res_slices workgroups per contract
+  // exchange their terminal sums and column sums through the sync area (res_slices <= 1: whole
+  // contracts, none of these are read)
+  int32_t res_slices;
+  int32_t res_groups;         // capacity of the sync area in groups
+  uint32_t* res_cnt;          // [groups][64]: terminal-sum arrivals at +0, column-sum arrivals at +32
+  double* res_xsum;           // [groups][2][W] slice terminal sums (2: contract round parity)
+  double* res_xcol;           // [groups][2][W][N] slice column sums of the put payoffs
 };
 
 #ifndef SMC_SLICE_CHUNKS
@@ -744,6 +752,16 @@ __global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
 // workgroup per CU runs contracts blockIdx.x, + gridDim.x, ...  Reduction orders follow 1024
 // lanes (oracle kernel mode, wg = 1024): lane over chunks, wave butterfly, waves 0..15 for the
 // terminal sum; item sums in ascending m, groups in order.
+//
+// Sliced (res_slices = W > 1, smc_train_step only; C3: P = 262,144, W = 4): a group of W
+// co-resident workgroups (on one XCD where the grid allows) runs each contract, slice s holding
+// paths [s P/W, (s+1) P/W) on chip.  The slices publish their terminal sums, wait for all W
+// (the exchange every payoff needs) and add them in slice order; each then publishes its column
+// sums, and the last to arrive adds the W of them in slice order, takes the M-mean and runs the
+// FFT.  Hand-offs: write-through (sc1) stores by one wave, drained, then an agent-scope add on
+// the group's counter; sc1 loads after the poll matched or the add returned
+// (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms, first table row).  Counters
+// are monotonic within a launch (W per contract round) and reset by the last workgroup.
 constexpr int kResThreads = 1024;
 constexpr int kResWaves = kResThreads / 64;
 constexpr int kResChunk = kResThreads * kPathsPerLane;  // 4096 paths
@@ -751,6 +769,8 @@ constexpr int kResMaxChunks = 16;
 constexpr int kResLdsChunks = 8;                        // chunks parked in LDS
 constexpr int kResRegChunks = kResMaxChunks - kResLdsChunks;
 constexpr size_t kResTermBytes = static_cast<size_t>(kResLdsChunks) * kResThreads * 16;  // 128 KiB
+constexpr int kResMaxSlices = 8;
+constexpr uint32_t kResSpinLimit = 1u << 20;  // ~1 s of polling: a partner that never arrives gives NaN targets
 
 size_t resident_lds_bytes(int N) {
   return kResTermBytes + (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 8) * sizeof(double);
@@ -764,7 +784,20 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   const int N = a.N, M = a.M;
   const int64_t P = a.P;
   const int64_t pitch = a.pitch ? a.pitch : P;
-  const int nch = static_cast<int>(P / kResChunk);
+  const int W = a.res_slices > 1 ? a.res_slices : 1;
+  // group (contract sequence) and slice of this workgroup: blocks b, b + 8, ... share an XCD
+  int grp = blockIdx.x, slc = 0;
+  if (W > 1) {
+    if (gridDim.x % (8 * W) == 0) {
+      slc = static_cast<int>((blockIdx.x >> 3) % W);
+      grp = static_cast<int>((blockIdx.x & 7) + 8 * (blockIdx.x / (8 * W)));
+    } else {
+      slc = static_cast<int>(blockIdx.x % W);
+      grp = static_cast<int>(blockIdx.x / W);
+    }
+  }
+  const int groups = static_cast<int>(gridDim.x) / W;
+  const int nch = static_cast<int>(P / (static_cast<int64_t>(W) * kResChunk));  // chunks of this slice
   const int cols = N / 4;
   const int G = kResChunk / N;            // batch rows per chunk
   const int q = tid % cols, g = tid / cols;
@@ -775,18 +808,22 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   double* avg = wsum + kResWaves;         // [N]
   double* cs = avg + N;                   // [N]
   double* sn = cs + N;                    // [N]
-  double* row = sn + N;                   // [6] this contract's drawn Sobol row (fused step)
+  double* row = sn + N;                   // [6] this contract's drawn Sobol row (fused step); [6]
+                                          // the exchanged terminal sum, [7] the last-arriver flag
   for (int j = tid; j < N; j += kResThreads) math::twiddle(j, N, sn[j], cs[j]);
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
   const int64_t sob0 = a.sobol ? a.cursor[0] + a.sobol_index0 : 0;
-  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+  uint32_t round = 0;
+  for (int64_t b = grp; b < a.B; b += groups, ++round) {
     Contract c;
     if (a.sobol) {  // draw the contract (sobol_sampler.py:222-246) instead of a separate kernel
       if (tid < 6) {
         const double v = sobol_coord(a.sobol, a.sobol_dim, tid, static_cast<uint64_t>(sob0 + b), a.lower, a.upper);
         row[tid] = v;
-        a.contracts_out[b * 6 + tid] = v;
-        if (a.cvnn_out) a.cvnn_out[b * 6 + tid] = static_cast<float>(v);
+        if (slc == 0) {
+          a.contracts_out[b * 6 + tid] = v;
+          if (a.cvnn_out) a.cvnn_out[b * 6 + tid] = static_cast<float>(v);
+        }
       }
       lds_barrier();
       c = Contract{row[0], row[1], row[2], row[3], row[4], row[5]};
@@ -796,6 +833,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     const Stepper<float, LOG_EULER, HW> step(c, kRowBlock);
     const float x0 = static_cast<float>(c.X0);
     float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * kRowBlock * pitch : b * pitch);
+    const int64_t p0 = static_cast<int64_t>(slc) * nch * kResChunk;  // first path of this slice
     // chunks >= kResLdsChunks: a shift register with static indices (a rolled loop indexing a
     // register array would put it in scratch memory); chunk ch ends in slot ch - nch + kResRegChunks
     float term[kResRegChunks][kPathsPerLane];
@@ -803,7 +841,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     for (int ch = 0; ch < nch; ++ch) {
       float xt[kPathsPerLane];
       lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(
-          a, step, x0, static_cast<uint64_t>(ord0 + b), static_cast<int64_t>(ch) * kResChunk, kPathsPerLane, 0,
+          a, step, x0, static_cast<uint64_t>(ord0 + b), p0 + static_cast<int64_t>(ch) * kResChunk, kPathsPerLane, 0,
           kRowBlock, base, acc, xt);
       if (ch < kResLdsChunks) {
         term_lds[ch * kResThreads + tid] = v4f{xt[0], xt[1], xt[2], xt[3]};
@@ -825,6 +863,24 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
 #endif
     double tot = 0.0;
     for (int k = 0; k < kResWaves; ++k) tot += wsum[k];
+    const int64_t xslot = (static_cast<int64_t>(grp) * 2 + (round & 1)) * W;  // this round's [W] slots
+    if (W > 1) {
+      // terminal-sum exchange: publish, arrive, wait for the W slices, add them in slice order
+      if (tid == 0) {
+        put_sc1(a.res_xsum + xslot + slc, tot);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t* cnt = a.res_cnt + static_cast<int64_t>(grp) * 64;
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t want = static_cast<uint32_t>(W) * (round + 1);
+        uint32_t spins = 0;
+        while (get_sc1(cnt) < want && ++spins < kResSpinLimit) __builtin_amdgcn_s_sleep(2);
+        double t = 0.0;
+        for (int j = 0; j < W; ++j) t += get_sc1(a.res_xsum + xslot + j);
+        row[6] = spins < kResSpinLimit ? t : __builtin_nan("");
+      }
+      lds_barrier();
+      tot = row[6];
+    }
     const Payoff<float> pay(a, c, tot);
     double colsum[kPathsPerLane] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -846,30 +902,93 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
 #pragma unroll
     for (int j = 0; j < kPathsPerLane; ++j) part[g * N + 4 * q + j] = colsum[j];
     lds_barrier();
-    for (int n = tid; n < N; n += kResThreads) {
-      double t = 0.0;
-      for (int gg = 0; gg < G; ++gg) t += part[gg * N + n];
-      avg[n] = t / static_cast<double>(M);
+    if (W == 1) {
+      for (int n = tid; n < N; n += kResThreads) {
+        double t = 0.0;
+        for (int gg = 0; gg < G; ++gg) t += part[gg * N + n];
+        avg[n] = t / static_cast<double>(M);
+      }
+    } else {
+      // column-sum exchange: the slice's G group sums per column, published by wave 0; the last
+      // slice to arrive adds the W column sums in slice order and runs the FFT
+      for (int n = tid; n < N; n += kResThreads) {
+        double t = 0.0;
+        for (int gg = 0; gg < G; ++gg) t += part[gg * N + n];
+        avg[n] = t;
+      }
+      lds_barrier();
+      double* xcol = a.res_xcol + xslot * N;
+      if (wave == 0) {
+        for (int n = lane; n < N; n += 64) put_sc1(xcol + static_cast<int64_t>(slc) * N + n, avg[n]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+          const uint32_t before = __hip_atomic_fetch_add(a.res_cnt + static_cast<int64_t>(grp) * 64 + 32, 1u,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          reinterpret_cast<int*>(row + 7)[0] = before == static_cast<uint32_t>(W) * (round + 1) - 1;
+        }
+      }
+      lds_barrier();
+      if (!reinterpret_cast<const int*>(row + 7)[0]) continue;  // uniform: another slice runs the FFT
+      for (int n = tid; n < N; n += kResThreads) {
+        double t = 0.0;
+        for (int j = 0; j < W; ++j) t += get_sc1(xcol + static_cast<int64_t>(j) * N + n);
+        avg[n] = t / static_cast<double>(M);
+      }
     }
     lds_barrier();
     fft_row<float, kResThreads, true>(avg, cs, sn, N, part, part + N, static_cast<float2*>(a.targets) + b * N);
     lds_barrier();  // part (= term_lds) / avg / wsum / row are reused by the next contract
   }
   if (a.done && tid == 0) {
-    // every workgroup read the cursor before it arrives here: the last one advances it
+    // every workgroup read the cursor (and made its last exchange) before it arrives here: the last
+    // one advances the cursor and resets the exchange counters
     __threadfence();
     if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
       a.cursor[0] += a.advance;
       a.cursor[1] += a.advance;
+      if (W > 1)
+        for (int k = 0; k < groups; ++k) {
+          a.res_cnt[static_cast<int64_t>(k) * 64] = 0u;
+          a.res_cnt[static_cast<int64_t>(k) * 64 + 32] = 0u;
+        }
       *a.done = 0u;
     }
   }
 }
 
 bool resident_ok(const EngineArgs& a, bool f32) {
+  const int64_t W = a.res_slices > 1 ? a.res_slices : 1;
   return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T == kRowBlock &&
-         a.P % kResChunk == 0 && a.P / kResChunk <= kResMaxChunks && a.N >= 4 && a.N <= 1024 &&
-         kResChunk % a.N == 0 && (a.pitch == 0 || a.pitch % 4 == 0);
+         W <= kResMaxSlices && a.P % (W * kResChunk) == 0 && a.P / (W * kResChunk) <= kResMaxChunks &&
+         a.N >= 4 && a.N <= 1024 && kResChunk % a.N == 0 && (a.pitch == 0 || a.pitch % 4 == 0) &&
+         (W == 1 || (a.res_cnt && a.res_xsum && a.res_xcol && a.done));
+}
+
+// Workgroups per contract of the resident kernel in smc_train_step: the fewest (a power of two
+// <= kResMaxSlices) whose slices hold <= 65,536 paths each.
+int32_t resident_slices(int64_t P) {
+  int32_t W = 1;
+  while (W < kResMaxSlices && P > static_cast<int64_t>(W) * kResMaxChunks * kResChunk) W *= 2;
+  return W;
+}
+
+// smc_train_step sync area: [0, 128) the done counter; then per group a 256-B record of two
+// 128-B counter lines; then the slice terminal sums [groups][2][W] and column sums [groups][2][W][N].
+// groups <= 2 #CUs / W (the resident kernel fits one workgroup per CU; twice that for margin).
+struct ResSyncLayout {
+  int64_t groups, xsum_off, xcol_off, bytes;
+};
+ResSyncLayout res_sync_layout(int32_t W, int32_t N, int cus) {
+  ResSyncLayout l{};
+  if (W <= 1) {
+    l.bytes = sizeof(uint32_t);
+    return l;
+  }
+  l.groups = (2 * static_cast<int64_t>(cus) + W - 1) / W;
+  l.xsum_off = 128 + 256 * l.groups;
+  l.xcol_off = (l.xsum_off + l.groups * 2 * W * 8 + 255) / 256 * 256;
+  l.bytes = l.xcol_off + l.groups * 2 * W * static_cast<int64_t>(N) * 8;
+  return l;
 }
 
 bool split_ok(const EngineArgs& a, bool f32) {
@@ -1096,8 +1215,18 @@ int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
     (void)hipGetLastError();
     return fail(SMC_ERR_HIP, "resident_kernel: cannot raise the dynamic LDS limit");
   }
+  const int W = a.res_slices > 1 ? a.res_slices : 1;
   unsigned grid = 0;
-  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kResThreads, lds, a.B, &grid)) return st;
+  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kResThreads, lds, a.B * W, &grid)) return st;
+  if (W > 1) {
+    // whole groups of W co-resident workgroups (every slice of a group waits for the others),
+    // in multiples of 8 W where possible so a group's slices share an XCD
+    unsigned groups = grid / W;
+    if (groups > static_cast<unsigned>(a.res_groups)) groups = static_cast<unsigned>(a.res_groups);
+    if (groups >= 8) groups -= groups % 8;
+    if (groups == 0) return fail(SMC_ERR_INVALID_SHAPE, "resident_kernel: fewer resident slots than slices");
+    grid = groups * W;
+  }
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(kResThreads), lds, stream, a);
   return check_launch("resident_kernel");
 }
@@ -1303,13 +1432,18 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
                        float* cvnn_input_dev, int64_t n_contracts, int32_t timesteps, int32_t network_size,
                        int32_t batches_per_mc_run, uint64_t mc_seed, int32_t scheme, int32_t normalization,
                        int32_t dtype, int32_t store_mode, void* paths_dev, int64_t path_pitch, int64_t chunk_contracts,
-                       void* targets_dev, uint32_t* counter_dev, void* stream) {
-  if (!sobol_tables_dev || !lower_dev || !upper_dev || !cursor_dev || !contracts_dev || !counter_dev)
+                       void* targets_dev, void* sync_dev, int64_t sync_bytes, void* stream) {
+  if (!sobol_tables_dev || !lower_dev || !upper_dev || !cursor_dev || !contracts_dev || !sync_dev)
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_step: NULL buffer");
   if (dim != 6) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_step: dim must be 6 (BlackScholes.Inputs)");
   if (index_offset < 0 || advance < 0) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_step: negative offset");
+  if (network_size <= 0 || batches_per_mc_run <= 0)
+    return fail(SMC_ERR_INVALID_SHAPE, "smc_train_step: network_size and batches_per_mc_run must be > 0");
   const hipStream_t s = as_stream(stream);
   const int64_t P = static_cast<int64_t>(network_size) * batches_per_mc_run;
+  const int64_t need = smc_train_step_sync_bytes(timesteps, network_size, batches_per_mc_run, dtype, path_pitch);
+  if (need <= 0) return fail(SMC_ERR_HIP, "smc_train_step: device query failed");
+  if (sync_bytes < need) return fail(SMC_ERR_INVALID_SHAPE, "smc_train_step: sync area smaller than smc_train_step_sync_bytes");
   EngineArgs a{};
   a.B = n_contracts;
   a.T = timesteps;
@@ -1318,7 +1452,6 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   a.M = batches_per_mc_run;
   a.seed = mc_seed;
   a.ordinal_dev = cursor_dev + 1;
-  a.ordinal0 = index_offset;
   a.scheme = scheme;
   a.normalize = normalization != SMC_NORM_RAW;
   a.store = store_mode;
@@ -1327,22 +1460,46 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   a.targets = targets_dev;
   a.pitch = path_pitch;
   a.slices = 1;
-  const bool fused = SMC_TRAIN_MODE == 3 && dtype == SMC_DTYPE_F32 && n_contracts > 0 && chunk_contracts >= n_contracts &&
+  a.res_slices = resident_slices(P);
+  char* sync = static_cast<char*>(sync_dev);
+  a.done = reinterpret_cast<uint32_t*>(sync);
+  if (a.res_slices > 1) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(SMC_ERR_HIP, "smc_train_step: device query failed");
+    }
+    const ResSyncLayout l = res_sync_layout(a.res_slices, network_size, cus);
+    a.res_groups = static_cast<int32_t>(l.groups);
+    a.res_cnt = reinterpret_cast<uint32_t*>(sync + 128);
+    a.res_xsum = reinterpret_cast<double*>(sync + l.xsum_off);
+    a.res_xcol = reinterpret_cast<double*>(sync + l.xcol_off);
+  }
+  const bool fused = SMC_TRAIN_MODE == 3 && dtype == SMC_DTYPE_F32 && n_contracts > 0 && chunk_contracts > 0 &&
                      valid_scheme(scheme) && (store_mode == SMC_STORE_ALL || store_mode == SMC_STORE_TERMINAL) &&
-                     paths_dev && targets_dev && network_size > 0 && batches_per_mc_run > 0 && resident_ok(a, true);
+                     paths_dev && targets_dev && resident_ok(a, true);
   if (fused) {
-    a.contracts = contracts_dev;
+    // one resident launch per chunk of contracts; each draws its own contracts, the last advances
+    // the cursor (the earlier ones read it unchanged)
     a.sobol = sobol_tables_dev;
     a.sobol_dim = dim;
     a.lower = lower_dev;
     a.upper = upper_dev;
-    a.contracts_out = contracts_dev;
-    a.cvnn_out = cvnn_input_dev;
     a.cursor = cursor_dev;
-    a.sobol_index0 = index_offset;
-    a.advance = advance;
-    a.done = counter_dev;
-    return dispatch_engine(a, dtype, s);
+    for (int64_t off = 0; off < n_contracts; off += chunk_contracts) {
+      const int64_t nb = n_contracts - off < chunk_contracts ? n_contracts - off : chunk_contracts;
+      EngineArgs c = a;
+      c.B = nb;
+      c.ordinal0 = index_offset + off;
+      c.contracts = contracts_dev + off * 6;
+      c.contracts_out = contracts_dev + off * 6;
+      c.cvnn_out = cvnn_input_dev ? cvnn_input_dev + off * 6 : nullptr;
+      c.targets = static_cast<char*>(targets_dev) + static_cast<size_t>(off) * network_size * 2 * sizeof(float);
+      c.sobol_index0 = index_offset + off;
+      c.advance = off + nb == n_contracts ? advance : 0;
+      if (int32_t st = dispatch_engine(c, dtype, s)) return st;
+    }
+    return SMC_OK;
   }
   // any other shape: the Sobol draw, the targets launch(es), then the cursor advance
   if (int32_t st = smc_sobol_draw(sobol_tables_dev, dim, cursor_dev, index_offset, n_contracts, lower_dev, upper_dev,
@@ -1354,6 +1511,51 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
     return st;
   hipLaunchKernelGGL(advance_cursor_kernel, dim3(1), dim3(64), 0, s, cursor_dev, advance);
   return check_launch("advance_cursor_kernel");
+}
+
+int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run, int32_t dtype,
+                                  int64_t path_pitch) {
+  if (network_size <= 0 || batches_per_mc_run <= 0) return sizeof(uint32_t);
+  EngineArgs a{};
+  a.T = timesteps;
+  a.N = network_size;
+  a.P = static_cast<int64_t>(network_size) * batches_per_mc_run;
+  a.simulate = 1;
+  a.targets = &a;
+  a.pitch = path_pitch;
+  a.slices = 1;
+  a.res_slices = resident_slices(a.P);
+  if (a.res_slices <= 1) return sizeof(uint32_t);
+  a.res_cnt = reinterpret_cast<uint32_t*>(&a);  // any non-null: the shape test only
+  a.res_xsum = a.res_xcol = reinterpret_cast<double*>(&a);
+  a.done = reinterpret_cast<uint32_t*>(&a);
+  if (!(SMC_TRAIN_MODE == 3 && resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))) return sizeof(uint32_t);
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return res_sync_layout(a.res_slices, network_size, cus).bytes;
+}
+
+const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run, int32_t dtype,
+                                  int64_t path_pitch) {
+  EngineArgs a{};
+  a.T = timesteps;
+  a.N = network_size;
+  a.P = static_cast<int64_t>(network_size) * batches_per_mc_run;
+  a.simulate = 1;
+  a.targets = &a;
+  a.pitch = path_pitch;
+  a.slices = 1;
+  a.res_slices = resident_slices(a.P);
+  a.res_cnt = reinterpret_cast<uint32_t*>(&a);
+  a.res_xsum = a.res_xcol = reinterpret_cast<double*>(&a);
+  a.done = reinterpret_cast<uint32_t*>(&a);
+  if (SMC_TRAIN_MODE == 3 && resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))
+    return a.res_slices > 1 ? "resident_kernel(sliced)" : "resident_kernel";
+  return smc_train_targets_kernel(timesteps, network_size, a.P, dtype, path_pitch, 0);
 }
 
 int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, int64_t n_paths, int32_t all_rows) {

@@ -111,10 +111,21 @@ class TrainingEngine:
         self._workspace = torch.zeros(max(ws, 8), dtype=torch.uint8, device=device) if ws else None
         self._workspace_bytes = ws
         self._f32_in = model_dtype == torch.float32
-        self._counter = torch.zeros(1, dtype=torch.int32, device=device)  # smc_train_step arrivals
-        # the path/CF kernel launch_targets runs for this shape (bench labels, rocprof cross-check)
-        self.kernel_name = _lib.lib().smc_train_targets_kernel(
-            self.T, self.N, self.P, self._dtype_code, self.pitch, 1 if ws else 0).decode()
+        # smc_train_step's sync area (arrival counters; the sliced resident kernel's exchanged sums),
+        # zero-filled once, left zeroed by every step
+        self._uses_train_step = self._f32_in and self.dim == 6 and self._workspace is None
+        sync = int(_lib.lib().smc_train_step_sync_bytes(self.T, self.N, self.M, self._dtype_code, self.pitch))
+        if sync < 0:
+            raise RuntimeError("smc_train_step_sync_bytes: device query failed")
+        self._sync = torch.zeros(max(sync, 8), dtype=torch.uint8, device=device)
+        self._sync_bytes = sync
+        # the path/CF kernel the step runs for this shape (bench labels, rocprof cross-check)
+        if self._uses_train_step:
+            self.kernel_name = _lib.lib().smc_train_step_kernel(self.T, self.N, self.M, self._dtype_code,
+                                                                self.pitch).decode()
+        else:
+            self.kernel_name = _lib.lib().smc_train_targets_kernel(
+                self.T, self.N, self.P, self._dtype_code, self.pitch, 1 if ws else 0).decode()
 
     @property
     def global_batch(self) -> int:
@@ -138,14 +149,14 @@ class TrainingEngine:
         stream = _lib.stream_handle()
         b = out if out is not None else self.buffers
         offset = self.rank * self.B
-        if self._f32_in and self.dim == 6 and self._workspace is None:
-            # draw + targets + cursor advance: one launch where the resident kernel takes the shape
+        if self._uses_train_step:
+            # draw + targets + cursor advance: one launch per chunk where the resident kernel takes the shape
             _lib.check(_lib.lib().smc_train_step(
                 _lib.ptr(self.tables), self.dim, _lib.ptr(self.lower), _lib.ptr(self.upper), _lib.ptr(self.cursor),
                 offset, self.global_batch, _lib.ptr(b.contracts), _lib.ptr(b.real_in), self.B, self.T, self.N,
                 self.M, self.seed, self._scheme, self._norm, self._dtype_code, self.store_mode,
-                _lib.ptr(self._paths_buf), self.pitch, self.chunk, _lib.ptr(b.targets), _lib.ptr(self._counter),
-                stream))
+                _lib.ptr(self._paths_buf), self.pitch, self.chunk, _lib.ptr(b.targets), _lib.ptr(self._sync),
+                self._sync_bytes, stream))
             return b
         draw_device(self.tables, self.dim, self.cursor[0:1], offset, self.B, self.lower, self.upper, b.contracts,
                     b.real_in if self._f32_in else None)

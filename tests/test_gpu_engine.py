@@ -371,54 +371,126 @@ def test_resident_kernel_bit_exact(oracle, golden, B, N, M, store) -> None:
 
 
 # ------------------------------------------------------------------------------ fused step
-STEP_CASES = [  # (B, T, N, M, math, store): resident shapes (fused launch) and fallback shapes
-    (None, 16, 256, 256, _lib.MATH_HW, _lib.STORE_ALL),      # C2 per-contract shape, 2 rounds + 3
-    (37, 16, 64, 64, 0, _lib.STORE_TERMINAL),                # resident, portable math, terminal rows
-    (21, 16, 128, 1024, _lib.MATH_HW, _lib.STORE_ALL),       # P = 131,072: split pair fallback
-    (9, 5, 64, 4, 0, _lib.STORE_ALL),                        # T != 16: contract_kernel fallback
+STEP_CASES = [  # (B, T, N, M, math, store, chunk): resident shapes (fused launch) and fallback shapes
+    (None, 16, 256, 256, _lib.MATH_HW, _lib.STORE_ALL, None),   # C2 per-contract shape, 2 rounds + 3
+    (37, 16, 64, 64, 0, _lib.STORE_TERMINAL, None),             # resident, portable math, terminal rows
+    (37, 16, 64, 64, 0, _lib.STORE_ALL, 10),                    # resident, four chunk launches per step
+    (9, 5, 64, 4, 0, _lib.STORE_ALL, None),                     # T != 16: contract_kernel fallback
+    (7, 16, 1000, 4, 0, _lib.STORE_ALL, None),                  # N does not divide 4096: split pair fallback
 ]
 
 
-@pytest.mark.parametrize("B,T,N,M,math,store", STEP_CASES)
-def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store) -> None:
-    """smc_train_step (Sobol draw + targets + cursor advance; one resident_kernel launch where the
-    shape allows) is bit-identical to smc_sobol_draw + smc_train_targets + the cursor update, over
-    three consecutive steps of a rank-1-of-2 shard; the arrival counter is left at zero."""
+def _sync(L, T, N, M, pitch):
+    n = int(L.smc_train_step_sync_bytes(T, N, M, _lib.DTYPE_F32, pitch))
+    assert n > 0
+    return torch.zeros(n, dtype=torch.uint8, device=DEV), n
+
+
+@pytest.mark.parametrize("B,T,N,M,math,store,chunk", STEP_CASES)
+def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store, chunk) -> None:
+    """smc_train_step (Sobol draw + targets + cursor advance; one resident_kernel launch per chunk
+    where the shape allows) is bit-identical to smc_sobol_draw + smc_train_targets + the cursor
+    update, over three consecutive steps of a rank-1-of-2 shard; the sync area is left zeroed."""
     L = _L()
     if B is None:
         B = 2 * torch.cuda.get_device_properties(0).multi_processor_count + 3
+    chunk = chunk or B
     P = N * M
     eng = SobolEngine(6, 7, 0)
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
     hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
     pitch = int(L.smc_path_pitch(P, 0))
-    shape = (B, T, pitch) if store == _lib.STORE_ALL else (B, pitch)
+    shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
     paths = torch.empty(shape, dtype=torch.float32, device=DEV)
     scheme = _lib.SCHEME_LOG_EULER | math
     offset, adv = B, 2 * B  # rank 1 of 2
     cur_a = torch.tensor([100, 50], dtype=torch.int64, device=DEV)
     cur_b = cur_a.clone()
-    counter = torch.zeros(1, dtype=torch.int32, device=DEV)
+    sync, nsync = _sync(L, T, N, M, pitch)
+    assert nsync == 4  # whole-contract shapes: one arrival counter
     for _ in range(3):
         ca = torch.empty((B, 6), dtype=torch.float64, device=DEV)
         fa = torch.empty((B, 6), dtype=torch.float32, device=DEV)
         ta = torch.empty((B, N), dtype=torch.complex64, device=DEV)
         _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur_a), offset, adv,
                                     _lib.ptr(ca), _lib.ptr(fa), B, T, N, M, 7, scheme, _lib.NORM_NORMALIZE,
-                                    _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, B, _lib.ptr(ta),
-                                    _lib.ptr(counter), None))
+                                    _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, chunk, _lib.ptr(ta),
+                                    _lib.ptr(sync), nsync, None))
         cb = torch.empty_like(ca)
         fb = torch.empty_like(fa)
         tb = torch.empty_like(ta)
         draw_device(tables, 6, cur_b[0:1], offset, B, lo, hi, cb, fb)
         _lib.check(L.smc_train_targets(_lib.ptr(cb), B, T, N, M, 7, _lib.ptr(cur_b[1:2]), offset, scheme,
-                                       _lib.NORM_NORMALIZE, _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, B, None,
-                                       _lib.ptr(tb), None, 0, None))
+                                       _lib.NORM_NORMALIZE, _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, chunk,
+                                       None, _lib.ptr(tb), None, 0, None))
         cur_b.add_(adv)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(ca.cpu().numpy(), cb.cpu().numpy())
         np.testing.assert_array_equal(fa.cpu().numpy(), fb.cpu().numpy())
         np.testing.assert_array_equal(ta.cpu().numpy(), tb.cpu().numpy())
         assert cur_a.tolist() == cur_b.tolist()
-        assert int(counter.item()) == 0
+        assert int(sync.view(torch.int32)[0].item()) == 0
+
+
+SLICED_CASES = [  # (B, N, M, store, chunk): shapes with P > 65,536 (W = P / 65,536 slices)
+    (None, 1024, 256, _lib.STORE_ALL, None),   # C3 per-contract shape, W = 4, > 1 contract per group
+    (70, 1024, 256, _lib.STORE_ALL, 24),       # C3 shape in three chunk launches
+    (23, 128, 1024, _lib.STORE_TERMINAL, None),  # W = 2, terminal rows only
+    (11, 512, 1024, _lib.STORE_ALL, None),     # W = 8, N = 512
+]
+
+
+@pytest.mark.parametrize("B,N,M,store,chunk", SLICED_CASES)
+def test_sliced_train_step_bit_exact(oracle, golden, B, N, M, store, chunk) -> None:
+    """smc_train_step at P > 65,536: W co-resident resident_kernel workgroups per contract that
+    exchange their terminal and column sums.  Portable math is bit-exact with the kernel-mode
+    oracle in the slice order (oracle.train_step_order); hw math within 1e-5 of the reference-mode
+    targets; contracts and CVNN input bit-equal to the Sobol draw; the cursor advances; the
+    arrival counters are left zeroed."""
+    L = _L()
+    T, P = 16, N * M
+    if B is None:
+        B = 2 * torch.cuda.get_device_properties(0).multi_processor_count // 4 + 3
+    chunk = chunk or B
+    wg, W = oracle.train_step_order(T, N, P)
+    assert wg == 1024 and W == P // 65536
+    pitch = int(L.smc_path_pitch(P, 0))
+    assert L.smc_train_step_kernel(T, N, M, 0, pitch) == b"resident_kernel(sliced)"
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
+    lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
+    hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
+    shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
+    paths = torch.empty(shape, dtype=torch.float32, device=DEV)
+    sync, nsync = _sync(L, T, N, M, pitch)
+    assert nsync > 4
+    start = [40, 9]
+    for math in (0, _lib.MATH_HW):
+        cur = torch.tensor(start, dtype=torch.int64, device=DEV)
+        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
+        f = torch.empty((B, 6), dtype=torch.float32, device=DEV)
+        t = torch.full((B, N), float("nan"), dtype=torch.complex64, device=DEV)
+        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
+                                    _lib.ptr(c), _lib.ptr(f), B, T, N, M, 7, _lib.SCHEME_LOG_EULER | math,
+                                    _lib.NORM_NORMALIZE, _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, chunk,
+                                    _lib.ptr(t), _lib.ptr(sync), nsync, None))
+        cb = torch.empty_like(c)
+        fb = torch.empty_like(f)
+        draw_device(tables, 6, torch.tensor(start[:1], dtype=torch.int64, device=DEV), 0, B, lo, hi, cb, fb)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(c.cpu().numpy(), cb.cpu().numpy())
+        np.testing.assert_array_equal(f.cpu().numpy(), fb.cpu().numpy())
+        assert cur.tolist() == [start[0] + B, start[1] + B]
+        # the done counter and the group counters are back at zero (the second pass depends on it:
+        # its exchanges wait for W arrivals per contract round from zero)
+        words = sync.view(torch.int32).cpu().numpy()
+        assert words[0] == 0 and not words[32:32 + 64 * 16].any()
+        contracts = c.cpu().numpy()
+        got = t.cpu().numpy()
+        if math == 0:
+            kt, _ = oracle.kernel_targets(contracts, T, N, M, seed=7, ordinal0=start[1], wg=wg, slices=W)
+            np.testing.assert_array_equal(got, kt)
+        else:
+            want = oracle.training_targets(contracts[:12], T, N, M, seed=7, ordinal0=start[1])
+            assert _norm_rel(got[:12], want) < 1e-5
