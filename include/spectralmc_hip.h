@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 8
+#define SMC_ABI_VERSION 9
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -143,7 +143,7 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
  * the sync area; the f64 sums are added in slice order (oracle kernel mode, slices = W).  Other
  * shapes run the three steps as separate launches, bit-identical to the separate calls.
  * sync_dev: smc_train_step_sync_bytes(...) bytes, zero-filled before the first call (every call
- * leaves it zeroed). */
+ * leaves its counters zeroed). */
 int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const double* lower_dev,
                        const double* upper_dev, int64_t* cursor_dev, int64_t index_offset, int64_t advance,
                        double* contracts_dev, float* cvnn_input_dev, int64_t n_contracts, int32_t timesteps,
@@ -183,15 +183,32 @@ int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t col
  * paths_dev: [chunk][A][T][pitch] f32 (SMC_STORE_ALL) or [chunk][A][pitch] (SMC_STORE_TERMINAL),
  * reused per launch of chunk_contracts; terminal_sum_dev (may be NULL): [B][A] f64 sums of the
  * terminal rows; targets_dev: [B][N] complex64.  math: 0 (portable, CPU-reproducible) or
- * SMC_MATH_HW.  Needs 1 <= A <= 8, N % 4 == 0, N <= 4096, N*M a multiple of 2048.  With
+ * SMC_MATH_HW.  Needs 1 <= A <= 8, N % 4 == 0, N <= 4096, N*M a multiple of 2048.
+ * sync_dev (may be NULL): smc_basket_sync_bytes(...) bytes, zero-filled before the first call (every
+ * call leaves its counters zeroed).  With it, shapes the resident kernel takes (T = 16, N | 4096, N <= 2048,
+ * N*M a multiple of 4096 up to 32 x 4096) run basket_resident_kernel per chunk, in which W = N*M /
+ * 4096 co-resident workgroups per contract keep the terminal rows on chip and exchange their
+ * terminal sums, then basket_mean_fft_kernel over the slices' column sums (reduction orders:
+ * oracle_basket_kernel(wg = 1024, slices = W)).  Otherwise, with
  * terminal_sum_dev each chunk is two launches (simulate + store + terminal sums, then the CF pass
- * over the stored terminal rows), without it one fused launch; the targets are bit-identical. */
+ * over the stored terminal rows), without it one fused launch; these two are bit-identical. */
 int32_t smc_basket_train_targets(const double* contracts_dev, int64_t n_contracts, int32_t n_assets,
                                  int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
                                  uint64_t mc_seed, const int64_t* ordinal_dev, int64_t ordinal0,
                                  int32_t math, int32_t normalization, int32_t store_mode,
                                  void* paths_dev, int64_t path_pitch, int64_t chunk_contracts,
-                                 double* terminal_sum_dev, void* targets_dev, void* stream);
+                                 double* terminal_sum_dev, void* targets_dev, void* sync_dev,
+                                 int64_t sync_bytes, void* stream);
+/* Bytes of smc_basket_train_targets' sync area for this shape and chunk_contracts on the current
+ * device (slice-sum exchange + the column sums of one launch; 0: the resident kernel does not take
+ * the shape, pass NULL; -1 on a bad argument or a failed query). */
+int64_t smc_basket_sync_bytes(int32_t n_assets, int32_t timesteps, int32_t network_size,
+                              int32_t batches_per_mc_run, int64_t chunk_contracts);
+/* Name of the kernel(s) smc_basket_train_targets launches for this shape ("basket_resident_kernel",
+ * "basket_kernel+basket_cf_kernel" or "basket_kernel"); with_sync / keep_sums: whether the call
+ * passes sync_dev / terminal_sum_dev.  Static string. */
+const char* smc_basket_train_targets_kernel(int32_t n_assets, int32_t timesteps, int32_t network_size,
+                                            int32_t batches_per_mc_run, int32_t with_sync, int32_t keep_sums);
 /* Basket workgroups (one per contract) resident on the current device at once, for sizing
  * chunk_contracts in whole rounds; -1 on a bad argument or a failed device query. */
 int64_t smc_basket_resident_slots(int32_t n_assets, int32_t network_size, int32_t math);

@@ -577,20 +577,33 @@ static void basket_cholesky(int A, double rho, double* L) {
 
 void oracle_basket_cholesky(int32_t A, double rho, double* L /* [8][8] */) { basket_cholesky(A, rho, L); }
 
+/* wg: lanes of the engine workgroup whose reduction orders to follow (512: basket_kernel /
+ * basket_cf_kernel; 1024: basket_resident_kernel); slices: workgroups per contract of
+ * basket_resident_kernel (slice s holds paths [s P/W, (s+1) P/W) = batch rows [s M/W, (s+1) M/W);
+ * its terminal sums and column sums are reduced like a whole contract's and the W of them are
+ * added in slice order from 0.0).  wg = 512, slices = 1 is the basket_kernel order. */
 void oracle_basket_kernel(const double* contracts, int64_t B, int32_t A, int32_t T, int32_t N, int32_t M,
-                          uint64_t seed, int64_t ordinal0, int32_t normalize, float* paths, double* terminal_sum,
-                          float* targets) {
+                          uint64_t seed, int64_t ordinal0, int32_t normalize, int32_t wg, int32_t slices,
+                          float* paths, double* terminal_sum, float* targets) {
   const double kLog2e = 1.4426950408889634;
   const int64_t P = (int64_t)N * M;
   const int width = 3 * A + 4;
+  const int lanes = wg > 0 ? wg : K_THREADS;
+  const int waves = lanes / 64;
+  const int64_t chunk_paths = (int64_t)K_PPL * lanes;
+  const int W = slices > 1 ? slices : 1;
+  const int64_t span = P / W;
+  const int Ms = M / W;
   float* X = (float*)malloc(sizeof(float) * (size_t)A * (size_t)P); /* terminal rows [A][P] */
-  double* lane_acc = (double*)malloc(sizeof(double) * (size_t)K_THREADS * (size_t)A);
+  double* lane_acc = (double*)malloc(sizeof(double) * (size_t)lanes * (size_t)A);
   const int cols = N / 4;
-  const int G = cols <= K_THREADS ? K_THREADS / cols : 1;
+  const int G = cols <= lanes ? lanes / cols : 1;
   double* part = (double*)malloc(sizeof(double) * (size_t)N * (size_t)G);
   double* avg = (double*)malloc(sizeof(double) * (size_t)N);
   double* cs = (double*)malloc(sizeof(double) * (size_t)N);
   double* sn = (double*)malloc(sizeof(double) * (size_t)N);
+  double* fxr = (double*)malloc(sizeof(double) * (size_t)N);
+  double* fxi = (double*)malloc(sizeof(double) * (size_t)N);
   for (int j = 0; j < N; ++j) twiddle(j, N, &sn[j], &cs[j]);
   for (int64_t b = 0; b < B; ++b) {
     const double* c = contracts + (int64_t)width * b;
@@ -641,29 +654,35 @@ void oracle_basket_kernel(const double* contracts, int64_t B, int32_t A, int32_t
       for (int i = 0; i < A; ++i)
         for (int j = 0; j < GROUP; ++j) X[(int64_t)i * P + gi * GROUP + j] = x[i][j];
     }
-    /* terminal sums: per lane over chunks (f32 4-path partials), wave butterfly, waves 0..7 */
-    memset(lane_acc, 0, sizeof(double) * (size_t)K_THREADS * (size_t)A);
-    for (int64_t chunk = 0; chunk < P; chunk += K_CHUNK)
-      for (int lane = 0; lane < K_THREADS; ++lane)
-        for (int i = 0; i < A; ++i) {
-          float p = 0.0f;
-          for (int j = 0; j < K_PPL; ++j) p += X[(int64_t)i * P + chunk + (int64_t)K_PPL * lane + j];
-          lane_acc[(size_t)lane * A + i] += (double)p;
-        }
+    /* terminal sums: per slice, per lane over the slice's chunks (f32 4-path partials), wave
+     * butterfly, waves in order; slices added in order */
     double tot[B_MAX_ASSETS];
-    for (int i = 0; i < A; ++i) {
-      tot[i] = 0.0;
-      for (int w = 0; w < K_WAVES; ++w) {
-        double v[64], nv[64];
-        for (int l = 0; l < 64; ++l) v[l] = lane_acc[(size_t)(64 * w + l) * A + i];
-        for (int off = 32; off >= 1; off >>= 1) {
-          for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
-          memcpy(v, nv, sizeof(v));
+    for (int i = 0; i < A; ++i) tot[i] = 0.0;
+    for (int sl = 0; sl < W; ++sl) {
+      memset(lane_acc, 0, sizeof(double) * (size_t)lanes * (size_t)A);
+      for (int64_t chunk = sl * span; chunk < (sl + 1) * span; chunk += chunk_paths)
+        for (int lane = 0; lane < lanes; ++lane)
+          for (int i = 0; i < A; ++i) {
+            float p = 0.0f;
+            for (int j = 0; j < K_PPL; ++j) p += X[(int64_t)i * P + chunk + (int64_t)K_PPL * lane + j];
+            lane_acc[(size_t)lane * A + i] += (double)p;
+          }
+      for (int i = 0; i < A; ++i) {
+        double st = 0.0;
+        for (int w = 0; w < waves; ++w) {
+          double v[64], nv[64];
+          for (int l = 0; l < 64; ++l) v[l] = lane_acc[(size_t)(64 * w + l) * A + i];
+          for (int off = 32; off >= 1; off >>= 1) {
+            for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+            memcpy(v, nv, sizeof(v));
+          }
+          st += v[0];
         }
-        tot[i] += v[0];
+        tot[i] = W > 1 ? tot[i] + st : st;
       }
-      if (terminal_sum) terminal_sum[b * A + i] = tot[i];
     }
+    for (int i = 0; i < A; ++i)
+      if (terminal_sum) terminal_sum[b * A + i] = tot[i];
     /* payoff + per-column batch sums (thread item (q, g): columns 4q..4q+3, m = g, g + G, ...) */
     const float Tf = (float)Tm;
     const float df = exp_any((float)(-r) * Tf);
@@ -674,24 +693,41 @@ void oracle_basket_kernel(const double* contracts, int64_t B, int32_t A, int32_t
       const float F = (float)c[4 + i] * exp_any((float)(r - c[4 + A + i]) * Tf);
       sc[i] = normalize ? F / (float)(tot[i] / (double)P) : 1.0f;
     }
-    for (int item = 0; item < cols * G; ++item) {
-      const int q = item % cols, gg = item / cols;
-      double sum[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int m = gg; m < M; m += G)
-        for (int e = 0; e < 4; ++e) {
-          float bs = 0.0f;
-          for (int i = 0; i < A; ++i) bs = bs + X[(int64_t)i * P + (int64_t)m * N + 4 * q + e] * sc[i];
-          const float diff = Kf - bs * wA;
-          sum[e] += (double)(df * (diff > 0.0f ? diff : 0.0f));
-        }
-      for (int e = 0; e < 4; ++e) part[gg * N + 4 * q + e] = sum[e];
+    for (int n = 0; n < N; ++n) avg[n] = 0.0;
+    for (int sl = 0; sl < W; ++sl) {
+      const int m0 = sl * Ms, m1 = (sl + 1) * Ms;
+      for (int item = 0; item < cols * G; ++item) {
+        const int q = item % cols, gg = item / cols;
+        double sum[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int m = m0 + gg; m < m1; m += G)
+          for (int e = 0; e < 4; ++e) {
+            float bs = 0.0f;
+            for (int i = 0; i < A; ++i) bs = bs + X[(int64_t)i * P + (int64_t)m * N + 4 * q + e] * sc[i];
+            const float diff = Kf - bs * wA;
+            sum[e] += (double)(df * (diff > 0.0f ? diff : 0.0f));
+          }
+        for (int e = 0; e < 4; ++e) part[gg * N + 4 * q + e] = sum[e];
+      }
+      for (int n = 0; n < N; ++n) {
+        double t2 = 0.0;
+        for (int gg = 0; gg < G; ++gg) t2 += part[gg * N + n];
+        avg[n] = W > 1 ? avg[n] + t2 : t2; /* slices in order from 0.0 */
+      }
     }
-    for (int n = 0; n < N; ++n) {
-      double t2 = 0.0;
-      for (int gg = 0; gg < G; ++gg) t2 += part[gg * N + n];
-      avg[n] = t2 / (double)M;
-    }
+    for (int n = 0; n < N; ++n) avg[n] = avg[n] / (double)M;
     float* out = targets + 2 * b * N;
+    if (lanes == 1024 && use_fft(N)) { /* basket_resident_kernel: fft_row as resident_kernel */
+      fft_real(avg, cs, sn, N, fxr, fxi);
+      for (int k = 0; k <= N / 2; ++k) {
+        out[2 * k] = (float)fxr[k];
+        out[2 * k + 1] = (float)fxi[k];
+        if (k != 0 && 2 * k != N) {
+          out[2 * (N - k)] = (float)fxr[k];
+          out[2 * (N - k) + 1] = (float)(-fxi[k]);
+        }
+      }
+      continue;
+    }
     for (int k = 0; k <= N / 2; ++k) {
       double re = 0.0, im = 0.0;
       int idx = 0;
@@ -709,6 +745,8 @@ void oracle_basket_kernel(const double* contracts, int64_t B, int32_t A, int32_t
       }
     }
   }
+  free(fxr);
+  free(fxi);
   free(part);
   free(avg);
   free(cs);

@@ -67,7 +67,8 @@ def lib() -> ctypes.CDLL:
                                        ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_basket_kernel.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64,
-                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_basket_cholesky.argtypes = [ctypes.c_int32, ctypes.c_double, ctypes.c_void_p]
         L.oracle_log_pos.argtypes = [ctypes.c_float]
         L.oracle_log_pos.restype = ctypes.c_float
@@ -275,11 +276,24 @@ def basket_cholesky(n_assets: int, rho: float) -> np.ndarray:
     return L[:n_assets, :n_assets].copy()
 
 
+def basket_order(n_assets: int, timesteps: int, network_size: int, batches: int, resident: bool = True) -> tuple[int, int]:
+    """(wg, slices) of the basket launch smc_basket_train_targets makes for this shape (basket.hip
+    basket_res_slices): basket_resident_kernel (1024 lanes, W = N*M / 4096 workgroups per contract)
+    when a sync area is passed and T = 16, N | 4096, 4 <= N <= 2048, 4096 | N*M, W <= 32 and the LDS
+    plan fits 160 KiB; else basket_kernel (512 lanes, one workgroup per contract)."""
+    N, P, A = network_size, network_size * batches, n_assets
+    lds = A * 1024 * 16 + (4096 + 2 * N + 16 * 8 + 16) * 8 + 2 * 64 * (2 * A + A * A) * 4
+    ok = (resident and timesteps == 16 and 4 <= N <= 2048 and N % 4 == 0 and 4096 % N == 0 and P % 4096 == 0
+          and P // 4096 <= 32 and lds <= 160 * 1024)
+    return (1024, P // 4096) if ok else (512, 1)
+
+
 def basket_kernel(contracts: np.ndarray, n_assets: int, timesteps: int, network_size: int, batches: int,
                   seed: int, ordinal0: int = 0, normalize: bool = True,
-                  want_paths: bool = False) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
+                  want_paths: bool = False, wg: int = 512, slices: int = 1) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
     """KERNEL mode restatement of the f32 basket engine (csrc/basket.hip, portable math):
-    (paths [B,A,T,P] or None, terminal sums [B,A] f64, targets [B,N] complex64)."""
+    (paths [B,A,T,P] or None, terminal sums [B,A] f64, targets [B,N] complex64).
+    (wg, slices): the launch's reduction orders, basket_order(...)."""
     contracts = np.ascontiguousarray(contracts, dtype=np.float64)
     B = contracts.shape[0]
     assert contracts.shape[1] == 3 * n_assets + 4
@@ -288,7 +302,7 @@ def basket_kernel(contracts: np.ndarray, n_assets: int, timesteps: int, network_
     tsum = np.empty((B, n_assets), dtype=np.float64)
     out = np.empty((B, network_size), dtype=np.complex64)
     lib().oracle_basket_kernel(_ptr(contracts), B, n_assets, timesteps, network_size, batches, seed, ordinal0,
-                               int(normalize), _ptr(paths), _ptr(tsum), _ptr(out))
+                               int(normalize), wg, slices, _ptr(paths), _ptr(tsum), _ptr(out))
     return paths, tsum, out
 
 

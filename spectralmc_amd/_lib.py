@@ -34,7 +34,7 @@ STORE_TERMINAL = 1
 MATH_HW = 0x100
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 
@@ -76,7 +76,10 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_cvnn_mfma_forward_backward": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64,
                                                 _c_vp, _c_i64, _c_vp, _c_i64, _c_vp]),
     "smc_basket_train_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_i32, _c_u64, _c_vp, _c_i64,
-                                          _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp]),
+                                          _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp,
+                                          _c_i64, _c_vp]),
+    "smc_basket_sync_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i64]),
+    "smc_basket_train_targets_kernel": (ctypes.c_char_p, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32]),
     "smc_basket_resident_slots": (_c_i64, [_c_i32, _c_i32, _c_i32]),
 }
 

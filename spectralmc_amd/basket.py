@@ -109,11 +109,23 @@ class BasketConfig:
                 np.array([b[n][1] for n in names], dtype=np.float64))
 
 
+def sync_bytes(cfg: BasketConfig, chunk_contracts: int) -> int:
+    """Bytes of the sync area the resident basket kernel needs for this shape and launch size (0: it
+    does not take the shape)."""
+    n = int(_lib.lib().smc_basket_sync_bytes(cfg.n_assets, cfg.timesteps, cfg.network_size, cfg.batches_per_mc_run,
+                                             chunk_contracts))
+    if n < 0:
+        raise RuntimeError("smc_basket_sync_bytes: bad shape or device query failed")
+    return n
+
+
 def basket_targets(contracts: torch.Tensor, cfg: BasketConfig, *, ordinal0: int = 0, paths: torch.Tensor | None = None,
                    terminal_sum: torch.Tensor | None = None, targets: torch.Tensor | None = None,
-                   pitch: int = 0) -> torch.Tensor:
+                   pitch: int = 0, resident: bool = True) -> torch.Tensor:
     """One call of the basket engine on explicit device contracts [B, 3A+4] f64.
-    ``paths``: [B, A, T, pitch] f32 to keep every row, else only terminal rows are kept (scratch)."""
+    ``paths``: [B, A, T, pitch] f32 to keep every row, else only terminal rows are kept (scratch).
+    ``resident``: pass a sync area, so shapes basket_resident_kernel takes run it (reduction orders:
+    oracle.basket_order(...))."""
     _lib.require_device()
     B = contracts.shape[0]
     if contracts.dtype != torch.float64 or contracts.shape[1] != cfg.dim or not contracts.is_contiguous():
@@ -127,19 +139,18 @@ def basket_targets(contracts: torch.Tensor, cfg: BasketConfig, *, ordinal0: int 
         raise ValueError("paths must be float32 with room for [B, A, T, pitch]")
     if targets is None:
         targets = torch.empty((B, cfg.network_size), dtype=torch.complex64, device=contracts.device)
+    nsync = sync_bytes(cfg, max(B, 1)) if resident else 0
+    sync = torch.zeros(nsync, dtype=torch.uint8, device=contracts.device) if nsync else None
     _lib.check(_lib.lib().smc_basket_train_targets(
         _lib.ptr(contracts), B, cfg.n_assets, cfg.timesteps, cfg.network_size, cfg.batches_per_mc_run, cfg.mc_seed,
         None, ordinal0, _lib.MATH_HW if cfg.math == "hw" else 0, 1 if cfg.normalize else 0, store, _lib.ptr(paths),
-        pitch, max(B, 1), _lib.ptr(terminal_sum), _lib.ptr(targets), _lib.stream_handle()))
+        pitch, max(B, 1), _lib.ptr(terminal_sum), _lib.ptr(targets), _lib.ptr(sync), nsync, _lib.stream_handle()))
     return targets
 
 
 class BasketEngine:
     """Device buffers + launches of the basket Monte-Carlo side of one training step
     (the ``TrainingEngine`` interface)."""
-
-    # the engine keeps the terminal sums, so each launch is the split pair (simulate, then CF)
-    kernel_name = "basket_kernel+basket_cf_kernel"
 
     def __init__(self, cfg: BasketConfig, batch_size: int, *, device: torch.device, sobol_skip: int = 0,
                  model_dtype: torch.dtype = torch.float32, rank: int = 0, world_size: int = 1,
@@ -187,6 +198,12 @@ class BasketEngine:
         self._paths_buf = torch.empty(shape, dtype=torch.float32, device=device)
         self.paths = self._paths_buf[..., :self.P]
         self._f32_in = model_dtype == torch.float32
+        # sync area of the resident kernel (zero-filled once; every launch leaves its counters zeroed);
+        # the engine keeps the terminal sums, so other shapes run the split pair (simulate, then CF)
+        self._sync_bytes = sync_bytes(cfg, self.chunk)
+        self._sync = torch.zeros(self._sync_bytes, dtype=torch.uint8, device=device) if self._sync_bytes else None
+        self.kernel_name = _lib.lib().smc_basket_train_targets_kernel(
+            self.A, self.T, self.N, self.M, 1 if self._sync is not None else 0, 1).decode()
 
     @property
     def global_batch(self) -> int:
@@ -222,7 +239,8 @@ class BasketEngine:
         _lib.check(_lib.lib().smc_basket_train_targets(
             _lib.ptr(b.contracts), self.B, self.A, self.T, self.N, self.M, self.cfg.mc_seed, ordinal_ptr, ordinal0,
             self._math, 1 if self.cfg.normalize else 0, self.store_mode, _lib.ptr(self._paths_buf), self.pitch,
-            self.chunk, _lib.ptr(self.terminal_sum), _lib.ptr(b.targets), stream))
+            self.chunk, _lib.ptr(self.terminal_sum), _lib.ptr(b.targets), _lib.ptr(self._sync), self._sync_bytes,
+            stream))
 
 
 def use_basket_engine(pricer, cfg: BasketConfig, *, store_paths: bool = True) -> None:

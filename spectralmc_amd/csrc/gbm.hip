@@ -30,6 +30,7 @@
 #include "smc_sobol.h"
 #include "smc_math.h"
 #include "smc_rng.h"
+#include "smc_device.h"
 
 namespace smc {
 namespace {
@@ -104,36 +105,6 @@ struct EngineArgs {
 constexpr int kSliceChunks = SMC_SLICE_CHUNKS;  // chunks (of kChunk paths) per workgroup when sliced
 
 
-// Stores / loads of bytes handed from one workgroup to another (possibly on another XCD):
-// write-through (sc1) 16-B stores drained before the arrival add, sc1 loads after it
-// (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms).
-// 16-B write-through stores through a buffer descriptor on the wave-uniform row base: the
-// compiler counts them in vmcnt and pads their data hazards.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row_base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row_base), static_cast<short>(0), 0x7fffffff,
-                                           0x00020000);
-}
-__device__ __forceinline__ void store_wt(const void* row_base, uint32_t off, float4 v) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  const v4f w = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(w, row_rsrc(row_base), off, 0, 16 /* sc1 */);
-}
-__device__ __forceinline__ void store_wt(const void* row_base, uint32_t off, double4 v) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  typedef double v2d __attribute__((ext_vector_type(2)));
-  const v2d lo = {v.x, v.y}, hi = {v.z, v.w};
-  const __amdgpu_buffer_rsrc_t r = row_rsrc(row_base);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, lo), r, off, 0, 16);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, hi), r, off + 16, 0, 16);
-}
-template <typename U>
-__device__ __forceinline__ void put_sc1(U* p, U v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename U>
-__device__ __forceinline__ U get_sc1(const U* p) {
-  return __hip_atomic_load(const_cast<U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 template <typename Real>
 struct Vec4T;
@@ -146,16 +117,6 @@ struct Vec4T<double> {
   using type = double4;
 };
 
-template <typename Real>
-struct Complex2;
-template <>
-struct Complex2<float> {
-  using type = float2;
-};
-template <>
-struct Complex2<double> {
-  using type = double2;
-};
 
 __device__ __forceinline__ Contract load_contract(const double* c) {
   return Contract{c[0], c[1], c[2], c[3], c[4], c[5]};
@@ -488,60 +449,6 @@ __host__ __device__ inline int cf_part_doubles(int N) {
   return need > 4 * kThreads ? need : 4 * kThreads;
 }
 
-// In-place radix-2 decimation-in-time FFT of the real sequence avg[0..N) into xr/xi (LDS), then
-// bins 0..N/2 and their Hermitian mirror -> out.  Stage len = 2, 4, ..., N: butterfly j of N/2,
-// i0 = (j / h) len + j mod h, i1 = i0 + h (h = len/2), w = cs[t] - i sn[t] with t = (j mod h) N/len:
-// (tr, ti) = x[i1] w (4 products, 2 sums, no contraction), x[i1] = x[i0] - t, x[i0] = x[i0] + t.
-__device__ __forceinline__ void lds_barrier() {  // LDS visibility only: no vmcnt drain of the stores
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-template <typename Real, int NT = kThreads, bool LDS_ONLY = false>
-__device__ void fft_row(const double* avg, const double* cs, const double* sn, int N, double* xr, double* xi,
-                        typename Complex2<Real>::type* out) {
-  using C2 = typename Complex2<Real>::type;
-  const int tid = threadIdx.x;
-  const int logN = 31 - __builtin_clz(static_cast<unsigned>(N));
-  auto barrier = [] {
-    if constexpr (LDS_ONLY) lds_barrier();
-    else __syncthreads();
-  };
-  for (int n = tid; n < N; n += NT) {
-    const int r = static_cast<int>(__builtin_bitreverse32(static_cast<unsigned>(n)) >> (32 - logN));
-    xr[r] = avg[n];
-    xi[r] = 0.0;
-  }
-  barrier();
-  for (int s = 1; s <= logN; ++s) {
-    const int h = 1 << (s - 1), shift = logN - s;  // twiddle index t = (j mod h) << shift
-    for (int j = tid; j < N / 2; j += NT) {
-      const int pos = j & (h - 1);
-      const int i0 = ((j >> (s - 1)) << s) + pos, i1 = i0 + h;
-      const double wr = cs[pos << shift], wi = -sn[pos << shift];
-      const double ar = xr[i1], ai = xi[i1];
-      const double tr = ar * wr - ai * wi;
-      const double ti = ar * wi + ai * wr;
-      const double br = xr[i0], bi = xi[i0];
-      xr[i1] = br - tr;
-      xi[i1] = bi - ti;
-      xr[i0] = br + tr;
-      xi[i0] = bi + ti;
-    }
-    barrier();
-  }
-  for (int k = tid; k <= N / 2; k += NT) {
-    C2 v;
-    v.x = static_cast<Real>(xr[k]);
-    v.y = static_cast<Real>(xi[k]);
-    out[k] = v;
-    if (k != 0 && 2 * k != N) {
-      v.y = static_cast<Real>(-xi[k]);
-      out[N - k] = v;
-    }
-  }
-}
 
 template <typename Real>
 __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int64_t b,
@@ -600,7 +507,7 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
   }
   __syncthreads();
 #if !defined(SMC_CF_NO_DFT)  // tools/micro decomposition builds only
-  if (use_fft(N)) fft_row<Real>(avg, cs, sn, N, part, part + N, static_cast<C2*>(a.targets) + b * N);
+  if (use_fft(N)) fft_row<Real, kThreads>(avg, cs, sn, N, part, part + N, static_cast<C2*>(a.targets) + b * N);
   else dft_row<Real>(avg, cs, sn, N, static_cast<C2*>(a.targets) + b * N);
 #endif
 }
@@ -874,8 +781,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
         const uint32_t want = static_cast<uint32_t>(W) * (round + 1);
         uint32_t spins = 0;
         while (get_sc1(cnt) < want && ++spins < kResSpinLimit) __builtin_amdgcn_s_sleep(2);
-        double t = 0.0;
-        for (int j = 0; j < W; ++j) t += get_sc1(a.res_xsum + xslot + j);
+        const double t = ordered_sum_wt(a.res_xsum + xslot, 0, W, 1);  // slices in order
         row[6] = spins < kResSpinLimit ? t : __builtin_nan("");
       }
       lds_barrier();
@@ -929,11 +835,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       }
       lds_barrier();
       if (!reinterpret_cast<const int*>(row + 7)[0]) continue;  // uniform: another slice runs the FFT
-      for (int n = tid; n < N; n += kResThreads) {
-        double t = 0.0;
-        for (int j = 0; j < W; ++j) t += get_sc1(xcol + static_cast<int64_t>(j) * N + n);
-        avg[n] = t / static_cast<double>(M);
-      }
+      for (int n = tid; n < N; n += kResThreads) avg[n] = ordered_sum_wt(xcol, n, W, N) / static_cast<double>(M);
     }
     lds_barrier();
     fft_row<float, kResThreads, true>(avg, cs, sn, N, part, part + N, static_cast<float2*>(a.targets) + b * N);

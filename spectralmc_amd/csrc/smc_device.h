@@ -1,0 +1,140 @@
+// Device helpers shared by the engine kernels (gbm.hip, basket.hip): buffer-descriptor row
+// stores, the write-through hand-off between workgroups, LDS-only barriers and the in-LDS FFT
+// of the CF targets.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace smc {
+namespace {
+
+// Stores / loads of bytes handed from one workgroup to another (possibly on another XCD):
+// write-through (sc1) 16-B stores drained before the arrival add, sc1 loads after it
+// (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms).
+// 16-B write-through stores through a buffer descriptor on the wave-uniform row base: the
+// compiler counts them in vmcnt and pads their data hazards.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* row_base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row_base), static_cast<short>(0), 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ void store_wt(const void* row_base, uint32_t off, float4 v) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, row_rsrc(row_base), off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ void store_wt(const void* row_base, uint32_t off, double4 v) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  const v2d lo = {v.x, v.y}, hi = {v.z, v.w};
+  const __amdgpu_buffer_rsrc_t r = row_rsrc(row_base);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, lo), r, off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, hi), r, off + 16, 0, 16);
+}
+// A path row's 16-B piece through a buffer descriptor, default cache policy (A/B at C2: the same
+// time as the flat global_store_dwordx4 form and as sc1, tools/micro/ringbench.hip).
+__device__ __forceinline__ void store_row(const void* row_base, uint32_t off, float4 v) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, row_rsrc(row_base), off, 0, 0);
+}
+template <typename U>
+__device__ __forceinline__ void put_sc1(U* p, U v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename U>
+__device__ __forceinline__ U get_sc1(const U* p) {
+  return __hip_atomic_load(const_cast<U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sum over s < n of base[s * stride + idx] in order from 0.0, for data other workgroups published
+// with put_sc1 after the caller saw their arrivals: write-through (sc1) buffer loads on the
+// wave-uniform base, 8 in flight at a time (a loop of single atomic loads would pay one memory
+// latency per term).  The compiler fence keeps the loads after the arrival poll.
+__device__ __forceinline__ double ordered_sum_wt(const double* base, int64_t idx, int n, int64_t stride) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  const __amdgpu_buffer_rsrc_t r = row_rsrc(base);
+  double t = 0.0;
+  for (int s = 0; s < n; s += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)  // a clamped index keeps the batch straight-line; extra terms are dropped
+      v[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                            r, static_cast<uint32_t>(((s + k < n ? s + k : s) * stride + idx) * 8),
+                                            0, 16 /* sc1 */));
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (s + k < n) t += v[k];
+  }
+  return t;
+}
+
+template <typename Real>
+struct Complex2;
+template <>
+struct Complex2<float> {
+  using type = float2;
+};
+template <>
+struct Complex2<double> {
+  using type = double2;
+};
+
+// In-place radix-2 decimation-in-time FFT of the real sequence avg[0..N) into xr/xi (LDS), then
+// bins 0..N/2 and their Hermitian mirror -> out.  Stage len = 2, 4, ..., N: butterfly j of N/2,
+// i0 = (j / h) len + j mod h, i1 = i0 + h (h = len/2), w = cs[t] - i sn[t] with t = (j mod h) N/len:
+// (tr, ti) = x[i1] w (4 products, 2 sums, no contraction), x[i1] = x[i0] - t, x[i0] = x[i0] + t.
+__device__ __forceinline__ void lds_barrier() {  // LDS visibility only: no vmcnt drain of the stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <typename Real, int NT, bool LDS_ONLY = false>
+__device__ void fft_row(const double* avg, const double* cs, const double* sn, int N, double* xr, double* xi,
+                        typename Complex2<Real>::type* out) {
+  using C2 = typename Complex2<Real>::type;
+  const int tid = threadIdx.x;
+  const int logN = 31 - __builtin_clz(static_cast<unsigned>(N));
+  auto barrier = [] {
+    if constexpr (LDS_ONLY) lds_barrier();
+    else __syncthreads();
+  };
+  for (int n = tid; n < N; n += NT) {
+    const int r = static_cast<int>(__builtin_bitreverse32(static_cast<unsigned>(n)) >> (32 - logN));
+    xr[r] = avg[n];
+    xi[r] = 0.0;
+  }
+  barrier();
+  for (int s = 1; s <= logN; ++s) {
+    const int h = 1 << (s - 1), shift = logN - s;  // twiddle index t = (j mod h) << shift
+    for (int j = tid; j < N / 2; j += NT) {
+      const int pos = j & (h - 1);
+      const int i0 = ((j >> (s - 1)) << s) + pos, i1 = i0 + h;
+      const double wr = cs[pos << shift], wi = -sn[pos << shift];
+      const double ar = xr[i1], ai = xi[i1];
+      const double tr = ar * wr - ai * wi;
+      const double ti = ar * wi + ai * wr;
+      const double br = xr[i0], bi = xi[i0];
+      xr[i1] = br - tr;
+      xi[i1] = bi - ti;
+      xr[i0] = br + tr;
+      xi[i0] = bi + ti;
+    }
+    barrier();
+  }
+  for (int k = tid; k <= N / 2; k += NT) {
+    C2 v;
+    v.x = static_cast<Real>(xr[k]);
+    v.y = static_cast<Real>(xi[k]);
+    out[k] = v;
+    if (k != 0 && 2 * k != N) {
+      v.y = static_cast<Real>(-xi[k]);
+      out[N - k] = v;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace smc

@@ -112,7 +112,7 @@ class TrainingEngine:
         self._workspace_bytes = ws
         self._f32_in = model_dtype == torch.float32
         # smc_train_step's sync area (arrival counters; the sliced resident kernel's exchanged sums),
-        # zero-filled once, left zeroed by every step
+        # zero-filled once; every step leaves its counters zeroed
         self._uses_train_step = self._f32_in and self.dim == 6 and self._workspace is None
         sync = int(_lib.lib().smc_train_step_sync_bytes(self.T, self.N, self.M, self._dtype_code, self.pitch))
         if sync < 0:

@@ -11,6 +11,7 @@ import re
 import numpy as np
 import pytest
 
+import oracle
 from spectralmc_amd import _lib
 from spectralmc_amd.sobol_sampler import SobolEngine
 
@@ -179,17 +180,42 @@ def test_basket_entry_points_validate_before_any_device_work() -> None:
     assert L.smc_basket_resident_slots(4, 8192, 0) == -1
     fake = 1 << 20  # never dereferenced: validation fails first
     assert L.smc_basket_train_targets(None, 1, 4, 16, 256, 8, 7, None, 0, 0, 1, 2, fake, 0, 1, None, fake,
-                                      None) == 1
+                                      None, 0, None) == 1
     assert L.smc_basket_train_targets(fake, 1, 0, 16, 256, 8, 7, None, 0, 0, 1, 2, fake, 0, 1, None, fake,
-                                      None) == 1
+                                      None, 0, None) == 1
     assert L.smc_basket_train_targets(fake, 1, 4, 16, 256, 3, 7, None, 0, 0, 1, 2, fake, 0, 1, None, fake,
-                                      None) == 2  # N*M not a multiple of 2048
+                                      None, 0, None) == 2  # N*M not a multiple of 2048
     assert L.smc_basket_train_targets(fake, 1, 4, 16, 256, 8, 7, None, 0, 7, 1, 2, fake, 0, 1, None, fake,
-                                      None) == 1  # bad math flag
+                                      None, 0, None) == 1  # bad math flag
     assert L.smc_basket_train_targets(fake, 1, 4, 16, 256, 8, 7, None, 0, 0, 1, 3, fake, 0, 1, None, fake,
-                                      None) == 1  # bad store mode
+                                      None, 0, None) == 1  # bad store mode
     assert L.smc_basket_train_targets(fake, 1, 4, 16, 256, 8, 7, None, 0, 0, 1, 2, fake, 100, 1, None, fake,
-                                      None) == 2  # pitch < P
+                                      None, 0, None) == 2  # pitch < P
+
+
+def test_basket_sync_bytes_and_kernel_choice_on_host() -> None:
+    """smc_basket_sync_bytes rejects bad arguments and returns 0 (no sync area, no device query)
+    for shapes the resident kernel does not take; the kernel-name query mirrors the dispatch
+    (oracle.basket_order states the same conditions)."""
+    L = _lib.lib()
+    assert L.smc_basket_sync_bytes(0, 16, 256, 512, 64) == -1
+    assert L.smc_basket_sync_bytes(9, 16, 256, 512, 64) == -1
+    assert L.smc_basket_sync_bytes(4, 16, 0, 512, 64) == -1
+    assert L.smc_basket_sync_bytes(4, 16, 256, 512, 0) == -1     # chunk_contracts <= 0
+    assert L.smc_basket_sync_bytes(4, 5, 256, 512, 64) == 0          # T != 16
+    assert L.smc_basket_sync_bytes(4, 16, 256, 8, 64) == 0           # P = 2048: not a multiple of 4096
+    assert L.smc_basket_sync_bytes(4, 16, 256, 1024, 64) == 0        # W = 64 > 32
+    assert L.smc_basket_sync_bytes(4, 16, 12, 1024, 64) == 0         # N does not divide 4096
+    assert L.smc_basket_sync_bytes(8, 16, 2048, 8, 64) == 0          # LDS plan over 160 KiB
+    name = lambda *a: L.smc_basket_train_targets_kernel(*a).decode()  # noqa: E731
+    assert name(4, 16, 256, 512, 1, 1) == "basket_resident_kernel"
+    assert name(4, 16, 256, 512, 0, 1) == "basket_kernel+basket_cf_kernel"
+    assert name(4, 16, 256, 512, 0, 0) == "basket_kernel"
+    assert name(4, 5, 256, 512, 1, 1) == "basket_kernel+basket_cf_kernel"
+    for A, T, N, M in [(4, 16, 256, 512), (1, 16, 64, 64), (8, 16, 256, 16), (8, 16, 2048, 8), (4, 16, 256, 1024),
+                       (3, 16, 1024, 8), (2, 4, 256, 16), (6, 16, 256, 32), (7, 16, 256, 32), (6, 16, 2048, 8)]:
+        wg, _ = oracle.basket_order(A, T, N, M)
+        assert (wg == 1024) == (name(A, T, N, M, 1, 1) == "basket_resident_kernel"), (A, T, N, M)
 
 
 def test_engine_workspace_size_and_check() -> None:

@@ -28,6 +28,7 @@ def main() -> None:
     ap.add_argument("--math", default="hw", choices=["hw", "portable"])
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
+    ap.add_argument("--split", action="store_true", help="no sync area: the basket_kernel (+ CF) launches")
     a = ap.parse_args()
     cfg = BasketConfig(n_assets=a.A, timesteps=a.T, network_size=a.N, batches_per_mc_run=a.M, math=a.math)
     lo, hi = cfg.arrays()
@@ -41,10 +42,13 @@ def main() -> None:
     tg = torch.empty((a.B, a.N), dtype=torch.complex64, device=dev)
     L = _lib.lib()
     mh = _lib.MATH_HW if a.math == "hw" else 0
+    ns = 0 if a.split else max(int(L.smc_basket_sync_bytes(a.A, a.T, a.N, a.M, a.B)), 0)
+    sync = torch.zeros(ns, dtype=torch.uint8, device=dev) if ns else None
 
     def launch():
         _lib.check(L.smc_basket_train_targets(_lib.ptr(cd), a.B, a.A, a.T, a.N, a.M, 7, None, 0, mh, 1,
-                                              store, _lib.ptr(paths), pitch, a.B, None, _lib.ptr(tg), None))
+                                              store, _lib.ptr(paths), pitch, a.B, None, _lib.ptr(tg), _lib.ptr(sync), ns,
+                                              None))
 
     launch()
     torch.cuda.synchronize()
@@ -54,7 +58,8 @@ def main() -> None:
         launch()
     e1.record()
     torch.cuda.synchronize()
-    print(f"basket A={a.A} {a.math} {a.store}: {e0.elapsed_time(e1) / a.iters:.3f} ms/launch checksum",
+    kname = L.smc_basket_train_targets_kernel(a.A, a.T, a.N, a.M, 1 if ns else 0, 0).decode()
+    print(f"basket A={a.A} {a.math} {a.store} {kname}: {e0.elapsed_time(e1) / a.iters:.3f} ms/launch checksum",
           float(tg.abs().double().mean()))
 
 

@@ -24,12 +24,13 @@ template <int AUX>
 __global__ __launch_bounds__(1024) void ring_store(float* out, int R) {
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     float* base = out + static_cast<int64_t>(b % R) * T * PITCH;
+#pragma unroll 1
     for (int c = 0; c < NCHUNK; ++c) {
       v4f v = {1.f, 2.f, 3.f, (float)c};
 #pragma unroll
       for (int t = 0; t < T; ++t) {
-        if constexpr (AUX < 0)
-          reinterpret_cast<v4f*>(base + t * PITCH + c * CHUNK)[threadIdx.x] = v;
+        if constexpr (AUX < 0)  // wave-uniform row base + 32-bit lane offset (lane_paths' form)
+          *reinterpret_cast<v4f*>(reinterpret_cast<char*>(base + t * PITCH + c * CHUNK) + threadIdx.x * 16u) = v;
         else
           __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(base + t * PITCH + c * CHUNK), threadIdx.x * 16, 0, AUX);
         v.x += 1.f;
