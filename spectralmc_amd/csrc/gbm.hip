@@ -683,6 +683,18 @@ size_t resident_lds_bytes(int N) {
   return kResTermBytes + (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 8) * sizeof(double);
 }
 
+#if defined(SMC_EXPERIMENT_TRACE)  // tools/micro decomposition builds only: per-workgroup timestamps
+constexpr int kTraceStride = 40;
+__device__ uint64_t g_trace[1024 * kTraceStride];
+#define SMC_TRACE(slot)                                                                         \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_trace[blockIdx.x * kTraceStride + (slot)] =    \
+        __builtin_amdgcn_s_memrealtime();                                                       \
+  } while (0)
+#else
+#define SMC_TRACE(slot) do {} while (0)
+#endif
+
 template <bool LOG_EULER, bool HW, bool STORE_ALL>
 __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   typedef float v4f __attribute__((ext_vector_type(4)));
@@ -717,6 +729,14 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   double* sn = cs + N;                    // [N]
   double* row = sn + N;                   // [6] this contract's drawn Sobol row (fused step); [6]
                                           // the exchanged terminal sum, [7] the last-arriver flag
+  SMC_TRACE(0);
+#if defined(SMC_EXPERIMENT_TRACE)
+  if (tid == 0 && blockIdx.x < 1024) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_trace[blockIdx.x * kTraceStride + 1] = xcc;
+  }
+#endif
   for (int j = tid; j < N; j += kResThreads) math::twiddle(j, N, sn[j], cs[j]);
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
   const int64_t sob0 = a.sobol ? a.cursor[0] + a.sobol_index0 : 0;
@@ -764,6 +784,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     const double w = wave_sum(acc[0]);
     if (lane == 0) wsum[wave] = w;
     lds_barrier();
+    if (round < 18) SMC_TRACE(2 + 2 * round);  // simulation of this contract done
 #if defined(SMC_RESIDENT_NO_CF)  // tools/micro decomposition builds only: no payoff / M-mean / FFT
     lds_barrier();
     continue;
@@ -840,7 +861,9 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     lds_barrier();
     fft_row<float, kResThreads, true>(avg, cs, sn, N, part, part + N, static_cast<float2*>(a.targets) + b * N);
     lds_barrier();  // part (= term_lds) / avg / wsum / row are reused by the next contract
+    if (round < 18) SMC_TRACE(3 + 2 * round);  // CF of this contract done
   }
+  SMC_TRACE(39);
   if (a.done && tid == 0) {
     // every workgroup read the cursor (and made its last exchange) before it arrives here: the last
     // one advances the cursor and resets the exchange counters
@@ -1242,6 +1265,12 @@ int32_t validate_common(const double* contracts, int64_t B, int32_t T, int64_t P
 using namespace smc;
 
 extern "C" {
+#if defined(SMC_EXPERIMENT_TRACE)
+__attribute__((visibility("default"))) int32_t smc_debug_trace(uint64_t* host, int64_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(smc::g_trace), static_cast<size_t>(n) * sizeof(uint64_t)) == hipSuccess
+             ? 0 : 1;
+}
+#endif
 #pragma GCC visibility push(default)
 
 int32_t smc_gbm_simulate(const double* contracts_dev, int64_t n_contracts, int32_t timesteps, int64_t n_paths,

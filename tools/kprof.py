@@ -59,8 +59,8 @@ def main() -> None:
     torch.cuda.synchronize()
     if a.trace:
         import ctypes
-        n = a.B * 16
-        buf = np.zeros((n, 5), dtype=np.uint64)
+        n = 1024 * 40  # gbm.hip g_trace: [workgroup][40] s_memrealtime stamps (SMC_EXPERIMENT_TRACE builds)
+        buf = np.zeros((1024, 40), dtype=np.uint64)
         fn = getattr(L, "smc_debug_trace")
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
         torch.cuda.synchronize()
