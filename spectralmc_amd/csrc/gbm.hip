@@ -97,6 +97,10 @@ struct EngineArgs {
   uint32_t* res_cnt;          // [groups][64]: terminal-sum arrivals at +0, column-sum arrivals at +32
   double* res_xsum;           // [groups][2][W] slice terminal sums (2: contract round parity)
   double* res_xcol;           // [groups][2][W][N] slice column sums of the put payoffs
+  // whole-contract resident_kernel in smc_train_step: the last quarter of the contract rounds is
+  // handed out from this counter (zero between launches) instead of statically, so workgroups on
+  // XCDs with more write bandwidth take more contracts (NULL: all static)
+  uint32_t* res_queue;
 };
 
 #ifndef SMC_SLICE_CHUNKS
@@ -680,7 +684,7 @@ constexpr int kResMaxSlices = 8;
 constexpr uint32_t kResSpinLimit = 1u << 20;  // ~1 s of polling: a partner that never arrives gives NaN targets
 
 size_t resident_lds_bytes(int N) {
-  return kResTermBytes + (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 8) * sizeof(double);
+  return kResTermBytes + (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 9) * sizeof(double);
 }
 
 #if defined(SMC_EXPERIMENT_TRACE)  // tools/micro decomposition builds only: per-workgroup timestamps
@@ -728,7 +732,8 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   double* cs = avg + N;                   // [N]
   double* sn = cs + N;                    // [N]
   double* row = sn + N;                   // [6] this contract's drawn Sobol row (fused step); [6]
-                                          // the exchanged terminal sum, [7] the last-arriver flag
+                                          // the exchanged terminal sum, [7] the last-arriver flag,
+                                          // [8] the next dynamically handed-out contract
   SMC_TRACE(0);
 #if defined(SMC_EXPERIMENT_TRACE)
   if (tid == 0 && blockIdx.x < 1024) {
@@ -741,7 +746,18 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
   const int64_t sob0 = a.sobol ? a.cursor[0] + a.sobol_index0 : 0;
   uint32_t round = 0;
-  for (int64_t b = grp; b < a.B; b += groups, ++round) {
+  // contracts grp, grp + groups, ... up to n_static; then (res_queue) the rest from the counter, one
+  // at a time: the per-XCD write rate differs by up to ~10 % (profiles/r02 trace), and a static
+  // split ends at the slowest XCD
+  const bool dyn = a.res_queue != nullptr && W == 1;
+  const int64_t n_static = dyn ? (a.B / groups) * 3 / 4 * groups : a.B;
+  auto grab = [&]() -> int64_t {
+    if (tid == 0) reinterpret_cast<int64_t*>(row + 8)[0] = n_static + atomicAdd(a.res_queue, 1u);
+    lds_barrier();
+    return reinterpret_cast<const int64_t*>(row + 8)[0];
+  };
+  auto next = [&](int64_t b) -> int64_t { return b + groups < n_static ? b + groups : (dyn ? grab() : a.B); };
+  for (int64_t b = grp < n_static ? grp : (dyn ? grab() : a.B); b < a.B; b = next(b), ++round) {
     Contract c;
     if (a.sobol) {  // draw the contract (sobol_sampler.py:222-246) instead of a separate kernel
       if (tid < 6) {
@@ -871,6 +887,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
       a.cursor[0] += a.advance;
       a.cursor[1] += a.advance;
+      if (a.res_queue) *a.res_queue = 0u;
       if (W > 1)
         for (int k = 0; k < groups; ++k) {
           a.res_cnt[static_cast<int64_t>(k) * 64] = 0u;
@@ -903,10 +920,11 @@ int32_t resident_slices(int64_t P) {
 struct ResSyncLayout {
   int64_t groups, xsum_off, xcol_off, bytes;
 };
+constexpr int64_t kStepSyncBytes = 2 * sizeof(uint32_t);  // whole contracts: done counter, contract queue
 ResSyncLayout res_sync_layout(int32_t W, int32_t N, int cus) {
   ResSyncLayout l{};
   if (W <= 1) {
-    l.bytes = sizeof(uint32_t);
+    l.bytes = kStepSyncBytes;
     return l;
   }
   l.groups = (2 * static_cast<int64_t>(cus) + W - 1) / W;
@@ -1394,6 +1412,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   a.res_slices = resident_slices(P);
   char* sync = static_cast<char*>(sync_dev);
   a.done = reinterpret_cast<uint32_t*>(sync);
+  if (a.res_slices <= 1) a.res_queue = reinterpret_cast<uint32_t*>(sync) + 1;
   if (a.res_slices > 1) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
@@ -1446,7 +1465,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
 
 int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run, int32_t dtype,
                                   int64_t path_pitch) {
-  if (network_size <= 0 || batches_per_mc_run <= 0) return sizeof(uint32_t);
+  if (network_size <= 0 || batches_per_mc_run <= 0) return kStepSyncBytes;
   EngineArgs a{};
   a.T = timesteps;
   a.N = network_size;
@@ -1456,11 +1475,11 @@ int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32
   a.pitch = path_pitch;
   a.slices = 1;
   a.res_slices = resident_slices(a.P);
-  if (a.res_slices <= 1) return sizeof(uint32_t);
+  if (a.res_slices <= 1) return kStepSyncBytes;
   a.res_cnt = reinterpret_cast<uint32_t*>(&a);  // any non-null: the shape test only
   a.res_xsum = a.res_xcol = reinterpret_cast<double*>(&a);
   a.done = reinterpret_cast<uint32_t*>(&a);
-  if (!(SMC_TRAIN_MODE == 3 && resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))) return sizeof(uint32_t);
+  if (!(SMC_TRAIN_MODE == 3 && resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))) return kStepSyncBytes;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0) {

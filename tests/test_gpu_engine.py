@@ -408,7 +408,7 @@ def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store, ch
     cur_a = torch.tensor([100, 50], dtype=torch.int64, device=DEV)
     cur_b = cur_a.clone()
     sync, nsync = _sync(L, T, N, M, pitch)
-    assert nsync == 4  # whole-contract shapes: one arrival counter
+    assert nsync == 8  # whole-contract shapes: an arrival counter and the contract queue
     for _ in range(3):
         ca = torch.empty((B, 6), dtype=torch.float64, device=DEV)
         fa = torch.empty((B, 6), dtype=torch.float32, device=DEV)
@@ -430,7 +430,7 @@ def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store, ch
         np.testing.assert_array_equal(fa.cpu().numpy(), fb.cpu().numpy())
         np.testing.assert_array_equal(ta.cpu().numpy(), tb.cpu().numpy())
         assert cur_a.tolist() == cur_b.tolist()
-        assert int(sync.view(torch.int32)[0].item()) == 0
+        assert sync.view(torch.int32)[:2].tolist() == [0, 0]
 
 
 SLICED_CASES = [  # (B, N, M, store, chunk): shapes with P > 65,536 (W = P / 65,536 slices)
