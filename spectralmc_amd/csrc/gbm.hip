@@ -95,7 +95,8 @@ struct EngineArgs {
   int32_t res_slices;
   int32_t res_groups;         // capacity of the sync area in groups
   uint32_t* res_cnt;          // [groups][64]: terminal-sum arrivals at +0, column-sum arrivals at +32
-  double* res_xsum;           // [groups][2][W] slice terminal sums (2: contract round parity)
+  double* res_xsum;           // [groups][2][W + 1] slice terminal sums + the group's next contract
+                              // (2: contract round parity)
   double* res_xcol;           // [groups][2][W][N] slice column sums of the put payoffs
   // whole-contract resident_kernel in smc_train_step: the last quarter of the contract rounds is
   // handed out from this counter (zero between launches) instead of statically, so workgroups on
@@ -749,14 +750,23 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   // contracts grp, grp + groups, ... up to n_static; then (res_queue) the rest from the counter, one
   // at a time: the per-XCD write rate differs by up to ~10 % (profiles/r02 trace), and a static
   // split ends at the slowest XCD
-  const bool dyn = a.res_queue != nullptr && W == 1;
-  const int64_t n_static = dyn ? (a.B / groups) * 3 / 4 * groups : a.B;
+  // (sliced, W > 1: slice 0 takes the group's next contract during the current contract's
+  // terminal-sum exchange, and the partners read it with the sums; only once every group has a
+  // static contract, n_static > 0)
+  const int64_t n_static0 = (a.B / groups) * 3 / 4 * groups;
+  const bool dyn = a.res_queue != nullptr && (W == 1 || n_static0 > 0);
+  const int64_t n_static = dyn ? n_static0 : a.B;
   auto grab = [&]() -> int64_t {
     if (tid == 0) reinterpret_cast<int64_t*>(row + 8)[0] = n_static + atomicAdd(a.res_queue, 1u);
     lds_barrier();
     return reinterpret_cast<const int64_t*>(row + 8)[0];
   };
-  auto next = [&](int64_t b) -> int64_t { return b + groups < n_static ? b + groups : (dyn ? grab() : a.B); };
+  auto next = [&](int64_t b) -> int64_t {
+    if (b + groups < n_static) return b + groups;
+    if (!dyn) return a.B;
+    if (W == 1) return grab();
+    return reinterpret_cast<const int64_t*>(row + 8)[0];  // learned in this contract's exchange
+  };
   for (int64_t b = grp < n_static ? grp : (dyn ? grab() : a.B); b < a.B; b = next(b), ++round) {
     Contract c;
     if (a.sobol) {  // draw the contract (sobol_sampler.py:222-246) instead of a separate kernel
@@ -807,11 +817,16 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
 #endif
     double tot = 0.0;
     for (int k = 0; k < kResWaves; ++k) tot += wsum[k];
-    const int64_t xslot = (static_cast<int64_t>(grp) * 2 + (round & 1)) * W;  // this round's [W] slots
+    // this round's [W + 1] slots: the W slice sums, then the group's next contract (dynamic tail)
+    const int64_t xslot = (static_cast<int64_t>(grp) * 2 + (round & 1)) * (W + 1);
     if (W > 1) {
-      // terminal-sum exchange: publish, arrive, wait for the W slices, add them in slice order
+      // terminal-sum exchange: publish, arrive, wait for the W slices, add them in slice order.
+      // Slice 0 also takes the group's next contract from the queue when the next round is in the
+      // dynamic tail (its atomic's latency overlaps the drain below) and publishes it in slot W.
       if (tid == 0) {
         put_sc1(a.res_xsum + xslot + slc, tot);
+        if (dyn && slc == 0 && b + groups >= n_static)
+          put_sc1(reinterpret_cast<int64_t*>(a.res_xsum + xslot + W), n_static + atomicAdd(a.res_queue, 1u));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t* cnt = a.res_cnt + static_cast<int64_t>(grp) * 64;
         __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -820,6 +835,9 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
         while (get_sc1(cnt) < want && ++spins < kResSpinLimit) __builtin_amdgcn_s_sleep(2);
         const double t = ordered_sum_wt(a.res_xsum + xslot, 0, W, 1);  // slices in order
         row[6] = spins < kResSpinLimit ? t : __builtin_nan("");
+        if (dyn && b + groups >= n_static)
+          reinterpret_cast<int64_t*>(row + 8)[0] =
+              spins < kResSpinLimit ? get_sc1(reinterpret_cast<const int64_t*>(a.res_xsum + xslot + W)) : a.B;
       }
       lds_barrier();
       tot = row[6];
@@ -914,8 +932,9 @@ int32_t resident_slices(int64_t P) {
   return W;
 }
 
-// smc_train_step sync area: [0, 128) the done counter; then per group a 256-B record of two
-// 128-B counter lines; then the slice terminal sums [groups][2][W] and column sums [groups][2][W][N].
+// smc_train_step sync area: [0, 128) the done counter (+0) and the contract queue (+64); then per
+// group a 256-B record of two 128-B counter lines; then the slice terminal sums + next contract
+// [groups][2][W + 1] and column sums [groups][2][W][N].
 // groups <= 2 #CUs / W (the resident kernel fits one workgroup per CU; twice that for margin).
 struct ResSyncLayout {
   int64_t groups, xsum_off, xcol_off, bytes;
@@ -929,7 +948,7 @@ ResSyncLayout res_sync_layout(int32_t W, int32_t N, int cus) {
   }
   l.groups = (2 * static_cast<int64_t>(cus) + W - 1) / W;
   l.xsum_off = 128 + 256 * l.groups;
-  l.xcol_off = (l.xsum_off + l.groups * 2 * W * 8 + 255) / 256 * 256;
+  l.xcol_off = (l.xsum_off + l.groups * 2 * (W + 1) * 8 + 255) / 256 * 256;
   l.bytes = l.xcol_off + l.groups * 2 * W * static_cast<int64_t>(N) * 8;
   return l;
 }
@@ -1412,7 +1431,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   a.res_slices = resident_slices(P);
   char* sync = static_cast<char*>(sync_dev);
   a.done = reinterpret_cast<uint32_t*>(sync);
-  if (a.res_slices <= 1) a.res_queue = reinterpret_cast<uint32_t*>(sync) + 1;
+  a.res_queue = reinterpret_cast<uint32_t*>(sync) + (a.res_slices <= 1 ? 1 : 16);  // after the done counter
   if (a.res_slices > 1) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
