@@ -282,7 +282,7 @@ def basket_order(n_assets: int, timesteps: int, network_size: int, batches: int,
     when a sync area is passed and T = 16, N | 4096, 4 <= N <= 2048, 4096 | N*M, W <= 32 and the LDS
     plan fits 160 KiB; else basket_kernel (512 lanes, one workgroup per contract)."""
     N, P, A = network_size, network_size * batches, n_assets
-    lds = A * 1024 * 16 + (4096 + 2 * N + 16 * 8 + 16) * 8 + 2 * 64 * (2 * A + A * A) * 4
+    lds = A * 1024 * 16 + (4096 + 16 * 8 + 16) * 8 + (2 * 64 + 2) * (2 * A + A * A) * 4
     ok = (resident and timesteps == 16 and 4 <= N <= 2048 and N % 4 == 0 and 4096 % N == 0 and P % 4096 == 0
           and P // 4096 <= 32 and lds <= 160 * 1024)
     return (1024, P // 4096) if ok else (512, 1)

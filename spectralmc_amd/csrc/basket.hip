@@ -333,8 +333,9 @@ constexpr int kRSlots = 4;                   // slice-sum slots (contract j mod 
 constexpr int kRTable = 64;                  // contracts per coefficient table (one per wave-0 lane)
 constexpr uint32_t kRSpinLimit = 1u << 20;  // ~1 s of polling: a partner that never arrives gives NaN targets
 
-// Sync area of the resident basket launch (bytes): [0, 128) done counter; per group a 128-B line
-// of slice-sum arrivals; slice sums [groups][4][W][A] f64; column sums [chunk][W][N] f64.
+// Sync area of the resident basket launch (bytes): [0, 128) done counter (+0) and contract queue
+// (+64); per group a 128-B line of slice-sum arrivals; slice sums [groups][4][W A + 1] f64 (the
+// last entry: the contract of the group's iteration j + 2, dynamic tail); column sums [chunk][W][N].
 struct BasketSyncLayout {
   int64_t groups, xsum_off, xcol_off, bytes;
 };
@@ -342,7 +343,7 @@ BasketSyncLayout basket_sync_layout(int A, int W, int N, int64_t groups, int64_t
   BasketSyncLayout l{};
   l.groups = groups;
   l.xsum_off = 128 + 128 * groups;
-  l.xcol_off = (l.xsum_off + groups * kRSlots * W * A * 8 + 255) / 256 * 256;
+  l.xcol_off = (l.xsum_off + groups * kRSlots * (W * A + 1) * 8 + 255) / 256 * 256;
   l.bytes = l.xcol_off + chunk * W * static_cast<int64_t>(N) * 8;
   return l;
 }
@@ -350,11 +351,11 @@ BasketSyncLayout basket_sync_layout(int A, int W, int N, int64_t groups, int64_t
 constexpr int coef_stride(int A) { return 2 * A + A * A; }  // ca[A], x0[A], Lb[A][A] (f32)
 
 size_t basket_resident_lds_bytes(int A, int N) {
-  // terminal slots [A][1024] v4f, part [4096] f64, twiddles cs / sn [N] f64, wsum [16][A] f64,
-  // scales, two coefficient tables [64][2A + A^2] f32
+  // terminal slots [A][1024] v4f, part [4096] f64, wsum [16][A] f64, scales + contract ring, two
+  // coefficient tables [64][2A + A^2] f32 and two coefficient slots of dynamic contracts
   return static_cast<size_t>(A) * kRThreads * 16 +
-         (4096 + 2 * static_cast<size_t>(N) + kRWaves * kMaxAssets + 16) * sizeof(double) +
-         2 * kRTable * static_cast<size_t>(coef_stride(A)) * sizeof(float);
+         (4096 + kRWaves * kMaxAssets + 16) * sizeof(double) +
+         (2 * kRTable + 2) * static_cast<size_t>(coef_stride(A)) * sizeof(float);
 }
 
 struct BasketResArgs {
@@ -364,6 +365,10 @@ struct BasketResArgs {
   uint8_t* sync;          // basket_sync_layout
   int64_t xsum_off, xcol_off;
 };
+
+#if defined(SMC_EXPERIMENT_TRACE)  // tools/micro decomposition builds only: per-workgroup start/end + XCD
+__device__ uint64_t g_btrace[1024 * 4];
+#endif
 
 template <int A, bool HW, bool STORE_ALL>
 __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArgs ra) {
@@ -388,9 +393,12 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
   double* part = lds + static_cast<size_t>(A) * kRThreads * 2;               // [G][N] = [4096]
   double* wsum = part + 4096;                                                 // [kRWaves][A]
   float* pco = reinterpret_cast<float*>(wsum + kRWaves * kMaxAssets);         // scales[A], df, K
+  int64_t* bidx = reinterpret_cast<int64_t*>(wsum + kRWaves * kMaxAssets + 12);  // [4] contract of iteration j
   float* table = reinterpret_cast<float*>(wsum + kRWaves * kMaxAssets + 16);  // [2][kRTable][CS]
+  float* dco = table + 2 * kRTable * CS;                                      // [2][CS] dynamic contracts
   uint32_t* cnt = reinterpret_cast<uint32_t*>(ra.sync + 128 + 128 * static_cast<int64_t>(grp));
-  double* xsum = reinterpret_cast<double*>(ra.sync + ra.xsum_off) + static_cast<int64_t>(grp) * kRSlots * W * A;
+  const int XS = W * A + 1;                // slice-sum slot: W x A sums + the group's contract of j + 2
+  double* xsum = reinterpret_cast<double*>(ra.sync + ra.xsum_off) + static_cast<int64_t>(grp) * kRSlots * XS;
   double* xcol = reinterpret_cast<double*>(ra.sync + ra.xcol_off);           // [chunk][W][N]
   const int cols = N / 4;
   const int G = kRChunk / N;               // batch rows per slice
@@ -400,13 +408,49 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
   const uint32_t lane_off = static_cast<uint32_t>(kBPaths * sizeof(float)) * tid;
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
   const int width = 3 * A + 4;
-  const int64_t n_own = a.B > grp ? (a.B - 1 - grp) / groups + 1 : 0;  // contracts of this group
+  // contracts: grp + j groups for the first S iterations (every group has them), then the rest of
+  // the launch from the queue, so groups on XCDs with more write bandwidth take more (per-XCD
+  // finish times differed by up to 15 % with a static split).  Slice 0 takes the contract of
+  // iteration j + 2 while publishing iteration j's slice sums; the partners read it with those sums
+  // in iteration j + 1 (no added wait).
+  const int64_t S = (a.B / groups) * 3 / 4;
+  const bool dyn = S >= 2;
+  const int64_t n_static = dyn ? S * groups : a.B;
+  uint32_t* queue = reinterpret_cast<uint32_t*>(ra.sync + 64);
+  auto bof = [&](int64_t jj) -> int64_t { return !dyn || jj < S ? grp + jj * groups : bidx[jj & 3]; };
+  auto coefs = [&](int64_t bb, float* e) {  // simulation coefficients of contract bb (f64 Cholesky, rounded once)
+    const double* c = a.contracts + bb * width;
+    double L[kMaxAssets * kMaxAssets];
+    cholesky_equicorr(A, c[3], L);
+    const double dt = c[1] / static_cast<double>(kRowBlock);
+    const double sq = sqrt(dt);
+    constexpr double zscale = HW ? PathStream::kNormalScale<true> : 1.0;
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+      const double v = c[4 + 2 * A + i], d = c[4 + A + i];
+      const double drift = c[2] - d - 0.5 * v * v;
+      e[i] = static_cast<float>(drift * dt * kBLog2e);
+      e[A + i] = static_cast<float>(c[4 + i]);
+      const double bi = v * sq * kBLog2e * zscale;
+#pragma unroll
+      for (int k = 0; k < A; ++k) e[2 * A + i * A + k] = k <= i ? static_cast<float>(bi * L[i * kMaxAssets + k]) : 0.0f;
+    }
+  };
+#if defined(SMC_EXPERIMENT_TRACE)
+  if (tid == 0 && blockIdx.x < 1024) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_btrace[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
+    g_btrace[blockIdx.x * 4 + 1] = xcc;
+    g_btrace[blockIdx.x * 4 + 2] = static_cast<uint64_t>(grp);
+  }
+#endif
 
   // step 0 (wave 0): the payoff constants of contract jj from every slice's terminal sums
   auto gather = [&](int64_t jj) {
-    const int64_t b = grp + jj * groups;
+    const int64_t b = bof(jj);
     const double* c = a.contracts + b * width;
-    const double* xs = xsum + (jj % kRSlots) * W * A;
+    const double* xs = xsum + (jj % kRSlots) * XS;
     const uint32_t want = static_cast<uint32_t>(W) * static_cast<uint32_t>(jj + 1);
     uint32_t spins = 0;
     while (get_sc1(cnt) < want && ++spins < kRSpinLimit) __builtin_amdgcn_s_sleep(2);
@@ -438,6 +482,11 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
     if (lane == 0) {
       pco[A] = math::exp_any(static_cast<float>(-c[2]) * static_cast<float>(c[1]));
       pco[A + 1] = static_cast<float>(c[0]);
+      if (dyn && jj + 2 >= S) {  // the contract of iteration jj + 2 (slice 0 took it) and its coefficients
+        const int64_t nb = spins < kRSpinLimit ? get_sc1(reinterpret_cast<const int64_t*>(xs + W * A)) : a.B;
+        bidx[(jj + 2) & 3] = nb;
+        if (nb < a.B) coefs(nb, dco + ((jj + 2) & 1) * CS);
+      }
     }
   };
   // step 2 (all waves, after a barrier that made pco visible): basket put of contract jj from the
@@ -460,7 +509,7 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
       part[g * N + 4 * q + e] = static_cast<double>(df * (diff > 0.0f ? diff : 0.0f));
     }
     lds_barrier();
-    double* xc = xcol + ((grp + jj * groups) * W + slc) * static_cast<int64_t>(N);
+    double* xc = xcol + (bof(jj) * W + slc) * static_cast<int64_t>(N);
     for (int n = tid; n < N; n += kRThreads) {
       double t = 0.0;
       for (int gg = 0; gg < G; ++gg) t += part[gg * N + n];
@@ -468,37 +517,22 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
     }
   };
 
-  for (int64_t jj = 0; jj < n_own; ++jj) {
-    const int64_t b = grp + jj * groups;
+  const int64_t n_tab = dyn ? S : (a.B > grp ? (a.B - 1 - grp) / groups + 1 : 0);  // static iterations
+  int64_t n_iter = 0;
+  for (int64_t jj = 0;; ++jj) {
+    const int64_t b = bof(jj);  // uniform (LDS ring, written before the last barrier)
+    if (b >= a.B) break;
+    n_iter = jj + 1;
     float* tab = table + ((jj / kRTable) & 1) * kRTable * CS;
-    if (jj % kRTable == 0) {
-      // wave 0 fills the coefficient table of the next 64 contracts, one per lane (f64 Cholesky,
-      // coefficients rounded once to f32)
+    if (jj < n_tab && jj % kRTable == 0) {
+      // wave 0 fills the coefficient table of the next 64 static contracts, one per lane
       const int64_t jl = jj + lane;
-      if (wave == 0 && jl < n_own) {
-        const double* c = a.contracts + (grp + jl * groups) * width;
-        double L[kMaxAssets * kMaxAssets];
-        cholesky_equicorr(A, c[3], L);
-        const double dt = c[1] / static_cast<double>(kRowBlock);
-        const double sq = sqrt(dt);
-        constexpr double zscale = HW ? PathStream::kNormalScale<true> : 1.0;
-        float* e = tab + lane * CS;
-#pragma unroll
-        for (int i = 0; i < A; ++i) {
-          const double v = c[4 + 2 * A + i], d = c[4 + A + i];
-          const double drift = c[2] - d - 0.5 * v * v;
-          e[i] = static_cast<float>(drift * dt * kBLog2e);
-          e[A + i] = static_cast<float>(c[4 + i]);
-          const double bi = v * sq * kBLog2e * zscale;
-#pragma unroll
-          for (int k = 0; k < A; ++k) e[2 * A + i * A + k] = k <= i ? static_cast<float>(bi * L[i * kMaxAssets + k]) : 0.0f;
-        }
-      }
+      if (wave == 0 && jl < n_tab) coefs(grp + jl * groups, tab + lane * CS);
       lds_barrier();
     }
     // 0. wave 0: contract jj - 1's scales (the other waves start simulating)
     if (jj > 0 && wave == 0) gather(jj - 1);
-    const float* e = tab + (jj % kRTable) * CS;
+    const float* e = jj < n_tab ? tab + (jj % kRTable) * CS : dco + (jj & 1) * CS;
     float ca[A], x0[A], Lb[A][A];
 #pragma unroll
     for (int i = 0; i < A; ++i) {
@@ -569,19 +603,24 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
       if (lane < A) {
         double t = 0.0;
         for (int w2 = 0; w2 < kRWaves; ++w2) t += wsum[w2 * A + lane];
-        put_sc1(xsum + (jj % kRSlots) * W * A + slc * A + lane, t);
+        put_sc1(xsum + (jj % kRSlots) * XS + slc * A + lane, t);
       }
+      if (dyn && slc == 0 && lane == 0 && jj + 2 >= S)  // the group's contract of iteration jj + 2
+        put_sc1(reinterpret_cast<int64_t*>(xsum + (jj % kRSlots) * XS + W * A), n_static + atomicAdd(queue, 1u));
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     lds_barrier();  // part / wsum are rewritten from here on
   }
 #if !defined(SMC_BASKET_RES_NO_EXCHANGE)
-  if (n_own > 0) {  // the last contract
-    if (wave == 0) gather(n_own - 1);
+  if (n_iter > 0) {  // the last contract
+    if (wave == 0) gather(n_iter - 1);
     lds_barrier();
-    payoff(n_own - 1);
+    payoff(n_iter - 1);
   }
+#endif
+#if defined(SMC_EXPERIMENT_TRACE)
+  if (tid == 0 && blockIdx.x < 1024) g_btrace[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
 #endif
   if (tid == 0) {
     // every workgroup made its last exchange before it arrives here: the last one resets the
@@ -590,6 +629,7 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
     uint32_t* done = reinterpret_cast<uint32_t*>(ra.sync);
     if (atomicAdd(done, 1u) == gridDim.x - 1) {
       for (int k = 0; k < groups; ++k) reinterpret_cast<uint32_t*>(ra.sync + 128 + 128 * static_cast<int64_t>(k))[0] = 0u;
+      *queue = 0u;
       *done = 0u;
     }
   }
@@ -784,6 +824,12 @@ using namespace smc;
 
 extern "C" {
 #pragma GCC visibility push(default)
+#if defined(SMC_EXPERIMENT_TRACE)
+int32_t smc_debug_btrace(uint64_t* host, int64_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(smc::g_btrace), static_cast<size_t>(n) * sizeof(uint64_t)) == hipSuccess
+             ? 0 : 1;
+}
+#endif
 
 int32_t smc_basket_train_targets(const double* contracts_dev, int64_t n_contracts, int32_t n_assets,
                                  int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,

@@ -59,11 +59,13 @@ def test_portable_bit_exact_vs_oracle(oracle, A, T, resident) -> None:
 
 
 @pytest.mark.parametrize("A,N,M,B", [(4, 256, 512, 11), (4, 256, 64, 150), (2, 1024, 16, 40), (1, 4, 2048, 5),
-                                     (6, 256, 32, 9), (3, 2048, 6, 17)])
+                                     (6, 256, 32, 9), (3, 2048, 6, 17), (4, 256, 512, 40), (2, 256, 64, 260)])
 def test_resident_sliced_bit_exact(oracle, A, N, M, B) -> None:
     """basket_resident_kernel with W = N*M/4096 workgroups per contract: C5's shape (W = 32, 8 groups,
     B = 11: some groups run two contracts, some one), several rounds per group (B = 150, W = 4), N = 4
-    and N = 2048 (the extremes of the column mapping), A = 6 (the largest whose LDS plan fits), a non-power-of-two W (3)."""
+    and N = 2048 (the extremes of the column mapping), A = 6 (the largest whose LDS plan fits), a non-power-of-two W (3);
+    B = 40 at C5 (5 contracts per group) and B = 260 at W = 4: the dynamic tail (contracts of the last quarter of
+    the rounds taken from the queue)."""
     cfg = BasketConfig(n_assets=A, timesteps=16, network_size=N, batches_per_mc_run=M, math="portable")
     wg, W = oracle.basket_order(A, 16, N, M)
     assert wg == 1024 and W == N * M // 4096

@@ -29,6 +29,7 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
     ap.add_argument("--split", action="store_true", help="no sync area: the basket_kernel (+ CF) launches")
+    ap.add_argument("--trace", default="", help="save per-workgroup [start, xcc, group, end] (SMC_EXPERIMENT_TRACE builds)")
     a = ap.parse_args()
     cfg = BasketConfig(n_assets=a.A, timesteps=a.T, network_size=a.N, batches_per_mc_run=a.M, math=a.math)
     lo, hi = cfg.arrays()
@@ -58,6 +59,13 @@ def main() -> None:
         launch()
     e1.record()
     torch.cuda.synchronize()
+    if a.trace:
+        import ctypes
+        buf = np.zeros((1024, 4), dtype=np.uint64)
+        fn = L.smc_debug_btrace
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        assert fn(buf.ctypes.data, buf.size) == 0
+        np.save(a.trace, buf)
     kname = L.smc_basket_train_targets_kernel(a.A, a.T, a.N, a.M, 1 if ns else 0, 0).decode()
     print(f"basket A={a.A} {a.math} {a.store} {kname}: {e0.elapsed_time(e1) / a.iters:.3f} ms/launch checksum",
           float(tg.abs().double().mean()))
