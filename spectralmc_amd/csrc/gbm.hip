@@ -753,7 +753,10 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   // (sliced, W > 1: slice 0 takes the group's next contract during the current contract's
   // terminal-sum exchange, and the partners read it with the sums; only once every group has a
   // static contract, n_static > 0)
-  const int64_t n_static0 = (a.B / groups) * 3 / 4 * groups;
+#ifndef SMC_RES_STATIC_QUARTERS
+#define SMC_RES_STATIC_QUARTERS 3  // statically assigned share of the contract rounds, in quarters
+#endif
+  const int64_t n_static0 = (a.B / groups) * SMC_RES_STATIC_QUARTERS / 4 * groups;
   const bool dyn = a.res_queue != nullptr && (W == 1 || n_static0 > 0);
   const int64_t n_static = dyn ? n_static0 : a.B;
   auto grab = [&]() -> int64_t {
