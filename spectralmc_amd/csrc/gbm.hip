@@ -684,8 +684,11 @@ constexpr size_t kResTermBytes = static_cast<size_t>(kResLdsChunks) * kResThread
 constexpr int kResMaxSlices = 8;
 constexpr uint32_t kResSpinLimit = 1u << 20;  // ~1 s of polling: a partner that never arrives gives NaN targets
 
+constexpr int kResPreDraw = 32;  // static contracts whose Sobol rows are drawn at kernel start
+
 size_t resident_lds_bytes(int N) {
-  return kResTermBytes + (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 9) * sizeof(double);
+  return kResTermBytes +
+         (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 9 + 6 * kResPreDraw) * sizeof(double);
 }
 
 #if defined(SMC_EXPERIMENT_TRACE)  // tools/micro decomposition builds only: per-workgroup timestamps
@@ -734,7 +737,8 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   double* sn = cs + N;                    // [N]
   double* row = sn + N;                   // [6] this contract's drawn Sobol row (fused step); [6]
                                           // the exchanged terminal sum, [7] the last-arriver flag,
-                                          // [8] the next dynamically handed-out contract
+                                          // [8] the next dynamically handed-out contract;
+  double* pre = row + 9;                  // [kResPreDraw][6] Sobol rows of the first static contracts
   SMC_TRACE(0);
 #if defined(SMC_EXPERIMENT_TRACE)
   if (tid == 0 && blockIdx.x < 1024) {
@@ -770,9 +774,31 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     if (W == 1) return grab();
     return reinterpret_cast<const int64_t*>(row + 8)[0];  // learned in this contract's exchange
   };
+  // the Sobol rows of the first kResPreDraw static contracts are drawn here, before any path store:
+  // a global load in a wave waits for that wave's outstanding stores (one vmcnt counter), so a
+  // per-contract draw made wave 0 drain its store queue at every contract start
+  int64_t n_pre = 0;
+  if (a.sobol) {
+    const int64_t mine = grp < n_static ? (n_static - 1 - grp) / groups + 1 : 0;
+    n_pre = mine < kResPreDraw ? mine : kResPreDraw;
+    for (int t = tid; t < n_pre * 6; t += kResThreads) {
+      const int k = t / 6, d = t % 6;
+      const int64_t bb = grp + static_cast<int64_t>(k) * groups;
+      const double v = sobol_coord(a.sobol, a.sobol_dim, d, static_cast<uint64_t>(sob0 + bb), a.lower, a.upper);
+      pre[t] = v;
+      if (slc == 0) {
+        a.contracts_out[bb * 6 + d] = v;
+        if (a.cvnn_out) a.cvnn_out[bb * 6 + d] = static_cast<float>(v);
+      }
+    }
+    lds_barrier();
+  }
   for (int64_t b = grp < n_static ? grp : (dyn ? grab() : a.B); b < a.B; b = next(b), ++round) {
     Contract c;
-    if (a.sobol) {  // draw the contract (sobol_sampler.py:222-246) instead of a separate kernel
+    if (a.sobol && static_cast<int64_t>(round) < n_pre) {  // drawn at kernel start
+      const double* r = pre + static_cast<int64_t>(round) * 6;
+      c = Contract{r[0], r[1], r[2], r[3], r[4], r[5]};
+    } else if (a.sobol) {  // draw the contract (sobol_sampler.py:222-246) instead of a separate kernel
       if (tid < 6) {
         const double v = sobol_coord(a.sobol, a.sobol_dim, tid, static_cast<uint64_t>(sob0 + b), a.lower, a.upper);
         row[tid] = v;
