@@ -11,10 +11,12 @@ M-batch mean + N-point DFT -> targets, CVNN forward/backward, Adam, grad norm.  
 every rank processes B contracts per step (contract-sharded data parallel, one RCCL all-reduce).
 
 Rank 0 prints ONE JSON line.  `value` = contracts x paths per second over the whole job.
-The roofline object is for the dominant kernel (the fused path/CF kernel: contract_kernel, or
-basket_kernel at C5),
-timed with HIP events on its own stream after the timed region; `cpu_baseline` is the
-oracle (CPU restatement: C/OpenMP paths + numpy.fft + torch-cpu CVNN) on a bounded sample.
+The roofline object is for the dominant kernel (the MC part of the step: resident_kernel at C2,
+its sliced form at C3, basket_resident_kernel at C5): algorithmic bytes per launch over the
+average duration of the MC launches inside the timed region (HIP events on the MC stream);
+`kernel_ms_isolated` is the same launch alone after the timed region.  `cpu_baseline` is the
+reference CPU path (torch-cpu + numpy.fft, oracle/torch_cpu.py) on a bounded sample, with the
+C/OpenMP oracle as a second leg and C1 timed over 10 whole steps.
 """
 
 from __future__ import annotations
