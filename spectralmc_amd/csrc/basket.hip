@@ -413,7 +413,10 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
   // finish times differed by up to 15 % with a static split).  Slice 0 takes the contract of
   // iteration j + 2 while publishing iteration j's slice sums; the partners read it with those sums
   // in iteration j + 1 (no added wait).
-  const int64_t S = (a.B / groups) * 3 / 4;
+#ifndef SMC_BASKET_STATIC_QUARTERS
+#define SMC_BASKET_STATIC_QUARTERS 3  // statically assigned share of the iterations, in quarters
+#endif
+  const int64_t S = (a.B / groups) * SMC_BASKET_STATIC_QUARTERS / 4;
   const bool dyn = S >= 2;
   const int64_t n_static = dyn ? S * groups : a.B;
   uint32_t* queue = reinterpret_cast<uint32_t*>(ra.sync + 64);
