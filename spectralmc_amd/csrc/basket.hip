@@ -12,9 +12,10 @@
 // Correlation matrix C = (1 - rho) I + rho 11^T, factored C = L L^T once per workgroup in LDS.
 //
 // Layout: paths [B][A][T][pitch] f32 (STORE_ALL) or [B][A][pitch] (terminal rows only), so each
-// asset's block is a single-asset [T][P] matrix.  One 512-thread workgroup per contract; each
-// lane owns 4 consecutive paths of a 2048-path chunk for all A assets and stores one dwordx4
-// per (asset, row).
+// asset's block is a single-asset [T][P] matrix.  basket_kernel: one 512-thread workgroup per
+// contract; each lane owns 4 consecutive paths of a 2048-path chunk for all A assets and stores
+// one dwordx4 per (asset, row).  basket_resident_kernel (the C5 kernel, below): W = P / 4096
+// co-resident 1024-thread workgroups per contract keep the terminal rows on chip.
 //
 // Per lane, per step t, per path j = 0..3: ceil(A/2) Box-Muller pairs from the lane's
 // PathStream (smc_rng.h; the same (seed, contract ordinal, group) keying as the single-asset
