@@ -107,20 +107,54 @@ __device__ void fft_row(const double* avg, const double* cs, const double* sn, i
     xi[r] = 0.0;
   }
   barrier();
-  for (int s = 1; s <= logN; ++s) {
+  // one radix-2 butterfly on registers, the operations of the stage loop in the same order
+  auto bfly = [](double& br, double& bi, double& ar, double& ai, double wr, double wi) {
+    const double tr = ar * wr - ai * wi;
+    const double ti = ar * wi + ai * wr;
+    ar = br - tr;
+    ai = bi - ti;
+    br = br + tr;
+    bi = bi + ti;
+  };
+  // stages s and s + 1 fused per thread on the quad i0, i0 + h, i0 + 2h, i0 + 3h (h = 2^(s-1)): the
+  // same butterflies with the same twiddles as two radix-2 stages, one barrier instead of two
+  int s = 1;
+  for (; s + 1 <= logN; s += 2) {
+    const int h = 1 << (s - 1), shift = logN - s;
+    for (int qd = tid; qd < N / 4; qd += NT) {
+      const int pos = qd & (h - 1);
+      const int i0 = ((qd >> (s - 1)) << (s + 1)) + pos;
+      double r0 = xr[i0], m0 = xi[i0], r1 = xr[i0 + h], m1 = xi[i0 + h];
+      double r2 = xr[i0 + 2 * h], m2 = xi[i0 + 2 * h], r3 = xr[i0 + 3 * h], m3 = xi[i0 + 3 * h];
+      const double w1r = cs[pos << shift], w1i = -sn[pos << shift];
+      bfly(r0, m0, r1, m1, w1r, w1i);  // stage s: (i0, i0 + h), (i0 + 2h, i0 + 3h)
+      bfly(r2, m2, r3, m3, w1r, w1i);
+      const double w2r = cs[pos << (shift - 1)], w2i = -sn[pos << (shift - 1)];
+      const double w3r = cs[(pos + h) << (shift - 1)], w3i = -sn[(pos + h) << (shift - 1)];
+      bfly(r0, m0, r2, m2, w2r, w2i);  // stage s + 1: (i0, i0 + 2h), (i0 + h, i0 + 3h)
+      bfly(r1, m1, r3, m3, w3r, w3i);
+      xr[i0] = r0;
+      xi[i0] = m0;
+      xr[i0 + h] = r1;
+      xi[i0 + h] = m1;
+      xr[i0 + 2 * h] = r2;
+      xi[i0 + 2 * h] = m2;
+      xr[i0 + 3 * h] = r3;
+      xi[i0 + 3 * h] = m3;
+    }
+    barrier();
+  }
+  if (s == logN) {  // an odd number of stages: the last one alone
     const int h = 1 << (s - 1), shift = logN - s;  // twiddle index t = (j mod h) << shift
     for (int j = tid; j < N / 2; j += NT) {
       const int pos = j & (h - 1);
       const int i0 = ((j >> (s - 1)) << s) + pos, i1 = i0 + h;
-      const double wr = cs[pos << shift], wi = -sn[pos << shift];
-      const double ar = xr[i1], ai = xi[i1];
-      const double tr = ar * wr - ai * wi;
-      const double ti = ar * wi + ai * wr;
-      const double br = xr[i0], bi = xi[i0];
-      xr[i1] = br - tr;
-      xi[i1] = bi - ti;
-      xr[i0] = br + tr;
-      xi[i0] = bi + ti;
+      double br = xr[i0], bi = xi[i0], ar = xr[i1], ai = xi[i1];
+      bfly(br, bi, ar, ai, cs[pos << shift], -sn[pos << shift]);
+      xr[i1] = ar;
+      xi[i1] = ai;
+      xr[i0] = br;
+      xi[i0] = bi;
     }
     barrier();
   }
