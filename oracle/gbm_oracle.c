@@ -10,7 +10,7 @@
  *   normals   reference src/spectralmc/async_normals.py:212-216 draws a (T, P) N(0,1) matrix
  *             per contract from CuPy XORWOW (absent here: normal-level parity with CuPy is
  *             unpinned).  Here: Philox4x32-10 (Salmon et al., SC'11; KAT-pinned in tests)
- *             seeds xoshiro128+ (Blackman & Vigna) per (contract ordinal, group of 4 paths);
+ *             seeds MWC64X (Thomas 2011) per (contract ordinal, group of 4 paths);
  *             per step pair, the group's 4 paths draw one Box-Muller pair each, in path order.
  *             f32: ln / sin / cos from the portable IEEE-only kernels below (bit-identical
  *             to the device's); f64: libm.
@@ -62,26 +62,21 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
   out[3] = c3;
 }
 
+/* MWC64X (D. B. Thomas, "The MWC64X random number generator", 2011): multiply-with-carry with
+ * multiplier A = 4294883355 and base 2^32, state (x, c), output x ^ c, then (x, c) <- A x + c.
+ * Period ~2^63; one 32x32->64 multiply-add per output on the device. */
+#define MWC_A 4294883355u
 typedef struct {
-  uint32_t s[4];
-} xoshiro128;
+  uint32_t x, c;
+} mwc64x;
 
-static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
-
-/* xoshiro128+ 1.0, reference implementation order. */
-static inline uint32_t xoshiro_next(xoshiro128* g) {
-  uint32_t* s = g->s;
-  const uint32_t result = s[0] + s[3];
-  const uint32_t t = s[1] << 9;
-  s[2] ^= s[0];
-  s[3] ^= s[1];
-  s[1] ^= s[2];
-  s[0] ^= s[3];
-  s[2] ^= t;
-  s[3] = rotl32(s[3], 11);
-  return result;
+static inline uint32_t mwc_next(mwc64x* g) {
+  const uint32_t r = g->x ^ g->c;
+  const uint64_t t = (uint64_t)MWC_A * g->x + g->c;
+  g->x = (uint32_t)t;
+  g->c = (uint32_t)(t >> 32);
+  return r;
 }
-
 
 /* ---- portable f32 math: op-for-op restatement of spectralmc_amd/csrc/smc_math.h ------
  * (coefficients from tools/fit_poly.py; compile with -ffp-contract=off) */
@@ -189,17 +184,31 @@ void oracle_sincos2pi_u24(uint32_t j, float* s, float* c) { sincos2pi_u24(j, s, 
 
 #define GROUP 4  /* paths per stream */
 
-static void path_stream(uint64_t seed, uint64_t ordinal, uint64_t group, xoshiro128* g) {
+/* Stream seed: words 0 and 1 of Philox4x32-10(counter = (group, ordinal), key = seed) give x and
+ * c (reduced below A); the two absorbing states (0, 0) and (2^32 - 1, A - 1) are moved off. */
+static void path_stream(uint64_t seed, uint64_t ordinal, uint64_t group, mwc64x* g) {
   const uint32_t ctr[4] = {(uint32_t)group, (uint32_t)(group >> 32), (uint32_t)ordinal, (uint32_t)(ordinal >> 32)};
   const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-  oracle_philox4x32_10(ctr, key, g->s);
-  if ((g->s[0] | g->s[1] | g->s[2] | g->s[3]) == 0u) g->s[0] = 1u;
+  uint32_t out[4];
+  oracle_philox4x32_10(ctr, key, out);
+  g->x = out[0];
+  g->c = out[1] >= MWC_A ? out[1] - MWC_A : out[1];
+  if ((g->x | g->c) == 0u) g->x = 1u;
+  if (g->x == 0xFFFFFFFFu && g->c == MWC_A - 1u) g->x = 0xFFFFFFFEu;
+}
+
+/* The first n u32 outputs of the stream of (seed, ordinal, group): tests pin it to a Python
+ * restatement of the published MWC64X recurrence on the KAT-pinned Philox seed. */
+void oracle_stream_u32(uint64_t seed, uint64_t ordinal, uint64_t group, int64_t n, uint32_t* out) {
+  mwc64x g;
+  path_stream(seed, ordinal, group, &g);
+  for (int64_t i = 0; i < n; ++i) out[i] = mwc_next(&g);
 }
 
 /* One Box-Muller pair.  f32: 23-bit uniforms and the portable kernels (bit-identical to the
  * device); f64: 32-bit uniforms and libm. */
-static void normal_pair(xoshiro128* g, int is_f64, double* z0, double* z1) {
-  const uint32_t a = xoshiro_next(g), b = xoshiro_next(g);
+static void normal_pair(mwc64x* g, int is_f64, double* z0, double* z1) {
+  const uint32_t a = mwc_next(g), b = mwc_next(g);
   if (is_f64) {
     const double u1 = ((double)a + 1.0) * 0x1p-32;
     const double u2 = (double)b * 0x1p-32;
@@ -220,7 +229,7 @@ static void normal_pair(xoshiro128* g, int is_f64, double* z0, double* z1) {
 
 /* Normals of one group of 4 paths: z[t][j] for t < rows (f64 holder of dtype values). */
 static void group_normals(uint64_t seed, uint64_t ordinal, uint64_t group, int32_t rows, int is_f64, double* z) {
-  xoshiro128 g;
+  mwc64x g;
   path_stream(seed, ordinal, group, &g);
   for (int t = 0; t < rows; t += 2)
     for (int j = 0; j < GROUP; ++j) {
@@ -626,7 +635,7 @@ void oracle_basket_kernel(const double* contracts, int64_t B, int32_t A, int32_t
     const int64_t groups = P / GROUP;
 #pragma omp parallel for schedule(static)
     for (int64_t gi = 0; gi < groups; ++gi) {
-      xoshiro128 g;
+      mwc64x g;
       path_stream(seed, ordinal, (uint64_t)gi, &g);
       float x[B_MAX_ASSETS][GROUP];
       for (int i = 0; i < A; ++i)

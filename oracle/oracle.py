@@ -12,7 +12,8 @@ Pieces and what pins them
   scipy 1.15.3 here; ``sobol_sampler.py:192,197,238-239``).  Pinned by golden vectors made
   with the reference's ``SobolSampler`` (tests/golden/make_golden.py).
 * Normals + paths  -> ``oracle/gbm_oracle.c`` (f64 recursion / dtype stores as the Numba
-  kernel, ``gbm.py:241-257``).  Philox pinned by Random123 KAT vectors; normal-level parity
+  kernel, ``gbm.py:241-257``).  Philox pinned by Random123 KAT vectors, the MWC64X stream by a
+  Python restatement of its recurrence (tests/test_oracle.py); normal-level parity
   with CuPy XORWOW is unpinned (CuPy absent).  The path arithmetic is additionally pinned by
   closed-form cases (v = 0, T = 0) and the reference test's Black-price acceptance
   (``tests/test_gbm.py:103-139``).
@@ -53,6 +54,8 @@ def lib() -> ctypes.CDLL:
             build()
         L = ctypes.CDLL(_LIB_PATH)
         L.oracle_philox4x32_10.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_stream_u32.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64,
+                                        ctypes.c_void_p]
         L.oracle_normals.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
                                      ctypes.c_int32, ctypes.c_void_p]
         L.oracle_gbm_paths.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64,
@@ -93,6 +96,13 @@ def philox4x32_10(ctr: tuple[int, int, int, int], key: tuple[int, int]) -> tuple
     out = np.zeros(4, dtype=np.uint32)
     lib().oracle_philox4x32_10(_ptr(c), _ptr(k), _ptr(out))
     return tuple(int(x) for x in out)
+
+
+def stream_u32(seed: int, ordinal: int, group: int, n: int) -> np.ndarray:
+    """The first n u32 outputs of the (seed, ordinal, group) path stream (csrc/smc_rng.h)."""
+    out = np.empty(n, dtype=np.uint32)
+    lib().oracle_stream_u32(seed, ordinal, group, n, _ptr(out))
+    return out
 
 
 def normals(seed: int, ordinal: int, rows: int, cols: int, dtype: str = "float32") -> np.ndarray:

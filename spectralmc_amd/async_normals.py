@@ -6,7 +6,7 @@ matrices on their own streams; matrix m (the m-th served, ``skips`` restores the
 ``numpy.random.default_rng(seed).integers(0, 1e9)``.
 
 Here matrix m is the normal matrix the HIP engine itself draws for contract ordinal m
-(``smc_normals``: Philox-keyed xoshiro128+ streams + Box-Muller, csrc/smc_rng.h), so the
+(``smc_normals``: Philox-seeded MWC64X streams + Box-Muller, csrc/smc_rng.h), so the
 generator and ``BlackScholes`` agree on every value, the matrices never cross PCIe, and
 ``skips`` restores a position in O(1).  The pool / stream / buffer-size structure, config
 validation and error values are the reference's; the values are not CuPy's (normal-level

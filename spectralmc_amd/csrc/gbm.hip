@@ -949,7 +949,7 @@ bool resident_ok(const EngineArgs& a, bool f32) {
   const int64_t W = a.res_slices > 1 ? a.res_slices : 1;
   return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T == kRowBlock &&
          W <= kResMaxSlices && a.P % (W * kResChunk) == 0 && a.P / (W * kResChunk) <= kResMaxChunks &&
-         a.N >= 4 && a.N <= 1024 && kResChunk % a.N == 0 && (a.pitch == 0 || a.pitch % 4 == 0) &&
+         a.N >= 4 && a.N <= 1024 && kResChunk % a.N == 0 && (a.pitch == 0 || (a.pitch % 4 == 0 && a.pitch >= a.P)) &&
          (W == 1 || (a.res_cnt && a.res_xsum && a.res_xcol && a.done));
 }
 
@@ -1438,6 +1438,8 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
     return fail(SMC_ERR_INVALID_SHAPE, "smc_train_step: network_size and batches_per_mc_run must be > 0");
   const hipStream_t s = as_stream(stream);
   const int64_t P = static_cast<int64_t>(network_size) * batches_per_mc_run;
+  if (path_pitch != 0 && (path_pitch < P || (path_pitch != P && path_pitch % kPathsPerLane != 0)))
+    return fail(SMC_ERR_INVALID_SHAPE, "smc_train_step: path_pitch must be 0, P, or a multiple of 4 >= P");
   const int64_t need = smc_train_step_sync_bytes(timesteps, network_size, batches_per_mc_run, dtype, path_pitch);
   if (need <= 0) return fail(SMC_ERR_HIP, "smc_train_step: device query failed");
   if (sync_bytes < need) return fail(SMC_ERR_INVALID_SHAPE, "smc_train_step: sync area smaller than smc_train_step_sync_bytes");

@@ -8,9 +8,8 @@
 //   paths are grouped g = p / 4 (a lane's 4 paths); one stream per (contract ordinal, group):
 //   seed state  = Philox4x32-10( counter = (g_lo, g_hi, ordinal_lo, ordinal_hi),
 //                                key     = (mc_seed_lo, mc_seed_hi) )      [Salmon et al. 2011]
-//   u32 stream  = xoshiro128+ seeded with that 128-bit state            [Blackman & Vigna 2018]
-//                 (only the top 23 bits of each output are used: the "+" scrambler's weak
-//                 low bits never reach a normal)
+//   u32 stream  = MWC64X seeded with Philox words (0, 1)                  [Thomas 2011]
+//                 (x, c) <- A x + c (mod 2^64 split into (x, c)), output x ^ c, A = 4294883355
 //   normals     = Box-Muller on consecutive u32 pairs (a, b):
 //                   u1 = 2 - 1.m(a >> 9) in (0, 1],  angle = (b >> 9) 2^-23 revolutions       (f32)
 //                   u1 = (a + 1) * 2^-32,                   u2 = b * 2^-32                    (f64)
@@ -22,8 +21,10 @@
 //   made and discarded, so the stream position never depends on P.
 //
 // Philox runs once per group (its round keys are wave-uniform, so the key schedule lives in
-// SGPRs) and is amortised over 4 paths x T steps; each further u32 costs 7 integer VALU ops
-// (v_bitop3_b32 xor3) with no 32-bit multiply.  oracle/gbm_oracle.c restates the same stream on the CPU.
+// SGPRs) and is amortised over 4 paths x T steps; each further u32 is one v_mad_u64_u32 plus an
+// xor (and a register move): measured on gfx950 the round-2 xoshiro128+ step (three v_bitop3, an
+// add, a xor, a shift and a rotate) cost ~2x as many VALU cycles per output
+// (tools/micro/valurate.hip).  oracle/gbm_oracle.c restates the same stream on the CPU.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -52,29 +53,29 @@ __device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32
 }
 
 struct PathStream {
-  uint32_t s0, s1, s2, s3;
+  // MWC64X (Thomas 2011): multiply-with-carry, base 2^32, multiplier kMwcA; state (x, c) with
+  // c < kMwcA; output x ^ c, then (x, c) <- kMwcA x + c as one v_mad_u64_u32.
+  static constexpr uint32_t kMwcA = 4294883355u;
+  uint32_t x, c;
 
+  // seed: words 0, 1 of Philox4x32-10(counter = (group, ordinal), key = mc_seed); the absorbing
+  // states (0, 0) and (2^32 - 1, kMwcA - 1) are moved off
   __device__ __forceinline__ PathStream(uint64_t mc_seed, uint64_t ordinal, uint64_t group) {
-    s0 = static_cast<uint32_t>(group);
-    s1 = static_cast<uint32_t>(group >> 32);
-    s2 = static_cast<uint32_t>(ordinal);
-    s3 = static_cast<uint32_t>(ordinal >> 32);
+    uint32_t s0 = static_cast<uint32_t>(group), s1 = static_cast<uint32_t>(group >> 32);
+    uint32_t s2 = static_cast<uint32_t>(ordinal), s3 = static_cast<uint32_t>(ordinal >> 32);
     philox4x32_10(s0, s1, s2, s3, static_cast<uint32_t>(mc_seed), static_cast<uint32_t>(mc_seed >> 32));
-    s0 |= static_cast<uint32_t>((s0 | s1 | s2 | s3) == 0u);  // xoshiro forbids the zero state
+    x = s0;
+    c = s1 >= kMwcA ? s1 - kMwcA : s1;
+    x |= static_cast<uint32_t>((x | c) == 0u);
+    x ^= static_cast<uint32_t>(x == 0xFFFFFFFFu && c == kMwcA - 1u);
   }
 
-  // xoshiro128+ 1.0 with the three xor chains merged into v_bitop3_b32 (xor3): 7 VALU ops.
   __device__ __forceinline__ uint32_t next() {
-    const uint32_t result = s0 + s3;
-    const uint32_t t = s1 << 9;
-    const uint32_t n1 = __builtin_amdgcn_bitop3_b32(s1, s2, s0, 0x96);  // s1 ^ (s2 ^ s0)
-    const uint32_t n0 = __builtin_amdgcn_bitop3_b32(s0, s3, s1, 0x96);  // s0 ^ (s3 ^ s1)
-    const uint32_t n2 = __builtin_amdgcn_bitop3_b32(s2, s0, t, 0x96);   // (s2 ^ s0) ^ t
-    s3 = __builtin_rotateleft32(s3 ^ s1, 11);
-    s0 = n0;
-    s1 = n1;
-    s2 = n2;
-    return result;
+    const uint32_t r = x ^ c;
+    const uint64_t t = static_cast<uint64_t>(kMwcA) * x + c;
+    x = static_cast<uint32_t>(t);
+    c = static_cast<uint32_t>(t >> 32);
+    return r;
   }
 
   // Scale of the f32 normal_pair<HW> output: HW returns z / sqrt(2 ln 2) (the constant is
@@ -134,14 +135,7 @@ struct PathStream {
       c[j] = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, eb, 9)) - 1.5f;
       sn[j] = c[j] * 0.5f;
 #else
-#if defined(SMC_EXPERIMENT_NO_RNG)
-      s0 += 0x9E3779B9u;
-      const uint32_t ua = s0, ub = s0 ^ s1;
-#elif defined(SMC_EXPERIMENT_HALF_RNG)  // timing only: one generator step per Box-Muller pair
-      const uint32_t ua = next(), ub = __builtin_rotateleft32(ua, 16) ^ 0x9E3779B9u;
-#else
       const uint32_t ua = next(), ub = next();
-#endif
       const float u1 = 2.0f - __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ua, 9));
       r[j] = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u1));
       const float w = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ub, 9));

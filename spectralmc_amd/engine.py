@@ -114,11 +114,14 @@ class TrainingEngine:
         # smc_train_step's sync area (arrival counters; the sliced resident kernel's exchanged sums),
         # zero-filled once; every step leaves its counters zeroed
         self._uses_train_step = self._f32_in and self.dim == 6 and self._workspace is None
-        sync = int(_lib.lib().smc_train_step_sync_bytes(self.T, self.N, self.M, self._dtype_code, self.pitch))
-        if sync < 0:
-            raise RuntimeError("smc_train_step_sync_bytes: device query failed")
-        self._sync = torch.zeros(max(sync, 8), dtype=torch.uint8, device=device)
-        self._sync_bytes = sync
+        self._sync: torch.Tensor | None = None
+        self._sync_bytes = 0
+        if self._uses_train_step:
+            sync = int(_lib.lib().smc_train_step_sync_bytes(self.T, self.N, self.M, self._dtype_code, self.pitch))
+            if sync < 0:
+                raise RuntimeError("smc_train_step_sync_bytes: device query failed")
+            self._sync = torch.zeros(max(sync, 8), dtype=torch.uint8, device=device)
+            self._sync_bytes = sync
         # the path/CF kernel the step runs for this shape (bench labels, rocprof cross-check)
         if self._uses_train_step:
             self.kernel_name = _lib.lib().smc_train_step_kernel(self.T, self.N, self.M, self._dtype_code,

@@ -129,6 +129,11 @@ def test_engine_argument_errors_do_not_launch() -> None:
         _lib.SMC_ERR_INVALID_SHAPE
     assert L.smc_train_targets(p, 4, 16, 8, 4, 7, None, 0, 0, 1, 0, 2, p, 34, 4, None, p, None, 0, None) == \
         _lib.SMC_ERR_INVALID_SHAPE
+    # smc_train_step checks the pitch before choosing the fused resident launch: a pitch below P
+    # would make the contract rows overlap and the last ones write past the caller's buffer
+    for pitch in (4, 65532, 65538):
+        assert L.smc_train_step(p, 6, p, p, p, 0, 0, p, None, 4, 16, 256, 256, 7, 0, 1, 0, 2, p, pitch, 4, p, p, 8,
+                                None) == _lib.SMC_ERR_INVALID_SHAPE, pitch
     assert L.smc_normals(7, 0, 0, 10, 0, p, None) == _lib.SMC_ERR_INVALID_SHAPE
     assert L.smc_sobol_draw(None, 6, None, 0, 4, p, p, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
 

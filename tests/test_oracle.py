@@ -32,6 +32,49 @@ def test_oracle_sobol_matches_reference_sampler(oracle, golden, seed, skip) -> N
     np.testing.assert_array_equal(nxt, golden[f"sobol_s{seed}_k{skip}_next"])
 
 
+MWC_A = 4294883355  # MWC64X multiplier (D. B. Thomas, "The MWC64X random number generator", 2011)
+
+
+def _mwc64x_reference(seed: int, ordinal: int, group: int, n: int) -> list[int]:
+    """The path stream restated in Python integers: Philox4x32-10 (KAT-pinned above) of
+    counter (group, ordinal) under key seed gives the MWC64X state (x, c) = (w0, w1 mod-reduced
+    below A, absorbing states moved off); each output is x ^ c, then x + c 2^32 <- A x + c."""
+    w = (group & 0xFFFFFFFF, group >> 32, ordinal & 0xFFFFFFFF, ordinal >> 32)
+    import oracle as _o
+    p = _o.philox4x32_10(w, (seed & 0xFFFFFFFF, seed >> 32))
+    x, c = p[0], p[1] - MWC_A if p[1] >= MWC_A else p[1]
+    if x == 0 and c == 0:
+        x = 1
+    if x == 0xFFFFFFFF and c == MWC_A - 1:
+        x = 0xFFFFFFFE
+    out = []
+    for _ in range(n):
+        out.append(x ^ c)
+        t = MWC_A * x + c
+        x, c = t & 0xFFFFFFFF, t >> 32
+    return out
+
+
+@pytest.mark.parametrize("seed,ordinal,group", [(7, 0, 0), (7, 3, 16383), (123, 1 << 33, 5), ((1 << 64) - 1, 99, 1 << 40)])
+def test_oracle_stream_is_mwc64x(oracle, seed, ordinal, group) -> None:
+    got = oracle.stream_u32(seed, ordinal, group, 200)
+    assert got.tolist() == _mwc64x_reference(seed, ordinal, group, 200)
+
+
+def test_oracle_stream_bits_are_uniform(oracle) -> None:
+    """Top-23-bit uniforms of 4096 streams x 64 draws (the draws of one C2 chunk): mean, variance and
+    lag-1 / cross-stream correlation at the level a 262,144-sample test resolves."""
+    u = np.stack([oracle.stream_u32(7, 11, g, 64) for g in range(4096)]).astype(np.float64) / 2.0**32
+    assert abs(u.mean() - 0.5) < 3e-3
+    assert abs(u.var() - 1.0 / 12.0) < 2e-3
+    assert abs(np.corrcoef(u[:, :-1].ravel(), u[:, 1:].ravel())[0, 1]) < 8e-3
+    assert abs(np.corrcoef(u[:-1].ravel(), u[1:].ravel())[0, 1]) < 8e-3
+    # every bit position (the kernels use bits 9..31) is a fair coin
+    bits = np.stack([oracle.stream_u32(7, 11, g, 64) for g in range(4096)]).ravel()
+    for b in range(32):
+        assert abs(((bits >> b) & 1).mean() - 0.5) < 4e-3, b
+
+
 def test_oracle_normals_are_standard(oracle) -> None:
     z = oracle.normals(7, 3, 16, 65536).astype(np.float64)
     assert abs(z.mean()) < 5e-3

@@ -63,6 +63,9 @@ for step in "$@"; do
     pmc_hw_term) cd /tmp && run pmc_hw_term 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d "$OUT/pmc_hw_term" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store terminal --unsliced; cd "$ROOT" ;;
     pmc_hw_bytes) cd /tmp && run pmc_hw_bytes 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_hw_bytes" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
     pmc_hw_fetch) cd /tmp && run pmc_hw_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_hw_fetch" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
+    orderbench) run orderbench 240 tools/micro/orderbench ;;
+    valurate) run valurate 120 tools/micro/valurate ;;
+    ab_resident) run ab_resident 900 bash tools/micro/ab_resident.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
