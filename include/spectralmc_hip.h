@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 9
+#define SMC_ABI_VERSION 10
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -47,6 +47,8 @@ extern "C" {
 #define SMC_ERR_SEQUENCE_EXHAUSTED  4  /* Sobol index would pass 2^30 points           */
 #define SMC_ERR_MEMORY_LIMIT        5  /* reference gbm.py:106-137 path-count guard     */
 #define SMC_ERR_HIP                 6  /* HIP runtime error (launch / device)           */
+#define SMC_ERR_EXCHANGE_TIMEOUT    7  /* a co-resident partner workgroup never arrived
+                                          (smc_sync_status; NaN targets were written)     */
 
 /* ---- enums (values mirror the reference enums' order) ------------------- */
 #define SMC_SCHEME_LOG_EULER     0  /* PathScheme.LOG_EULER   effects/montecarlo.py:24-29 */
@@ -67,6 +69,23 @@ typedef struct smc_sobol smc_sobol;
 
 int32_t     smc_abi_version(void);
 const char* smc_last_error_string(void);
+
+/* ---- sync-area status (smc_train_step, smc_basket_train_targets) ---------- */
+/* Launches whose workgroups exchange sums (the sliced resident kernel, the resident basket kernel)
+ * poll for their partners a bounded time (~1 s).  A partner that never arrives (e.g. the group's
+ * workgroups were not all co-resident) sets SMC_SYNC_EXCHANGE_TIMEOUT in the 32-bit status word at
+ * byte SMC_SYNC_STATUS_OFFSET of the sync area; the launch still completes (every later wait of the
+ * launch gives up at once) with NaN targets for the contracts it could not finish.  The word is
+ * sticky across launches: the caller reads (and clears) it with smc_sync_status. */
+#define SMC_SYNC_STATUS_OFFSET     32
+#define SMC_SYNC_EXCHANGE_TIMEOUT  1u
+/* Waits for `stream`, then copies the status word of sync_dev to *status_out (0: no failure) and,
+ * if clear != 0, zeroes it.  The only call of this ABI that synchronises the host. */
+int32_t smc_sync_status(void* sync_dev, int32_t clear, int32_t* status_out, void* stream);
+/* Test hook (tests/test_gpu_engine.py): for the exchanging launches enqueued after this call,
+ * withhold = 1 makes slice W-1 of group 0 skip its first arrival (its partners time out), and
+ * spin_limit (> 0) replaces the ~1 s poll budget.  (0, 0) restores normal operation. */
+int32_t smc_test_exchange_fault(int32_t withhold, uint32_t spin_limit);
 
 /* ---- scrambled Sobol (SciPy-bit-exact) ---------------------------------- */
 /* Build the LMS+digital-shift scrambled generator SciPy builds for
@@ -143,7 +162,8 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
  * the sync area; the f64 sums are added in slice order (oracle kernel mode, slices = W).  Other
  * shapes run the three steps as separate launches, bit-identical to the separate calls.
  * sync_dev: smc_train_step_sync_bytes(...) bytes, zero-filled before the first call (every call
- * leaves its counters zeroed). */
+ * leaves its counters zeroed; the status word at SMC_SYNC_STATUS_OFFSET is sticky, see
+ * smc_sync_status). */
 int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const double* lower_dev,
                        const double* upper_dev, int64_t* cursor_dev, int64_t index_offset, int64_t advance,
                        double* contracts_dev, float* cvnn_input_dev, int64_t n_contracts, int32_t timesteps,
@@ -151,9 +171,9 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
                        int32_t normalization, int32_t dtype, int32_t store_mode, void* paths_dev,
                        int64_t path_pitch, int64_t chunk_contracts, void* targets_dev, void* sync_dev,
                        int64_t sync_bytes, void* stream);
-/* Bytes of smc_train_step's sync area for this shape on the current device (8 for whole-contract
- * shapes: a done counter and the contract queue of the dynamically handed-out last quarter of the
- * rounds; -1 if the device query fails). */
+/* Bytes of smc_train_step's sync area for this shape on the current device (128 for whole-contract
+ * shapes: a done counter, the status word and the contract queue of the dynamically handed-out last
+ * quarter of the rounds; -1 if the device query fails). */
 int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
                                   int32_t dtype, int64_t path_pitch);
 /* Name of the kernel smc_train_step launches for this shape ("resident_kernel",

@@ -23,6 +23,9 @@ SMC_ERR_SEED_OUT_OF_RANGE = 3
 SMC_ERR_SEQUENCE_EXHAUSTED = 4
 SMC_ERR_MEMORY_LIMIT = 5
 SMC_ERR_HIP = 6
+SMC_ERR_EXCHANGE_TIMEOUT = 7
+SYNC_STATUS_OFFSET = 32
+SYNC_EXCHANGE_TIMEOUT = 1
 
 SCHEME_LOG_EULER = 0
 SCHEME_SIMPLE_EULER = 1
@@ -34,7 +37,7 @@ STORE_TERMINAL = 1
 MATH_HW = 0x100
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 
@@ -42,6 +45,8 @@ _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
 SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_abi_version": (_c_i32, []),
     "smc_last_error_string": (ctypes.c_char_p, []),
+    "smc_sync_status": (_c_i32, [_c_vp, _c_i32, ctypes.POINTER(_c_i32), _c_vp]),
+    "smc_test_exchange_fault": (_c_i32, [_c_i32, ctypes.c_uint32]),
     "smc_sobol_create": (_c_i32, [_c_i32, _c_u64, _c_u64, ctypes.POINTER(_c_vp)]),
     "smc_sobol_destroy": (None, [_c_vp]),
     "smc_sobol_state": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp]),
@@ -154,6 +159,13 @@ def last_error() -> str:
 def check(status: int) -> None:
     if status != SMC_OK:
         raise SmcError(status, last_error())
+
+
+def sync_status(sync: Any, clear: bool = True, stream: Any = None) -> int:
+    """The status word of an exchanging launch's sync area (waits for the stream; 0: no failure)."""
+    out = _c_i32(0)
+    check(lib().smc_sync_status(ptr(sync), 1 if clear else 0, ctypes.byref(out), stream_handle(stream)))
+    return int(out.value)
 
 
 def require_device() -> None:

@@ -29,7 +29,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .engine import StepBuffers
+from .engine import StepBuffers, check_sync_status
 from .sobol_sampler import SobolEngine, draw_device
 
 MAX_ASSETS = 8
@@ -204,6 +204,11 @@ class BasketEngine:
         self._sync = torch.zeros(self._sync_bytes, dtype=torch.uint8, device=device) if self._sync_bytes else None
         self.kernel_name = _lib.lib().smc_basket_train_targets_kernel(
             self.A, self.T, self.N, self.M, 1 if self._sync is not None else 0, 1).decode()
+
+    def check_status(self, stream: torch.cuda.Stream | None = None) -> None:
+        """SmcError(SMC_ERR_EXCHANGE_TIMEOUT) if a resident launch gave up on a partner slice since the
+        last check (engine.check_sync_status)."""
+        check_sync_status(self._sync, stream)
 
     @property
     def global_batch(self) -> int:

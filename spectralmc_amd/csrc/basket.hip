@@ -332,10 +332,9 @@ constexpr int kRMaxSlices = 32;
 constexpr int kRowBlock = 16;
 constexpr int kRSlots = 4;                   // slice-sum slots (contract j mod 4)
 constexpr int kRTable = 64;                  // contracts per coefficient table (one per wave-0 lane)
-constexpr uint32_t kRSpinLimit = 1u << 20;  // ~1 s of polling: a partner that never arrives gives NaN targets
 
-// Sync area of the resident basket launch (bytes): [0, 128) done counter (+0) and contract queue
-// (+64); per group a 128-B line of slice-sum arrivals; slice sums [groups][4][W A + 1] f64 (the
+// Sync area of the resident basket launch (bytes): [0, 128) done counter (+0), the sticky status
+// word (+SMC_SYNC_STATUS_OFFSET) and contract queue (+64); per group a 128-B line of slice-sum arrivals; slice sums [groups][4][W A + 1] f64 (the
 // last entry: the contract of the group's iteration j + 2, dynamic tail); column sums [chunk][W][N].
 struct BasketSyncLayout {
   int64_t groups, xsum_off, xcol_off, bytes;
@@ -365,6 +364,8 @@ struct BasketResArgs {
   int32_t groups;         // contract sequences (grid = groups * W)
   uint8_t* sync;          // basket_sync_layout
   int64_t xsum_off, xcol_off;
+  uint32_t spin_limit;    // polls of an exchange before it gives up (status word, NaN targets)
+  int32_t withhold;       // smc_test_exchange_fault: slice W-1 of group 0 skips its first arrival
 };
 
 #if defined(SMC_EXPERIMENT_TRACE)  // tools/micro decomposition builds only: per-workgroup start/end + XCD
@@ -421,6 +422,7 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
   const bool dyn = S >= 2;
   const int64_t n_static = dyn ? S * groups : a.B;
   uint32_t* queue = reinterpret_cast<uint32_t*>(ra.sync + 64);
+  uint32_t* status = reinterpret_cast<uint32_t*>(ra.sync + SMC_SYNC_STATUS_OFFSET);
   auto bof = [&](int64_t jj) -> int64_t { return !dyn || jj < S ? grp + jj * groups : bidx[jj & 3]; };
   auto coefs = [&](int64_t bb, float* e) {  // simulation coefficients of contract bb (f64 Cholesky, rounded once)
     const double* c = a.contracts + bb * width;
@@ -456,8 +458,13 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
     const double* c = a.contracts + b * width;
     const double* xs = xsum + (jj % kRSlots) * XS;
     const uint32_t want = static_cast<uint32_t>(W) * static_cast<uint32_t>(jj + 1);
+    // bounded poll; once any exchange of the launch has failed (status word set) the others stop
+    // waiting at once, so a failed launch still drains in about one poll budget
     uint32_t spins = 0;
-    while (get_sc1(cnt) < want && ++spins < kRSpinLimit) __builtin_amdgcn_s_sleep(2);
+    bool ok;
+    while (!(ok = get_sc1(cnt) >= want) && get_sc1(status) == 0u && ++spins < ra.spin_limit)
+      __builtin_amdgcn_s_sleep(2);
+    if (!ok && lane == 0) __hip_atomic_fetch_or(status, SMC_SYNC_EXCHANGE_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the W x A slice sums in one round of loads across the wave (<= 4 per lane), parked in part[]
     // (free until the payoff), then lanes 0..A-1 add their asset's W sums in slice order
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -477,7 +484,7 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
     if (lane < A) {
       double t = 0.0;  // slices in order
       for (int s2 = 0; s2 < W; ++s2) t += part[s2 * A + lane];
-      if (spins >= kRSpinLimit) t = __builtin_nan("");
+      if (!ok) t = __builtin_nan("");
       if (slc == 0 && a.terminal_sum) a.terminal_sum[b * A + lane] = t;
       const float Tf = static_cast<float>(c[1]);
       const float F = static_cast<float>(c[4 + lane]) * math::exp_any(static_cast<float>(c[2] - c[4 + A + lane]) * Tf);
@@ -487,7 +494,7 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
       pco[A] = math::exp_any(static_cast<float>(-c[2]) * static_cast<float>(c[1]));
       pco[A + 1] = static_cast<float>(c[0]);
       if (dyn && jj + 2 >= S) {  // the contract of iteration jj + 2 (slice 0 took it) and its coefficients
-        const int64_t nb = spins < kRSpinLimit ? get_sc1(reinterpret_cast<const int64_t*>(xs + W * A)) : a.B;
+        const int64_t nb = ok ? get_sc1(reinterpret_cast<const int64_t*>(xs + W * A)) : a.B;
         bidx[(jj + 2) & 3] = nb;
         if (nb < a.B) coefs(nb, dco + ((jj + 2) & 1) * CS);
       }
@@ -612,7 +619,8 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
       if (dyn && slc == 0 && lane == 0 && jj + 2 >= S)  // the group's contract of iteration jj + 2
         put_sc1(reinterpret_cast<int64_t*>(xsum + (jj % kRSlots) * XS + W * A), n_static + atomicAdd(queue, 1u));
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0 && !(ra.withhold && grp == 0 && slc == W - 1 && jj == 0))
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     lds_barrier();  // part / wsum are rewritten from here on
   }
@@ -760,7 +768,8 @@ int32_t launch_basket_resident_k(const BasketArgs& a, int W, int64_t groups, int
     return fail(SMC_ERR_HIP, "basket_resident_kernel: cannot raise the dynamic LDS limit");
   }
   const BasketSyncLayout l = basket_sync_layout(A, W, a.N, groups, chunk);
-  const BasketResArgs ra{a, W, static_cast<int32_t>(groups), sync, l.xsum_off, l.xcol_off};
+  const BasketResArgs ra{a, W, static_cast<int32_t>(groups), sync, l.xsum_off, l.xcol_off, exchange_spin_limit(),
+                        exchange_fault().withhold};
   hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(groups * W)), dim3(kRThreads), lds, stream, ra);
   if (int32_t st = check_launch("basket_resident_kernel")) return st;
   const size_t flds = 5 * static_cast<size_t>(a.N) * sizeof(double);

@@ -1,4 +1,6 @@
-// C-ABI housekeeping of libspectralmc_hip.so: ABI version and per-thread error text.
+// C-ABI housekeeping of libspectralmc_hip.so: ABI version, per-thread error text, the sync-area
+// status word of the exchanging launches, and the exchange-fault test hook.
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 
@@ -7,6 +9,8 @@
 namespace smc {
 namespace {
 thread_local char g_last_error[512] = "";
+std::atomic<int32_t> g_fault_withhold{0};
+std::atomic<uint32_t> g_fault_spin_limit{0};
 }
 
 void set_error(const char* fmt, ...) {
@@ -16,6 +20,8 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+ExchangeFault exchange_fault() { return ExchangeFault{g_fault_withhold.load(), g_fault_spin_limit.load()}; }
+
 }  // namespace smc
 
 extern "C" {
@@ -24,6 +30,33 @@ extern "C" {
 int32_t smc_abi_version(void) { return SMC_ABI_VERSION; }
 
 const char* smc_last_error_string(void) { return smc::g_last_error; }
+
+int32_t smc_sync_status(void* sync_dev, int32_t clear, int32_t* status_out, void* stream) {
+  if (!sync_dev || !status_out) return smc::fail(SMC_ERR_INVALID_ARGUMENT, "smc_sync_status: NULL pointer");
+  const hipStream_t s = smc::as_stream(stream);
+  uint32_t word = 0;
+  char* w = static_cast<char*>(sync_dev) + SMC_SYNC_STATUS_OFFSET;
+  if (hipMemcpyAsync(&word, w, sizeof(word), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    const hipError_t e = hipGetLastError();
+    smc::set_error("smc_sync_status: %s", hipGetErrorString(e));
+    return SMC_ERR_HIP;
+  }
+  if (clear && word != 0u && (hipMemsetAsync(w, 0, sizeof(word), s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)) {
+    const hipError_t e = hipGetLastError();
+    smc::set_error("smc_sync_status: %s", hipGetErrorString(e));
+    return SMC_ERR_HIP;
+  }
+  *status_out = static_cast<int32_t>(word);
+  return SMC_OK;
+}
+
+int32_t smc_test_exchange_fault(int32_t withhold, uint32_t spin_limit) {
+  if (withhold != 0 && withhold != 1) return smc::fail(SMC_ERR_INVALID_ARGUMENT, "smc_test_exchange_fault: withhold");
+  smc::g_fault_withhold.store(withhold);
+  smc::g_fault_spin_limit.store(spin_limit);
+  return SMC_OK;
+}
 
 #pragma GCC visibility pop
 }  // extern "C"

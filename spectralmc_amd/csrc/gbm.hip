@@ -102,6 +102,12 @@ struct EngineArgs {
   // handed out from this counter (zero between launches) instead of statically, so workgroups on
   // XCDs with more write bandwidth take more contracts (NULL: all static)
   uint32_t* res_queue;
+  // sliced resident_kernel: the sync area's sticky status word (SMC_SYNC_STATUS_OFFSET), the poll
+  // budget of an exchange and the smc_test_exchange_fault hook (withhold: slice W-1 of group 0 skips
+  // its first terminal-sum arrival)
+  uint32_t* status;
+  uint32_t spin_limit;
+  int32_t withhold;
 };
 
 #ifndef SMC_SLICE_CHUNKS
@@ -682,7 +688,6 @@ constexpr int kResLdsChunks = 8;                        // chunks parked in LDS
 constexpr int kResRegChunks = kResMaxChunks - kResLdsChunks;
 constexpr size_t kResTermBytes = static_cast<size_t>(kResLdsChunks) * kResThreads * 16;  // 128 KiB
 constexpr int kResMaxSlices = 8;
-constexpr uint32_t kResSpinLimit = 1u << 20;  // ~1 s of polling: a partner that never arrives gives NaN targets
 
 constexpr int kResPreDraw = 32;  // static contracts whose Sobol rows are drawn at kernel start
 
@@ -858,15 +863,21 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
           put_sc1(reinterpret_cast<int64_t*>(a.res_xsum + xslot + W), n_static + atomicAdd(a.res_queue, 1u));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t* cnt = a.res_cnt + static_cast<int64_t>(grp) * 64;
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!(a.withhold && grp == 0 && slc == W - 1 && round == 0))
+          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t want = static_cast<uint32_t>(W) * (round + 1);
+        // bounded poll; once any exchange of the launch has failed (status word set) the others
+        // stop waiting at once, so a failed launch still drains in about one poll budget
         uint32_t spins = 0;
-        while (get_sc1(cnt) < want && ++spins < kResSpinLimit) __builtin_amdgcn_s_sleep(2);
+        bool ok;
+        while (!(ok = get_sc1(cnt) >= want) && get_sc1(a.status) == 0u && ++spins < a.spin_limit)
+          __builtin_amdgcn_s_sleep(2);
+        if (!ok) __hip_atomic_fetch_or(a.status, SMC_SYNC_EXCHANGE_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const double t = ordered_sum_wt(a.res_xsum + xslot, 0, W, 1);  // slices in order
-        row[6] = spins < kResSpinLimit ? t : __builtin_nan("");
+        row[6] = ok ? t : __builtin_nan("");
         if (dyn && b + groups >= n_static)
           reinterpret_cast<int64_t*>(row + 8)[0] =
-              spins < kResSpinLimit ? get_sc1(reinterpret_cast<const int64_t*>(a.res_xsum + xslot + W)) : a.B;
+              ok ? get_sc1(reinterpret_cast<const int64_t*>(a.res_xsum + xslot + W)) : a.B;
       }
       lds_barrier();
       tot = row[6];
@@ -961,14 +972,15 @@ int32_t resident_slices(int64_t P) {
   return W;
 }
 
-// smc_train_step sync area: [0, 128) the done counter (+0) and the contract queue (+64); then per
+// smc_train_step sync area: [0, 128) the done counter (+0), the sticky status word
+// (+SMC_SYNC_STATUS_OFFSET) and the contract queue (+64); then per
 // group a 256-B record of two 128-B counter lines; then the slice terminal sums + next contract
 // [groups][2][W + 1] and column sums [groups][2][W][N].
 // groups <= 2 #CUs / W (the resident kernel fits one workgroup per CU; twice that for margin).
 struct ResSyncLayout {
   int64_t groups, xsum_off, xcol_off, bytes;
 };
-constexpr int64_t kStepSyncBytes = 2 * sizeof(uint32_t);  // whole contracts: done counter, contract queue
+constexpr int64_t kStepSyncBytes = 128;  // whole contracts: done counter (+0), status (+32), contract queue (+64)
 ResSyncLayout res_sync_layout(int32_t W, int32_t N, int cus) {
   ResSyncLayout l{};
   if (W <= 1) {
@@ -1462,7 +1474,10 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   a.res_slices = resident_slices(P);
   char* sync = static_cast<char*>(sync_dev);
   a.done = reinterpret_cast<uint32_t*>(sync);
-  a.res_queue = reinterpret_cast<uint32_t*>(sync) + (a.res_slices <= 1 ? 1 : 16);  // after the done counter
+  a.status = reinterpret_cast<uint32_t*>(sync + SMC_SYNC_STATUS_OFFSET);
+  a.res_queue = reinterpret_cast<uint32_t*>(sync + 64);
+  a.spin_limit = exchange_spin_limit();
+  a.withhold = exchange_fault().withhold;
   if (a.res_slices > 1) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {

@@ -31,6 +31,22 @@ inline int32_t check_launch(const char* kernel) {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Polls of an inter-workgroup exchange before it gives up (~1 s of s_sleep(2) polling); the
+// exchange then sets SMC_SYNC_EXCHANGE_TIMEOUT in the sync area's status word and writes NaN
+// targets for the contracts it could not finish.
+constexpr uint32_t kExchangeSpinLimit = 1u << 20;
+
+// Test hook (smc_test_exchange_fault): applied by the host to the next exchanging launches.
+struct ExchangeFault {
+  int32_t withhold;     // 1: slice W-1 of group 0 skips its first arrival
+  uint32_t spin_limit;  // polls before an exchange gives up (0: kExchangeSpinLimit)
+};
+ExchangeFault exchange_fault();
+inline uint32_t exchange_spin_limit() {
+  const uint32_t l = exchange_fault().spin_limit;
+  return l ? l : kExchangeSpinLimit;
+}
+
 }  // namespace smc
 
 // Opaque Sobol handle (smc_sobol_*).

@@ -130,6 +130,12 @@ class TrainingEngine:
             self.kernel_name = _lib.lib().smc_train_targets_kernel(
                 self.T, self.N, self.P, self._dtype_code, self.pitch, 1 if ws else 0).decode()
 
+    def check_status(self, stream: torch.cuda.Stream | None = None) -> None:
+        """Raise SmcError(SMC_ERR_EXCHANGE_TIMEOUT) if a launch since the last check gave up waiting
+        for a partner workgroup (its targets hold NaN); clears the sticky status word.  Waits for
+        ``stream`` (default: the current stream)."""
+        check_sync_status(self._sync, stream)
+
     @property
     def global_batch(self) -> int:
         return self.B * self.world_size
@@ -180,4 +186,15 @@ class TrainingEngine:
             self.chunk, None, _lib.ptr(b.targets), _lib.ptr(self._workspace), self._workspace_bytes, stream))
 
 
-__all__ = ["TrainingEngine", "StepBuffers", "DEFAULT_PATH_BUFFER_BYTES"]
+def check_sync_status(sync: torch.Tensor | None, stream: torch.cuda.Stream | None = None) -> None:
+    """The sync area's status word (include/spectralmc_hip.h, smc_sync_status) as an exception."""
+    if sync is None:
+        return
+    status = _lib.sync_status(sync, clear=True, stream=stream)
+    if status & _lib.SYNC_EXCHANGE_TIMEOUT:
+        raise _lib.SmcError(_lib.SMC_ERR_EXCHANGE_TIMEOUT,
+                            "a workgroup exchange timed out: a partner workgroup never arrived, so the step's "
+                            "targets hold NaN (were all workgroups of a group co-resident?)")
+
+
+__all__ = ["TrainingEngine", "StepBuffers", "DEFAULT_PATH_BUFFER_BYTES", "check_sync_status"]

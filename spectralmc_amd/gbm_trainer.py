@@ -594,9 +594,11 @@ class GbmCVNNPricer:
                     loss, _ = session.read_metrics()
                     self._commit_to_blockchain(blockchain_store, session.adam, template, loss,
                                                batch=session.global_step)
+            final_state = session.close()
         except _lib.SmcError as exc:
+            if not session._closed:
+                session.close_quietly()
             return Failure(EngineFailure(code=exc.code, message=exc.message))
-        final_state = session.close()
         return self._finish(session.adam, final_state, config, blockchain_store, commit_plan)
 
     def _train_checked(self, config: TrainingConfig, sampler: SobolSampler, logger, blockchain_store,
@@ -839,7 +841,12 @@ class TrainingSession:
             self.program.run_mc(slot)
 
     def sync(self) -> None:
+        """Wait for the enqueued steps; raises SmcError (SMC_ERR_EXCHANGE_TIMEOUT) if an exchanging
+        path launch gave up on a partner workgroup since the last check (its targets hold NaN)."""
         self.stream.synchronize()
+        check = getattr(self.engine, "check_status", None)
+        if check is not None:
+            check(self.mc_stream)
 
     def read_metrics(self) -> tuple[float, float]:
         self.sync()
@@ -849,7 +856,7 @@ class TrainingSession:
         if self._closed:
             raise RuntimeError("session already closed")
         self._closed = True
-        self.sync()
+        self.stream.synchronize()
         self.mc_stream.synchronize()
         dev = self.pricer._torch_device
         torch.cuda.current_stream(dev).wait_stream(self.stream)
@@ -858,7 +865,22 @@ class TrainingSession:
         for p in self.params:  # detach the flat-buffer grad views from the parameters
             p.grad = p.grad.clone()
         self.sampler.skip(self.sobol_skip - self.sobol_skip0)
+        check = getattr(self.engine, "check_status", None)
+        if check is not None:  # after the bookkeeping: the session is closed either way
+            check(self.mc_stream)
         return _BatchState(self.sobol_skip, self.global_step, loss, gn)
+
+
+    def close_quietly(self) -> None:
+        """Release the session after a failure: wait for the streams, leave the status unread."""
+        if self._closed:
+            return
+        self._closed = True
+        self.stream.synchronize()
+        self.mc_stream.synchronize()
+        for p in self.params:
+            if p.grad is not None:
+                p.grad = p.grad.clone()
 
 
 def _bounds_always_valid(lower: np.ndarray) -> bool:

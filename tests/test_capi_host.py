@@ -36,7 +36,8 @@ def test_library_exports_every_declared_symbol() -> None:
 INTEGRATION = os.path.join(os.path.dirname(HEADER), "..", "INTEGRATION.md")
 _CTYPES = {"c_int32": ctypes.c_int32, "c_int64": ctypes.c_int64, "c_uint64": ctypes.c_uint64,
            "c_void_p": ctypes.c_void_p, "c_char_p": ctypes.c_char_p, "None": None,
-           "ctypes.POINTER(c_void_p)": ctypes.POINTER(ctypes.c_void_p),
+           "ctypes.POINTER(c_void_p)": ctypes.POINTER(ctypes.c_void_p), "c_uint32": ctypes.c_uint32,
+           "ctypes.POINTER(c_int32)": ctypes.POINTER(ctypes.c_int32),
            "ctypes.POINTER(c_int64)": ctypes.POINTER(ctypes.c_int64)}
 
 
@@ -134,6 +135,12 @@ def test_engine_argument_errors_do_not_launch() -> None:
     for pitch in (4, 65532, 65538):
         assert L.smc_train_step(p, 6, p, p, p, 0, 0, p, None, 4, 16, 256, 256, 7, 0, 1, 0, 2, p, pitch, 4, p, p, 8,
                                 None) == _lib.SMC_ERR_INVALID_SHAPE, pitch
+    # whole-contract step shapes need no device query: done counter, status word, contract queue
+    assert L.smc_train_step_sync_bytes(16, 256, 256, 0, 66560) == 128
+    out = ctypes.c_int32(-1)
+    assert L.smc_sync_status(None, 1, ctypes.byref(out), None) == _lib.SMC_ERR_INVALID_ARGUMENT
+    assert L.smc_test_exchange_fault(2, 0) == _lib.SMC_ERR_INVALID_ARGUMENT
+    assert L.smc_test_exchange_fault(0, 0) == _lib.SMC_OK
     assert L.smc_normals(7, 0, 0, 10, 0, p, None) == _lib.SMC_ERR_INVALID_SHAPE
     assert L.smc_sobol_draw(None, 6, None, 0, 4, p, p, p, None, None) == _lib.SMC_ERR_INVALID_ARGUMENT
 

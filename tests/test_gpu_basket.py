@@ -261,3 +261,32 @@ def test_pricer_trains_on_baskets_and_matches_oracle_step(oracle, M) -> None:
     pricer.warmup_steps = 2
     res = expect_success(pricer.train(make_training_config(num_batches=5, batch_size=B, learning_rate=1e-2)))
     assert np.isfinite(res.final_loss)
+
+
+def test_resident_exchange_timeout_is_reported() -> None:
+    """basket_resident_kernel with a withheld slice arrival (test hook): the launch completes, the
+    contract's targets are NaN, and BasketEngine.check_status raises SMC_ERR_EXCHANGE_TIMEOUT instead of
+    training on NaN silently; the next launch with the hook cleared matches a clean launch."""
+    cfg = BasketConfig(n_assets=4, timesteps=16, network_size=256, batches_per_mc_run=128, math="portable")
+    eng = BasketEngine(cfg, 12, device=torch.device(DEV))
+    assert eng.kernel_name == "basket_resident_kernel"
+    eng.set_position(0, 0)
+    eng.enqueue_step()
+    clean = eng.buffers.targets.clone()
+    eng.check_status()
+    L = _lib.lib()
+    _lib.check(L.smc_test_exchange_fault(1, 20000))
+    try:
+        eng.set_position(0, 0)
+        eng.enqueue_step()
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(L.smc_test_exchange_fault(0, 0))
+    assert torch.isnan(eng.buffers.targets[0].real).all()
+    with pytest.raises(_lib.SmcError) as exc:
+        eng.check_status()
+    assert exc.value.code == _lib.SMC_ERR_EXCHANGE_TIMEOUT
+    eng.set_position(0, 0)
+    eng.enqueue_step()
+    eng.check_status()
+    assert torch.equal(eng.buffers.targets, clean)

@@ -408,7 +408,7 @@ def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store, ch
     cur_a = torch.tensor([100, 50], dtype=torch.int64, device=DEV)
     cur_b = cur_a.clone()
     sync, nsync = _sync(L, T, N, M, pitch)
-    assert nsync == 8  # whole-contract shapes: an arrival counter and the contract queue
+    assert nsync == 128  # whole-contract shapes: done counter, status word, contract queue
     for _ in range(3):
         ca = torch.empty((B, 6), dtype=torch.float64, device=DEV)
         fa = torch.empty((B, 6), dtype=torch.float32, device=DEV)
@@ -430,7 +430,7 @@ def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store, ch
         np.testing.assert_array_equal(fa.cpu().numpy(), fb.cpu().numpy())
         np.testing.assert_array_equal(ta.cpu().numpy(), tb.cpu().numpy())
         assert cur_a.tolist() == cur_b.tolist()
-        assert sync.view(torch.int32)[:2].tolist() == [0, 0]
+        assert not sync.view(torch.int32).any()  # done counter, status word and contract queue
 
 
 SLICED_CASES = [  # (B, N, M, store, chunk): shapes with P > 65,536 (W = P / 65,536 slices)
@@ -485,7 +485,10 @@ def test_sliced_train_step_bit_exact(oracle, golden, B, N, M, store, chunk) -> N
         # the done counter and the group counters are back at zero (the second pass depends on it:
         # its exchanges wait for W arrivals per contract round from zero)
         words = sync.view(torch.int32).cpu().numpy()
-        assert words[0] == 0 and not words[32:32 + 64 * 16].any()
+        groups = -(-2 * torch.cuda.get_device_properties(0).multi_processor_count // W)  # sync-area capacity
+        # done counter, status word, contract queue and every group's two counter lines
+        assert words[0] == 0 and words[8] == 0 and words[16] == 0
+        assert not words[32:32 + 64 * groups].any()
         contracts = c.cpu().numpy()
         got = t.cpu().numpy()
         if math == 0:
@@ -494,3 +497,52 @@ def test_sliced_train_step_bit_exact(oracle, golden, B, N, M, store, chunk) -> N
         else:
             want = oracle.training_targets(contracts[:12], T, N, M, seed=7, ordinal0=start[1])
             assert _norm_rel(got[:12], want) < 1e-5
+
+
+def test_exchange_timeout_sets_status_not_silent_nan(oracle, golden) -> None:
+    """A sliced contract whose partner slice never arrives (test hook: slice W-1 of group 0 withholds
+    its first arrival, 20,000-poll budget) ends the launch with NaN targets AND the sticky status word
+    SMC_SYNC_EXCHANGE_TIMEOUT, which smc_sync_status reports (and clears) and TrainingEngine maps to
+    SmcError(SMC_ERR_EXCHANGE_TIMEOUT).  With the hook cleared the next step is bit-exact again."""
+    from spectralmc_amd.engine import check_sync_status
+
+    L = _L()
+    T, N, M = 16, 128, 1024  # P = 131,072: W = 2 slices per contract
+    P = N * M
+    B = 9
+    pitch = int(L.smc_path_pitch(P, 0))
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
+    lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
+    hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
+    paths = torch.empty((B, pitch), dtype=torch.float32, device=DEV)
+    sync, nsync = _sync(L, T, N, M, pitch)
+
+    def step(cur):
+        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
+        t = torch.zeros((B, N), dtype=torch.complex64, device=DEV)
+        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
+                                    _lib.ptr(c), None, B, T, N, M, 7, _lib.SCHEME_LOG_EULER, _lib.NORM_NORMALIZE,
+                                    _lib.DTYPE_F32, _lib.STORE_TERMINAL, _lib.ptr(paths), pitch, B, _lib.ptr(t),
+                                    _lib.ptr(sync), nsync, None))
+        return c, t
+
+    _lib.check(L.smc_test_exchange_fault(1, 20000))
+    try:
+        cur = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
+        _, t = step(cur)
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(L.smc_test_exchange_fault(0, 0))
+    assert np.isnan(t[0].cpu().numpy()).all()  # group 0's first contract could not finish
+    assert cur.tolist() == [B, B]                # the launch still completed and advanced the cursor
+    with pytest.raises(_lib.SmcError) as exc:
+        check_sync_status(sync)
+    assert exc.value.code == _lib.SMC_ERR_EXCHANGE_TIMEOUT
+    assert _lib.sync_status(sync) == 0  # read-and-clear
+    cur = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
+    c, t = step(cur)
+    check_sync_status(sync)
+    wg, W = oracle.train_step_order(T, N, P)
+    kt, _ = oracle.kernel_targets(c.cpu().numpy(), T, N, M, seed=7, ordinal0=0, wg=wg, slices=W)
+    np.testing.assert_array_equal(t.cpu().numpy(), kt)
