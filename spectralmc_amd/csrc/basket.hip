@@ -491,7 +491,8 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
       pco[lane] = a.normalize ? F / static_cast<float>(t / static_cast<double>(P)) : 1.0f;
     }
     if (lane == 0) {
-      pco[A] = math::exp_any(static_cast<float>(-c[2]) * static_cast<float>(c[1]));
+      // a failed exchange: NaN discount, so the targets are NaN (max(K - NaN, 0) alone would give 0)
+      pco[A] = ok ? math::exp_any(static_cast<float>(-c[2]) * static_cast<float>(c[1])) : __builtin_nanf("");
       pco[A + 1] = static_cast<float>(c[0]);
       if (dyn && jj + 2 >= S) {  // the contract of iteration jj + 2 (slice 0 took it) and its coefficients
         const int64_t nb = ok ? get_sc1(reinterpret_cast<const int64_t*>(xs + W * A)) : a.B;

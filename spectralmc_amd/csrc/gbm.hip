@@ -364,6 +364,9 @@ struct Payoff {
     }
     s = a.normalize ? F / static_cast<Real>(terminal_sum / static_cast<double>(a.P)) : Real(1);
     K = static_cast<Real>(c.K);
+    // a failed exchange hands over a NaN terminal sum: keep the targets NaN (df * max(K - NaN, 0)
+    // would be 0, a plausible value) so a caller that skips smc_sync_status still sees it
+    if (terminal_sum != terminal_sum) df = static_cast<Real>(__builtin_nan(""));
   }
   __device__ __forceinline__ Real operator()(Real x) const {
     const Real xs = x * s;  // sims *= scale (rounded to Real)

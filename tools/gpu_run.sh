@@ -64,6 +64,7 @@ for step in "$@"; do
     pmc_hw_bytes) cd /tmp && run pmc_hw_bytes 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/pmc_hw_bytes" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
     pmc_hw_fetch) cd /tmp && run pmc_hw_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_hw_fetch" -o run --output-format csv -- python "$ROOT/tools/kprof.py" --math hw --store all --unsliced; cd "$ROOT" ;;
     orderbench) run orderbench 240 tools/micro/orderbench ;;
+    prof_order) cd /tmp && run prof_order 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_order" -o run --output-format csv -- "$ROOT/tools/micro/orderbench"; cd "$ROOT" ;;
     valurate) run valurate 120 tools/micro/valurate ;;
     ab_resident) run ab_resident 900 bash tools/micro/ab_resident.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
