@@ -95,13 +95,17 @@ def any_dtype_from_torch(dt: torch.dtype) -> Result[AnyDType, UnsupportedTorchDT
 
 
 class Device(str, Enum):
-    """``cuda`` is the process's GPU: one process per GPU, so every rank sees cuda:0
-    (``HIP_VISIBLE_DEVICES`` / ``LOCAL_RANK`` binding, see spectralmc_amd/dp.py)."""
+    """``cuda`` is the process's GPU (reference ``models/torch.py:158-175``: the single-GPU policy
+    "cuda:0").  One process per GPU: a rank bound with ``torch.cuda.set_device(LOCAL_RANK)``
+    (spectralmc_amd/dp.py) maps ``cuda`` to ITS device, so tensors a rank reloads (storage/wire.py)
+    land on its own GPU, not on rank 0's."""
 
     cpu = "cpu"
     cuda = "cuda:0"
 
     def to_torch(self) -> torch.device:
+        if self is Device.cuda and torch.cuda.is_available():
+            return torch.device("cuda", torch.cuda.current_device())
         return torch.device(self.value)
 
     @classmethod

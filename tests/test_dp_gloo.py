@@ -1,4 +1,4 @@
-"""Data-parallel step on CPU (gloo, world_size 2): the product's network step program
+"""Data-parallel step on CPU (gloo, world_size 2 and 8 = C4's world): the product's network step program
 (`_StepProgram`: flat [grads..., loss] buffer, one all-reduce, Adam, grad norm) with the
 product's `DataParallel`, fed per-rank shards of the global batch.
 
@@ -37,8 +37,9 @@ def _shard_inputs(oracle, base: int, start: int, n: int):
     return contracts, targets
 
 
-def _run(rank: int, world: int, outdir: str) -> None:
-    """Train STEPS steps on this rank's shards; save params and losses."""
+def _run(rank: int, world: int, outdir: str, global_world: int = 2) -> None:
+    """Train STEPS steps on this rank's shards of a global batch of global_world * B_LOCAL
+    contracts per step (world == 1: the whole global batch in one process); save params, losses."""
     from oracle import oracle
     from spectralmc_amd.dp import DataParallel, current
     from spectralmc_amd.engine import StepBuffers
@@ -52,13 +53,13 @@ def _run(rank: int, world: int, outdir: str) -> None:
     ctx = current() if world > 1 else None
     if world > 1:
         assert isinstance(ctx, DataParallel) and ctx.rank == rank and ctx.world_size == world
-    b = B_LOCAL * (1 if world > 1 else 2)
+    b = B_LOCAL * (1 if world > 1 else global_world)
     buffers = StepBuffers(contracts=torch.zeros(b, 6, dtype=torch.float64), real_in=torch.zeros(b, 6),
                           imag_in=torch.zeros(b, 6), targets=torch.zeros(b, N, dtype=torch.complex64))
     prog = _StepProgram(types.SimpleNamespace(_cvnn=model), types.SimpleNamespace(buffers=buffers), adam, params, ctx)
     losses = []
     for s in range(STEPS):
-        base = s * 2 * B_LOCAL  # global batch = 2 * B_LOCAL contracts per step in both runs
+        base = s * global_world * B_LOCAL  # the same global batch per step in both runs
         start = base + (ctx.shard(0, B_LOCAL)[0] if ctx else 0)
         contracts, targets = _shard_inputs(oracle, base, start, b)
         buffers.contracts.copy_(torch.from_numpy(contracts))
@@ -73,11 +74,14 @@ def _run(rank: int, world: int, outdir: str) -> None:
 
 
 def _worker(rank: int, world: int, port: int, outdir: str) -> None:
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from spectralmc_amd.dp import init_from_env
+
+    init_from_env("gloo")  # the product's torchrun-style initialisation
     try:
-        _run(rank, world, outdir)
+        _run(rank, world, outdir, global_world=world)
     finally:
         dist.destroy_process_group()
 
@@ -114,15 +118,34 @@ def test_shards_concatenate_to_global_batch(oracle) -> None:
 
 
 @pytest.mark.timeout(300)
-def test_dp_step_matches_single_process(tmp_path, oracle) -> None:
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    _run(0, 1, str(tmp_path))  # single process, global batch of 2 * B_LOCAL
-    r0, r1 = np.load(tmp_path / "rank0_w2.npz"), np.load(tmp_path / "rank1_w2.npz")
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_step_matches_single_process(tmp_path, oracle, world) -> None:
+    """W gloo ranks (8 = C4's world: 8 x 4096 contracts) each on their shard == one process with the
+    global batch (partition invariance up to f32 summation order), and every replica bit-identical."""
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    _run(0, 1, str(tmp_path), global_world=world)  # single process, global batch of world * B_LOCAL
+    ranks = [np.load(tmp_path / f"rank{r}_w{world}.npz") for r in range(world)]
+    r0 = ranks[0]
     single = np.load(tmp_path / "rank0_w1.npz")
-    for k in r0.files:
-        np.testing.assert_array_equal(r0[k], r1[k])  # replicas stay bit-identical
+    for rr in ranks[1:]:
+        for k in r0.files:
+            np.testing.assert_array_equal(r0[k], rr[k])  # replicas stay bit-identical
     # mean of equal-size shard means == global mean up to f32 summation order
     np.testing.assert_allclose(r0["losses"], single["losses"], rtol=1e-5)
     for k in r0.files:
         if k != "losses":
             np.testing.assert_allclose(r0[k], single[k], rtol=1e-5, atol=1e-6)
+
+
+def test_device_enum_follows_the_bound_rank_device(monkeypatch) -> None:
+    """Device.cuda.to_torch() is the process's bound GPU (torch.cuda.set_device(LOCAL_RANK) in
+    dp.init_from_env), so a rank's reloaded checkpoint tensors (storage/wire.py) land on its own
+    device; on a host without a GPU it stays the reference's "cuda:0"."""
+    from spectralmc_amd.models.torch import Device
+
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 5)
+    assert Device.cuda.to_torch() == torch.device("cuda", 5)
+    assert Device.cpu.to_torch() == torch.device("cpu")
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    assert Device.cuda.to_torch() == torch.device("cuda:0")

@@ -88,6 +88,39 @@ __global__ __launch_bounds__(NT) void rowpair(float* out) {
   }
 }
 
+// contract-interleaved layout [T][P/K][B][K]: chunk j of row t of every contract side by side, so the
+// persistent workgroups (contracts b, b + grid, ...) write neighbouring K-path pieces at the same time
+template <int NT, int K>
+__global__ __launch_bounds__(NT) void interleaved(float* out) {
+  constexpr int PER = K / (4 * NT);
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    v4f v = {1.f + b, 2.f, 3.f, static_cast<float>(threadIdx.x)};
+    for (int c = 0; c < P / K; ++c) {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        float* piece = out + ((static_cast<int64_t>(t) * (P / K) + c) * B + b) * K;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+          __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(piece), (k * NT + threadIdx.x) * 16u, 0, 0);
+          v.x += 1.f;
+        }
+      }
+    }
+  }
+}
+
+// linear grid-stride fill over the whole padded matrix (hipMemset's __amd_rocclr_fillBufferAligned
+// runs 256 x 256 threads of this shape)
+template <int NT>
+__global__ __launch_bounds__(NT) void fill_linear(float* out, int64_t n16) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * NT;
+  v4f v = {1.f, 2.f, 3.f, static_cast<float>(threadIdx.x)};
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x; i < n16; i += stride) {
+    reinterpret_cast<v4f*>(out)[i] = v;
+    v.x += 1.f;
+  }
+}
+
 template <typename F>
 void timeit(const char* name, F launch) {
   hipEvent_t e0, e1;
@@ -113,8 +146,23 @@ int main() {
   float* out;
   CK(hipMalloc(&out, static_cast<size_t>(B) * T * PITCH * 4));
   std::printf("CUs %d, %d contracts x %d rows x %lld paths (pitch %lld)\n", cus, B, T, (long long)P, (long long)PITCH);
+  const int64_t n16 = static_cast<int64_t>(B) * T * PITCH / 4;
   for (int rep = 0; rep < 2; ++rep) {
     timeit("memset (rows of 17.45 GB)", [&] { (void)hipMemsetAsync(out, 0, static_cast<size_t>(B) * T * PITCH * 4); });
+    timeit("fill_linear 256x256 (17.45 GB)", [&] { fill_linear<256><<<256, 256>>>(out, n16); });
+    timeit("fill_linear 256x1024 (17.45 GB)", [&] { fill_linear<256><<<1024, 256>>>(out, n16); });
+    timeit("fill_linear 1024x256 (17.45 GB)", [&] { fill_linear<1024><<<256, 1024>>>(out, n16); });
+    timeit("fill_linear 512x512 (17.45 GB)", [&] { fill_linear<512><<<512, 512>>>(out, n16); });
+    timeit("interleaved K4096 nt1024", [&] { interleaved<1024, 4096><<<cus, 1024>>>(out); });
+    timeit("interleaved K8192 nt1024", [&] { interleaved<1024, 8192><<<cus, 1024>>>(out); });
+    timeit("interleaved K16384 nt1024", [&] { interleaved<1024, 16384><<<cus, 1024>>>(out); });
+    timeit("interleaved K4096 nt512", [&] { interleaved<512, 4096><<<cus, 512>>>(out); });
+    timeit("interleaved K2048 nt512", [&] { interleaved<512, 2048><<<cus, 512>>>(out); });
+    timeit("rowmaj nt256", [&] { rowmaj<256, 0><<<cus, 256>>>(out); });
+    timeit("rowmaj nt256 x2/CU", [&] { rowmaj<256, 0><<<2 * cus, 256>>>(out); });
+    timeit("rowmaj nt128", [&] { rowmaj<128, 0><<<cus, 128>>>(out); });
+    timeit("chunk4096 nt256", [&] { chunked<256, 4096, 0><<<cus, 256>>>(out); });
+    timeit("chunk16384 nt256", [&] { chunked<256, 16384, 0><<<cus, 256>>>(out); });
     timeit("chunk4096 nt1024 (resident)", [&] { chunked<1024, 4096, 0><<<cus, 1024>>>(out); });
     timeit("chunk8192 nt1024", [&] { chunked<1024, 8192, 0><<<cus, 1024>>>(out); });
     timeit("chunk16384 nt1024", [&] { chunked<1024, 16384, 0><<<cus, 1024>>>(out); });
