@@ -325,8 +325,9 @@ def main() -> None:
                    "frac": flops / (net_ms * 1e-3) / 1e12 / peak,
                    "peak_note": "dense MFMA peak of the operand type (bf16 2.52 PF; f32 MFMA = f32 VALU "
                                 "157.3 TF), MI355X_MICROARCH.md",
-                   "note": "small complex GEMMs (K = 12..512) plus the targets read; runs on its own stream "
-                           "beside the next step's path kernel"}
+                   "note": "small complex GEMMs (K = 12..512) plus the targets read; enqueued on its own "
+                           "stream, it runs in the gaps between consecutive path kernels (the path kernel "
+                           "holds every CU's registers while it runs)"}
 
     # ---- measured HBM ceilings on this device (STREAM-style, 8 GiB buffers) --------------
     stream_gbs = {}
@@ -348,17 +349,23 @@ def main() -> None:
         del buf, src
         torch.cuda.empty_cache()
 
-    traffic = None
+    # PMC traffic of THIS kernel at this config (profiles/pmc_traffic.json, tools/pmc_summary.py): an
+    # entry counts only if it measured the same kernel (engine.kernel_name), config, store and math;
+    # the latest round wins
+    traffic, traffic_src = None, None
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tpath):
         try:
             with open(tpath) as f:
                 tj = json.load(f)
-            key = f"{args.config}_{args.store}_{args.math}"
-            if key in tj:
-                traffic = tj[key]["hbm_bytes_per_launch"]
+            hits = sorted((v.get("round", ""), k) for k, v in tj.items()
+                          if v.get("kernel_name") == eng.kernel_name and v.get("config") == args.config
+                          and v.get("store") == args.store and v.get("math") == args.math)
+            if hits:
+                traffic_src = hits[-1][1]
+                traffic = tj[traffic_src]["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
-            traffic = None
+            traffic, traffic_src = None, None
 
     total_units = world * B * P * args.steps
     value = total_units / elapsed
@@ -386,6 +393,9 @@ def main() -> None:
                    "path_store": args.store, "math": args.math, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": eng.kernel_name, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     # bytes the kernel actually moved (PMC) over its live time, against the same peak
+                     "frac_moved": (traffic / (live_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                      "kernel_ms": live_ms, "kernel_ms_isolated": kernel_ms, "live_launches": len(live),
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "contracts_per_launch": contracts_per_launch,

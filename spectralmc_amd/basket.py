@@ -22,18 +22,17 @@ stays single-asset (the reference has no basket pricing API).
 
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 
 from . import _lib
+from . import engine as _engine
 from .engine import StepBuffers, check_sync_status
 from .sobol_sampler import SobolEngine, draw_device
 
 MAX_ASSETS = 8
-DEFAULT_PATH_BUFFER_BYTES = int(float(os.environ.get("SMC_PATH_BUFFER_GB", "40")) * (1 << 30))
 
 
 def basket_fields(n_assets: int) -> tuple[str, ...]:
@@ -184,7 +183,7 @@ class BasketEngine:
         self.pitch = int(_lib.lib().smc_path_pitch(self.P, 0))
         rows = self.T if store_paths else 1
         per_contract = self.A * rows * self.pitch * 4
-        budget = path_buffer_bytes if path_buffer_bytes is not None else DEFAULT_PATH_BUFFER_BYTES
+        budget = path_buffer_bytes if path_buffer_bytes is not None else _engine.path_buffer_budget(device)
         max_chunk = max(1, min(B, budget // per_contract))
         if max_chunk < B:
             # several launches: whole rounds of resident workgroups, so no launch ends in a

@@ -31,8 +31,19 @@ from .gbm import BlackScholesConfig, dtype_code, normalization_code, scheme_code
 from .models.numerical import Precision
 from .sobol_sampler import SobolSampler, draw_device
 
-# path scratch budget: 288 GB of HBM per MI355X; C2 needs 17.4 GB, C3 is cut into equal launches
-DEFAULT_PATH_BUFFER_BYTES = int(float(os.environ.get("SMC_PATH_BUFFER_GB", "40")) * (1 << 30))
+# path scratch budget (SMC_PATH_BUFFER_GB overrides): by default half of the device's HBM (144 GB of
+# an MI355X's 288 GB).  C2 needs 17.4 GB (one launch); C3's 275 GB of paths per step run as 2 launches
+# of 8192 contracts instead of 8 of 2048 (each launch ends in a tail of unevenly finishing workgroup
+# groups: 47.1 vs 51.9 ms/step measured)
+DEFAULT_PATH_BUFFER_BYTES: int | None = (int(float(os.environ["SMC_PATH_BUFFER_GB"]) * (1 << 30))
+                                         if os.environ.get("SMC_PATH_BUFFER_GB") else None)
+
+
+def path_buffer_budget(device: torch.device) -> int:
+    """Bytes of path scratch an engine may allocate on ``device``."""
+    if DEFAULT_PATH_BUFFER_BYTES is not None:
+        return DEFAULT_PATH_BUFFER_BYTES
+    return torch.cuda.get_device_properties(device).total_memory // 2
 
 
 @dataclass(frozen=True)
@@ -92,7 +103,7 @@ class TrainingEngine:
         # scratch rows at a padded pitch: a power-of-two row stride aliases in HBM
         self.pitch = int(_lib.lib().smc_path_pitch(self.P, self._dtype_code))
         per_contract = (self.T * self.pitch if store_paths else self.pitch) * torch.finfo(sim_torch).bits // 8
-        budget = path_buffer_bytes if path_buffer_bytes is not None else DEFAULT_PATH_BUFFER_BYTES
+        budget = path_buffer_bytes if path_buffer_bytes is not None else path_buffer_budget(device)
         max_chunk = max(1, min(B, budget // per_contract))
         if max_chunk < B:
             # several launches: whole rounds of resident contract workgroups (2 per CU)
@@ -197,4 +208,4 @@ def check_sync_status(sync: torch.Tensor | None, stream: torch.cuda.Stream | Non
                             "targets hold NaN (were all workgroups of a group co-resident?)")
 
 
-__all__ = ["TrainingEngine", "StepBuffers", "DEFAULT_PATH_BUFFER_BYTES", "check_sync_status"]
+__all__ = ["TrainingEngine", "StepBuffers", "DEFAULT_PATH_BUFFER_BYTES", "check_sync_status", "path_buffer_budget"]

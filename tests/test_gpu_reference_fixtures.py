@@ -105,6 +105,60 @@ def test_c2_bench_instantiation_whole_rounds(oracle, gbm_golden) -> None:
     np.testing.assert_array_equal(port, kt)
 
 
+def test_c2_timed_call_train_step(oracle, gbm_golden) -> None:
+    """The exact call bench.py times at C2: smc_train_step, B = 4096, T = 16, N = M = 256, STORE_ALL,
+    padded pitch, the sync area (dynamic contract tail + Sobol pre-draw), two consecutive steps from a
+    non-zero cursor.  Contracts bit-equal to the reference sampler's points; hw math within 1e-5 per
+    contract of the reference-mode oracle on a strided sample of 32 contracts (the first two against
+    the reference's own c2shape fixture on step 1); portable math bit-exact with the kernel-mode
+    oracle on a strided 64-contract sub-batch."""
+    from tests.helpers import make_domain_bounds
+    from spectralmc_amd.sobol_sampler import SobolEngine
+
+    L = _lib.lib()
+    B, T, N, M = 4096, 16, 256, 256
+    P = N * M
+    pitch = int(L.smc_path_pitch(P, 0))
+    assert L.smc_train_step_kernel(T, N, M, 0, pitch) == b"resident_kernel"
+    lo, hi = make_domain_bounds().arrays()
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
+    lo_d, hi_d = torch.from_numpy(lo).to(DEV), torch.from_numpy(hi).to(DEV)
+    paths = torch.empty((B, T, pitch), dtype=torch.float32, device=DEV)
+    nsync = int(L.smc_train_step_sync_bytes(T, N, M, 0, pitch))
+    sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
+    for math in (_lib.MATH_HW, 0):
+        cur = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
+        for step in range(2):
+            c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
+            f = torch.empty((B, 6), dtype=torch.float32, device=DEV)
+            t = torch.empty((B, N), dtype=torch.complex64, device=DEV)
+            _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo_d), _lib.ptr(hi_d), _lib.ptr(cur), 0, B,
+                                        _lib.ptr(c), _lib.ptr(f), B, T, N, M, 7, _lib.SCHEME_LOG_EULER | math,
+                                        _lib.NORM_NORMALIZE, _lib.DTYPE_F32, _lib.STORE_ALL, _lib.ptr(paths), pitch,
+                                        B, _lib.ptr(t), _lib.ptr(sync), nsync, None))
+            torch.cuda.synchronize()
+            assert _lib.sync_status(sync) == 0 and not sync.any()
+            contracts = c.cpu().numpy()
+            np.testing.assert_array_equal(contracts, oracle.sobol_contracts(7, step * B, B, lo, hi))
+            np.testing.assert_array_equal(f.cpu().numpy(), contracts.astype(np.float32))
+            got = t.cpu().numpy()
+            if math:
+                if step == 0:
+                    assert per_contract_rel(got[:2], gbm_golden["c2shape_targets"]).max() < 1e-5
+                idx = np.arange(step, B, B // 32)
+                # the ordinal of contract i is step * B + i (one oracle call per sampled contract)
+                want = np.stack([oracle.training_targets(contracts[i:i + 1], T, N, M, seed=7,
+                                                         ordinal0=step * B + int(i))[0] for i in idx])
+                assert per_contract_rel(got[idx], want).max() < 1e-5
+            else:
+                idx = np.arange(2 * step + 1, B, B // 64)
+                kt = np.stack([oracle.kernel_targets(contracts[i:i + 1], T, N, M, seed=7, ordinal0=step * B + int(i),
+                                                     wg=1024)[0][0] for i in idx])
+                np.testing.assert_array_equal(got[idx], kt)
+        assert cur.tolist() == [2 * B, 2 * B]
+
+
 def test_c3_per_contract_shape(oracle, gbm_golden) -> None:
     """C3: N = 1024, M = 256 (P = 262,144 paths per contract), T = 16, hw math."""
     from tests.helpers import make_domain_bounds

@@ -67,6 +67,18 @@ for step in "$@"; do
     prof_order) cd /tmp && run prof_order 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_order" -o run --output-format csv -- "$ROOT/tools/micro/orderbench"; cd "$ROOT" ;;
     valurate) run valurate 120 tools/micro/valurate ;;
     ab_resident) run ab_resident 900 bash tools/micro/ab_resident.sh ;;
+    pmcstep:*)  # pmcstep:<config>:<counter>[:iters] -> rocprofv3 PMC pass over tools/kprof_step.py
+      IFS=: read -r _ cfg ctr its <<< "$step"
+      cd /tmp && run "pmc_${cfg}_${ctr}" 300 rocprofv3 --kernel-trace --pmc "$ctr" -d "$OUT/pmc_${cfg}_${ctr}" -o run --output-format csv -- python "$ROOT/tools/kprof_step.py" --config "$cfg" --iters "${its:-3}"; cd "$ROOT" ;;
+    profbench:*)  # profbench:<config>[:steps] -> rocprofv3 kernel stats of bench.py (no CPU leg)
+      IFS=: read -r _ cfg st <<< "$step"
+      cd /tmp && run "prof_${cfg}" 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_${cfg}" -o run --output-format csv -- python "$ROOT/bench.py" --config "$cfg" --steps "${st:-5}" --warmup 2 --kernel-iters 2 --no-cpu-baseline; cd "$ROOT" ;;
+    benchcfg:*)  # benchcfg:<config>[:steps] -> bench.py line with the CPU baseline
+      IFS=: read -r _ cfg st <<< "$step"
+      run "bench_${cfg}" 900 python bench.py --config "$cfg" --steps "${st:-10}" --warmup 3 --kernel-iters 2 ;;
+    kstep:*)  # kstep:<config>[:extra args with , for spaces]
+      IFS=: read -r _ cfg extra <<< "$step"
+      run "kstep_${cfg}" 300 python tools/kprof_step.py --config "$cfg" ${extra//,/ } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,83 @@
+"""Kernel-only driver for rocprofv3: the MC part of one training step exactly as the trainer enqueues
+it — smc_train_step (Sobol draw + path/CF kernel + cursor advance; resident_kernel at C2, its sliced
+form at C3) — `--iters` times after one warm-up, no CVNN.
+
+    rocprofv3 --kernel-trace --pmc WRITE_SIZE -- python tools/kprof_step.py --config c3
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from spectralmc_amd import _lib  # noqa: E402
+from spectralmc_amd.sobol_sampler import SobolEngine  # noqa: E402
+
+SHAPES = {"c2": (4096, 16, 256, 256), "c3": (16384, 16, 1024, 256), "e2e": (4096, 16, 128, 4),
+          "lockstep": (4096, 1, 16, 4096)}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2", choices=sorted(SHAPES))
+    ap.add_argument("--B", type=int, default=0, help="contracts per step (default: the config's)")
+    ap.add_argument("--math", default="hw", choices=["hw", "portable"])
+    ap.add_argument("--store", default="all", choices=["all", "terminal"])
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--budget-gb", type=float, default=40.0, help="path scratch budget (engine default)")
+    a = ap.parse_args()
+    B, T, N, M = SHAPES[a.config]
+    B = a.B or B
+    P = N * M
+    L = _lib.lib()
+    dev = torch.device("cuda", 0)
+    f64 = a.dtype == "f64"
+    dcode = _lib.DTYPE_F64 if f64 else _lib.DTYPE_F32
+    store = _lib.STORE_ALL if a.store == "all" else _lib.STORE_TERMINAL
+    pitch = int(L.smc_path_pitch(P, dcode))
+    esz = 8 if f64 else 4
+    per = (T if store == _lib.STORE_ALL else 1) * pitch * esz
+    chunk = max(1, min(B, int(a.budget_gb * (1 << 30)) // per))
+    launches = -(-B // chunk)
+    chunk = -(-B // launches)
+    paths = torch.empty((chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch),
+                        dtype=torch.float64 if f64 else torch.float32, device=dev)
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(dev)
+    lo = torch.tensor([0.001, 0.001, 0.0, -0.2, -0.2, 0.0], dtype=torch.float64, device=dev)
+    hi = torch.tensor([1e4, 2e4, 10.0, 0.2, 0.2, 2.0], dtype=torch.float64, device=dev)
+    cur = torch.zeros(2, dtype=torch.int64, device=dev)
+    c = torch.empty((B, 6), dtype=torch.float64, device=dev)
+    f = torch.empty((B, 6), dtype=torch.float32, device=dev)
+    t = torch.empty((B, N), dtype=torch.complex128 if f64 else torch.complex64, device=dev)
+    nsync = int(L.smc_train_step_sync_bytes(T, N, M, dcode, pitch))
+    sync = torch.zeros(max(nsync, 8), dtype=torch.uint8, device=dev)
+    scheme = _lib.SCHEME_LOG_EULER | (_lib.MATH_HW if a.math == "hw" else 0)
+
+    def step():
+        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B, _lib.ptr(c),
+                                    None if f64 else _lib.ptr(f), B, T, N, M, 7, scheme, _lib.NORM_NORMALIZE, dcode,
+                                    store, _lib.ptr(paths), pitch, chunk, _lib.ptr(t), _lib.ptr(sync), nsync, None))
+
+    step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        step()
+    e1.record()
+    torch.cuda.synchronize()
+    assert _lib.sync_status(sync) == 0
+    name = L.smc_train_step_kernel(T, N, M, dcode, pitch).decode()
+    ms = e0.elapsed_time(e1) / a.iters
+    print(f"{a.config} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
+          f"({launches} launch(es) of {chunk}), checksum {float(t.abs().double().mean()):.6g}")
+
+
+if __name__ == "__main__":
+    main()
