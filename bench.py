@@ -361,9 +361,10 @@ def main() -> None:
             hits = sorted((v.get("round", ""), k) for k, v in tj.items()
                           if v.get("kernel_name") == eng.kernel_name and v.get("config") == args.config
                           and v.get("store") == args.store and v.get("math") == args.math)
-            if hits:
+            if hits:  # per-launch bytes of the profiled launch, scaled to this launch's contracts
                 traffic_src = hits[-1][1]
-                traffic = tj[traffic_src]["hbm_bytes_per_launch"]
+                ent = tj[traffic_src]
+                traffic = ent["hbm_bytes_per_launch"] / ent["contracts_per_launch"] * contracts_per_launch
         except (OSError, ValueError, KeyError):
             traffic, traffic_src = None, None
 

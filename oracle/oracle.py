@@ -241,10 +241,10 @@ def kernel_cf(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndar
 def engine_wg(timesteps: int, network_size: int, n_paths: int, with_rowsum: bool = False,
               sliced: bool = False) -> int:
     """Lanes of the engine workgroup smc_train_targets uses for an f32 training launch: 1024 for
-    resident_kernel (T = 16, 4096 | P <= 65,536, N | 4096, N <= 1024, no row sums, no workspace),
-    512 otherwise (gbm.hip resident_ok)."""
+    resident_kernel (1 <= T <= 65,536, 4096 | P <= 65,536, N | 4096, 4 <= N <= 1024, no row sums, no
+    workspace), 512 otherwise (gbm.hip resident_ok)."""
     N, P = network_size, n_paths
-    ok = (timesteps == 16 and not with_rowsum and not sliced and P % 4096 == 0 and P // 4096 <= 16
+    ok = (1 <= timesteps <= 65536 and not with_rowsum and not sliced and P % 4096 == 0 and P // 4096 <= 16
           and 4 <= N <= 1024 and 4096 % N == 0)
     return 1024 if ok else 512
 
@@ -257,7 +257,7 @@ def train_step_order(timesteps: int, network_size: int, n_paths: int) -> tuple[i
     W = 1
     while W < 8 and P > W * 65536:
         W *= 2
-    ok = (timesteps == 16 and P % (W * 4096) == 0 and P // (W * 4096) <= 16 and 4 <= N <= 1024
+    ok = (1 <= timesteps <= 65536 and P % (W * 4096) == 0 and P // (W * 4096) <= 16 and 4 <= N <= 1024
           and 4096 % N == 0)
     return (1024, W) if ok else (engine_wg(timesteps, N, P), 1)
 

@@ -284,6 +284,68 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   }
 }
 
+// The lane's 4 paths p0..p0+3 through all T rows in one rolled loop over step pairs (any T >= 1):
+// the stream, the draw order (one Box-Muller pair per path and step pair; the second normal of an
+// odd T's last pair is drawn and discarded) and the arithmetic are lane_paths'; x and the generator
+// stay in registers from row to row (no replay of earlier rows, no per-row branches).  STORE_ALL:
+// row t at row_base + t * pitch; else only the terminal row, at row_base.  The lane's 4 terminal
+// values go to x_out and their f32 sum (in f64) is added to acc.
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
+__device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<float, LOG_EULER, HW>& step, float x0,
+                                          uint64_t ordinal, int64_t chunk, float* contract_base, int T, int64_t pitch,
+                                          double& acc, float (&x_out)[kPathsPerLane]) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
+  PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));
+  constexpr bool kPacked = HW && LOG_EULER;
+  float x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
+#pragma unroll
+  for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
+  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(float)) * threadIdx.x;
+  const char* row = reinterpret_cast<const char*>(contract_base + chunk);
+  const int64_t rstride = STORE_ALL ? pitch * static_cast<int64_t>(sizeof(float)) : 0;
+  auto draw = [&] {
+    if constexpr (kPacked) {
+      s.hw_log_increments4(step.b, step.a, zl, zh);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
+    }
+  };
+  auto advance = [&](const float (&z)[kPathsPerLane]) {
+    if constexpr (kPacked) {
+      advance_packed(x, z);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], z[j]);
+    }
+  };
+  auto store = [&] { store_row(row, lane_off, float4{x[0], x[1], x[2], x[3]}); };
+#pragma unroll 1
+  for (int t = 0; t + 1 < T; t += 2) {
+    draw();
+    advance(zl);
+    if constexpr (STORE_ALL) store();
+    row += rstride;
+    advance(zh);
+    if constexpr (STORE_ALL) store();
+    row += rstride;
+  }
+  if (T & 1) {
+    draw();
+    advance(zl);
+    if constexpr (STORE_ALL) store();
+  }
+  if constexpr (!STORE_ALL) store();
+  float part = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kPathsPerLane; ++j) {
+    part += x[j];
+    x_out[j] = x[j];
+  }
+  acc += static_cast<double>(part);
+}
+
 // ---- phase 1: simulate the contract's P paths ----------------------------------------
 // Fills lds_tot[0..T) (ALLROWS) or lds_tot[T-1] with the f64 sum over paths of the row(s),
 // in a fixed order: per lane sequentially over its chunks, wave butterfly (xor 32..1),
@@ -693,6 +755,7 @@ constexpr size_t kResTermBytes = static_cast<size_t>(kResLdsChunks) * kResThread
 constexpr int kResMaxSlices = 8;
 
 constexpr int kResPreDraw = 32;  // static contracts whose Sobol rows are drawn at kernel start
+constexpr int kResMaxT = 1 << 16;  // bound on T for the rolled (T != 16) row loop
 
 size_t resident_lds_bytes(int N) {
   return kResTermBytes +
@@ -711,7 +774,7 @@ __device__ uint64_t g_trace[1024 * kTraceStride];
 #define SMC_TRACE(slot) do {} while (0)
 #endif
 
-template <bool LOG_EULER, bool HW, bool STORE_ALL>
+template <bool LOG_EULER, bool HW, bool STORE_ALL, bool T16>
 __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   typedef float v4f __attribute__((ext_vector_type(4)));
   extern __shared__ double lds[];
@@ -820,9 +883,10 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     } else {
       c = load_contract(a.contracts + b * 6);
     }
-    const Stepper<float, LOG_EULER, HW> step(c, kRowBlock);
+    const int T = T16 ? kRowBlock : a.T;
+    const Stepper<float, LOG_EULER, HW> step(c, T);
     const float x0 = static_cast<float>(c.X0);
-    float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * kRowBlock * pitch : b * pitch);
+    float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * T * pitch : b * pitch);
     const int64_t p0 = static_cast<int64_t>(slc) * nch * kResChunk;  // first path of this slice
     // chunks >= kResLdsChunks: a shift register with static indices (a rolled loop indexing a
     // register array would put it in scratch memory); chunk ch ends in slot ch - nch + kResRegChunks
@@ -830,9 +894,13 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     double acc[1] = {0.0};
     for (int ch = 0; ch < nch; ++ch) {
       float xt[kPathsPerLane];
-      lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(
-          a, step, x0, static_cast<uint64_t>(ord0 + b), p0 + static_cast<int64_t>(ch) * kResChunk, kPathsPerLane, 0,
-          kRowBlock, base, acc, xt);
+      if constexpr (T16)  // the straight-line 16-row block (the benchmark shape)
+        lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(
+            a, step, x0, static_cast<uint64_t>(ord0 + b), p0 + static_cast<int64_t>(ch) * kResChunk, kPathsPerLane,
+            0, kRowBlock, base, acc, xt);
+      else
+        lane_rows<LOG_EULER, HW, STORE_ALL>(a, step, x0, static_cast<uint64_t>(ord0 + b),
+                                            p0 + static_cast<int64_t>(ch) * kResChunk, base, T, pitch, acc[0], xt);
       if (ch < kResLdsChunks) {
         term_lds[ch * kResThreads + tid] = v4f{xt[0], xt[1], xt[2], xt[3]};
       } else {
@@ -961,7 +1029,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
 
 bool resident_ok(const EngineArgs& a, bool f32) {
   const int64_t W = a.res_slices > 1 ? a.res_slices : 1;
-  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T == kRowBlock &&
+  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T >= 1 && a.T <= kResMaxT &&
          W <= kResMaxSlices && a.P % (W * kResChunk) == 0 && a.P / (W * kResChunk) <= kResMaxChunks &&
          a.N >= 4 && a.N <= 1024 && kResChunk % a.N == 0 && (a.pitch == 0 || (a.pitch % 4 == 0 && a.pitch >= a.P)) &&
          (W == 1 || (a.res_cnt && a.res_xsum && a.res_xcol && a.done));
@@ -1213,7 +1281,8 @@ int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
 
 template <bool LOG_EULER, bool HW, bool STORE_ALL>
 int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
-  auto kernel = resident_kernel<LOG_EULER, HW, STORE_ALL>;
+  auto kernel = a.T == kRowBlock ? resident_kernel<LOG_EULER, HW, STORE_ALL, true>
+                                 : resident_kernel<LOG_EULER, HW, STORE_ALL, false>;
   const size_t lds = resident_lds_bytes(a.N);
   if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
