@@ -50,7 +50,15 @@ CONFIGS = {
     "c5": (8192, 16, 256, 512, [32, 32],
            "C5: 8192 contracts x 131072 paths (N=256 x M=512), 4 correlated assets, T=16, basket put, "
            "3-layer CVNN 16->32->32->256 fp32"),
+    # the reference's other legal shapes (not BASELINE configs; parity-tested, timed for coverage):
+    # the lock-step trainer shape (tests/test_gbm_trainer.py:122-131, T = 1, N = 16, M = 4096) at C2's
+    # batch, and C2 in float64 (Precision.float64: f64 paths, complex128 targets, f64 CVNN)
+    "lockstep": (4096, 1, 16, 4096, [32, 32],
+                 "lock-step shape: 4096 contracts x 65536 paths (N=16 x M=4096), T=1, 3-layer CVNN 6->32->32->16 fp32"),
+    "c2f64": (4096, 16, 256, 256, [32, 32],
+              "C2 in float64: 4096 contracts x 65536 paths (N=256 x M=256), T=16, 3-layer CVNN 6->32->32->256 fp64"),
 }
+SIM_DTYPE = {"c2f64": "float64"}  # default float32
 BASKET_ASSETS = {"c5": 4}
 NETWORK_COMPUTE = {"c3": "bf16"}  # default "auto": f32 on the f32 MFMA kernels
 MFMA_PEAK_TFLOPS = {"mfma_bf16": 2516.6, "mfma_f32": 157.3, "valu": 157.3}  # MI355X_MICROARCH.md, dense
@@ -75,10 +83,11 @@ def parse() -> argparse.Namespace:
     return ap.parse_args()
 
 
-def algorithmic_bytes_per_contract(T: int, N: int, M: int, store_all: bool) -> int:
-    """path matrix store + terminal-row re-read + complex64 targets (+ 48 B contract in)."""
+def algorithmic_bytes_per_contract(T: int, N: int, M: int, store_all: bool, esz: int = 4) -> int:
+    """SURVEY §8(d): path matrix store + terminal-row re-read + complex targets (+ 48 B contract in);
+    esz = 4 (f32 paths, complex64 targets) or 8 (f64, complex128)."""
     P = N * M
-    return (T * P * 4 if store_all else P * 4) + P * 4 + N * 8
+    return (T * P * esz if store_all else P * esz) + P * esz + N * 2 * esz
 
 
 def cpu_threads() -> int:
@@ -89,7 +98,8 @@ def cpu_threads() -> int:
     return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
 
 
-def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: float, n_assets: int = 0) -> dict:
+def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: float, n_assets: int = 0,
+                 dtype: str = "float32") -> dict:
     """The reference CPU path (north_star: torch-cpu + numpy.fft; oracle/torch_cpu.py) timed on the
     host cores: MC for a time-boxed sample of the B contracts (extrapolated to B) + one full-size
     CVNN/Adam step on torch-cpu; plus C1 (BASELINE configs[0]) timed over 10 whole steps, and the
@@ -127,14 +137,15 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
                                  budget_s * 0.8, threads)
         path = "oracle C basket kernel-mode (f32)"
     else:
-        per_c, done, tg = sample(lambda c, o: cpu_path_targets(c, T, N, M, 7, o, normals="numpy"),
+        per_c, done, tg = sample(lambda c, o: cpu_path_targets(c, T, N, M, 7, o, dtype=dtype, normals="numpy"),
                                  budget_s * 0.6, 2 * threads)
         path = ("torch-cpu paths (f64 recursion, numpy default_rng normals per contract) + numpy.fft "
                 "(oracle/torch_cpu.py)")
-    model = make_test_cvnn(n_inputs=contracts.shape[1], n_outputs=N, seed=123, dtype=torch.float32, device="cpu",
+    tdt = torch.float64 if dtype == "float64" else torch.float32
+    model = make_test_cvnn(n_inputs=contracts.shape[1], n_outputs=N, seed=123, dtype=tdt, device="cpu",
                            hidden_layers=len(widths), hidden_width=widths[0])
     adam = torch.optim.Adam(model.parameters(), lr=1e-2)
-    x = torch.tensor(contracts, dtype=torch.float32)
+    x = torch.tensor(contracts, dtype=tdt)
     tgt = torch.from_numpy(np.concatenate(tg))
     tgt = tgt.repeat((B + tgt.shape[0] - 1) // tgt.shape[0], 1)[:B]
     oracle.torch_step(model, x, torch.zeros_like(x), tgt, adam)  # warm
@@ -165,7 +176,7 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
     }
     if not n_assets:
         # second leg: the C/OpenMP oracle (f64 recursion, this build's normal streams)
-        per_c2, done2, _ = sample(lambda c, o: oracle.training_targets(c, T, N, M, seed=7, ordinal0=o),
+        per_c2, done2, _ = sample(lambda c, o: oracle.training_targets(c, T, N, M, seed=7, ordinal0=o, dtype=dtype),
                                   budget_s * 0.2, threads)
         line["c_openmp_leg"] = {"value": B * N * M / (per_c2 * B + t_nn), "unit": "contracts*paths/s",
                                 "cores": threads, "kind": "port",
@@ -214,12 +225,14 @@ def main() -> None:
 
     B, T, N, M, widths, desc = CONFIGS[args.config]
     P = N * M
+    f64 = SIM_DTYPE.get(args.config) == "float64"
+    esz = 8 if f64 else 4
     sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=M, threads_per_block=256,
-                                mc_seed=7, buffer_size=512, dtype=Precision.float32)
+                                mc_seed=7, buffer_size=512, dtype=Precision.float64 if f64 else Precision.float32)
     n_assets = BASKET_ASSETS.get(args.config, 0)
     n_inputs = 3 * n_assets + 4 if n_assets else 6
-    model = make_test_cvnn(n_inputs=n_inputs, n_outputs=N, seed=123, dtype=torch.float32, device=dev,
-                           hidden_layers=len(widths), hidden_width=widths[0])
+    model = make_test_cvnn(n_inputs=n_inputs, n_outputs=N, seed=123, dtype=torch.float64 if f64 else torch.float32,
+                           device=dev, hidden_layers=len(widths), hidden_width=widths[0])
     cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
                                domain_bounds=make_domain_bounds())
     pricer = expect_success(GbmCVNNPricer.create(cfg))
@@ -285,7 +298,7 @@ def main() -> None:
     if n_assets:
         bytes_launch = eng.algorithmic_bytes_per_contract() * contracts_per_launch
     else:
-        bytes_launch = algorithmic_bytes_per_contract(T, N, M, pricer.store_paths) * contracts_per_launch + \
+        bytes_launch = algorithmic_bytes_per_contract(T, N, M, pricer.store_paths, esz) * contracts_per_launch + \
             48 * contracts_per_launch
     # live: HIP events on the MC stream around each MC-part launch inside the timed region
     # (Sobol draw + path/CF kernel + cursor update; the path/CF kernel is >99 % of it)
@@ -314,7 +327,7 @@ def main() -> None:
         n1.synchronize()
         net_ms = n0.elapsed_time(n1) / args.kernel_iters
         kern = fused.kernels
-        peak = MFMA_PEAK_TFLOPS[kern]
+        peak = 78.6 if (f64 and kern == "valu") else MFMA_PEAK_TFLOPS[kern]  # f64 vector peak (dense)
         desc_k = {"mfma_bf16": "pack + fb + wgrad (csrc/cvnn_mfma.hip, v_mfma_f32_16x16x32_bf16, bf16 operands, "
                                "f32 accumulate / master weights) + reduce/Adam + finalize",
                   "mfma_f32": "pack + fb + wgrad (csrc/cvnn_mfma.hip, v_mfma_f32_16x16x4_f32) + reduce/Adam + "
@@ -383,8 +396,9 @@ def main() -> None:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "network_dtype": ({"mfma_bf16": "bf16 operands, f32 accumulate / master weights"}.get(network["compute"], "f32")
+        "dtype": "f64" if f64 else "f32",
+        "network_dtype": ("f64" if f64 else
+                          {"mfma_bf16": "bf16 operands, f32 accumulate / master weights"}.get(network["compute"], "f32")
                           if network else "f32 (torch-ROCm modules)"),
         "data": ("synthetic: Sobol basket contracts (seed 7, basket.default_basket_bounds), random-init CVNN (seed 123)"
                  if n_assets else
@@ -406,7 +420,7 @@ def main() -> None:
         "final_loss": final.loss,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(B, T, N, M, widths, args.cpu_seconds, n_assets)
+        cb = cpu_baseline(B, T, N, M, widths, args.cpu_seconds, n_assets, "float64" if f64 else "float32")
         line["cpu_baseline"] = cb
         line["speedup_vs_cpu"] = value / cb["value"]
     if rank == 0:

@@ -109,6 +109,29 @@ __global__ __launch_bounds__(NT) void interleaved(float* out) {
   }
 }
 
+// chip-wide contracts: wave w of workgroup c owns contract (r * NW + w)'s path slice c (64 lanes x 4
+// paths = 256 paths; 256 workgroups cover a 65,536-path contract), so the same-numbered waves of all
+// workgroups write one contract row's 256 KiB window at about the same time
+template <int NT>
+__global__ __launch_bounds__(NT) void chipwide(float* out) {
+  constexpr int NW = NT / 64;
+  const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+  const int slices = static_cast<int>(P / 256);  // 256 paths per wave slice
+  for (int64_t task = static_cast<int64_t>(blockIdx.x) * NW + w; task < static_cast<int64_t>(B) * slices;
+       task += static_cast<int64_t>(gridDim.x) * NW) {
+    // tasks ordered so that consecutive workgroups take neighbouring slices of one contract
+    const int64_t b = (task / NW) / slices * NW + task % NW;
+    const int64_t sl = (task / NW) % slices;
+    float* base = out + b * T * PITCH + sl * 256;
+    v4f v = {1.f + b, 2.f, 3.f, static_cast<float>(l)};
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(base + t * PITCH), l * 16u, 0, 0);
+      v.x += 1.f;
+    }
+  }
+}
+
 // linear grid-stride fill over the whole padded matrix (hipMemset's __amd_rocclr_fillBufferAligned
 // runs 256 x 256 threads of this shape)
 template <int NT>
@@ -158,6 +181,9 @@ int main() {
     timeit("interleaved K16384 nt1024", [&] { interleaved<1024, 16384><<<cus, 1024>>>(out); });
     timeit("interleaved K4096 nt512", [&] { interleaved<512, 4096><<<cus, 512>>>(out); });
     timeit("interleaved K2048 nt512", [&] { interleaved<512, 2048><<<cus, 512>>>(out); });
+    timeit("chipwide nt1024 x256", [&] { chipwide<1024><<<256, 1024>>>(out); });
+    timeit("chipwide nt256 x256", [&] { chipwide<256><<<256, 256>>>(out); });
+    timeit("chipwide nt512 x256", [&] { chipwide<512><<<256, 512>>>(out); });
     timeit("rowmaj nt256", [&] { rowmaj<256, 0><<<cus, 256>>>(out); });
     timeit("rowmaj nt256 x2/CU", [&] { rowmaj<256, 0><<<2 * cus, 256>>>(out); });
     timeit("rowmaj nt128", [&] { rowmaj<128, 0><<<cus, 128>>>(out); });
