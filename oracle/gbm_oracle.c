@@ -13,7 +13,7 @@
  *             seeds MWC64X (Thomas 2011) per (contract ordinal, group of 4 paths);
  *             per step pair, the group's 4 paths draw one Box-Muller pair each, in path order.
  *             f32: ln / sin / cos from the portable IEEE-only kernels below (bit-identical
- *             to the device's); f64: libm.
+ *             to the device's); f64: the 32-bit-uniform log / sincos below (bit-identical too).
  *
  * Two modes:
  *   REFERENCE  (oracle_gbm_paths): reference src/spectralmc/gbm.py:241-257 — the Numba
@@ -178,6 +178,96 @@ static void twiddle(int64_t j, int64_t N, double* s_out, double* c_out) {
   *c_out = ((q + 1) & 2) ? -cb : cb;
 }
 
+/* ---- f64 normals: op-for-op restatement of smc_math.h log_u32 / sincos2pi_u32 ---------- */
+static inline uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
+static inline double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+
+static double log_u32(uint32_t a) {
+  const double m = (double)a + 1.0;
+  const uint64_t bits = d2u(m);
+  int e = (int)(bits >> 52) - 1023;
+  uint64_t fb = (bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
+  const int hi = fb > 0x3FF6A09E667F3BCDull;
+  if (hi) { fb -= 0x0010000000000000ull; e += 1; }
+  const double f = u2d(fb);
+  const double sn = (f - 1.0) / (f + 1.0);
+  const double t = sn * sn;
+  double p = 0.08695652173913043;
+  p = fma(p, t, 0.09523809523809523);
+  p = fma(p, t, 0.10526315789473684);
+  p = fma(p, t, 0.11764705882352941);
+  p = fma(p, t, 0.13333333333333333);
+  p = fma(p, t, 0.15384615384615385);
+  p = fma(p, t, 0.18181818181818182);
+  p = fma(p, t, 0.2222222222222222);
+  p = fma(p, t, 0.2857142857142857);
+  p = fma(p, t, 0.4);
+  p = fma(p, t, 0.6666666666666666);
+  const double lf = fma(sn * t, p, 2.0 * sn);
+  const double k = (double)(e - 32);
+  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, lf));
+}
+
+static void sincos_series(double x, double* s_out, double* c_out) {
+  const double u = x * x;
+  double s = 2.8114572543455206e-15;
+  s = fma(s, -u, 7.647163731819816e-13);
+  s = fma(s, -u, 1.6059043836821613e-10);
+  s = fma(s, -u, 2.505210838544172e-08);
+  s = fma(s, -u, 2.7557319223985893e-06);
+  s = fma(s, -u, 0.0001984126984126984);
+  s = fma(s, -u, 0.008333333333333333);
+  s = fma(s, -u, 0.16666666666666666);
+  s = fma(s, -u, 1.0);
+  *s_out = s * x;
+  double c = 1.5619206968586225e-16;
+  c = fma(c, -u, 4.779477332387385e-14);
+  c = fma(c, -u, 1.1470745597729725e-11);
+  c = fma(c, -u, 2.08767569878681e-09);
+  c = fma(c, -u, 2.755731922398589e-07);
+  c = fma(c, -u, 2.48015873015873e-05);
+  c = fma(c, -u, 0.001388888888888889);
+  c = fma(c, -u, 0.041666666666666664);
+  c = fma(c, -u, 0.5);
+  *c_out = fma(c, -u, 1.0);
+}
+
+static void sincos2pi_u32(uint32_t b, double* s_out, double* c_out) {
+  const uint32_t k = (b + (1u << 29)) >> 30;
+  const int32_t rem = (int32_t)(b - (k << 30));
+  const double x = (double)rem * 0x1p-32 * 6.283185307179586;
+  double s, c;
+  sincos_series(x, &s, &c);
+  const int odd = (k & 1u) != 0u;
+  const double sb = odd ? c : s, cb = odd ? s : c;
+  *s_out = (k & 2u) ? -sb : sb;
+  *c_out = ((k + 1u) & 2u) ? -cb : cb;
+}
+
+/* e^y as smc_math.h exp_f64 (the f64 device recursion; the oracle's reference mode keeps libm exp) */
+double oracle_exp_f64(double y) {
+  const double n = rint(y * 1.4426950408889634);
+  double r = fma(-n, 0.6931471803691238, y);
+  r = fma(-n, 1.9082149292705877e-10, r);
+  double p = 1.6059043836821613e-10;
+  p = fma(p, r, 2.08767569878681e-09);
+  p = fma(p, r, 2.505210838544172e-08);
+  p = fma(p, r, 2.755731922398589e-07);
+  p = fma(p, r, 2.7557319223985893e-06);
+  p = fma(p, r, 2.48015873015873e-05);
+  p = fma(p, r, 0.0001984126984126984);
+  p = fma(p, r, 0.001388888888888889);
+  p = fma(p, r, 0.008333333333333333);
+  p = fma(p, r, 0.041666666666666664);
+  p = fma(p, r, 0.16666666666666666);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, (int)n);
+}
+double oracle_log_u32(uint32_t a) { return log_u32(a); }
+void oracle_sincos2pi_u32(uint32_t b, double* s, double* c) { sincos2pi_u32(b, s, c); }
+
 float oracle_log_pos(float u) { return log_pos(u); }
 float oracle_exp2(float y) { return exp2_any(y); }
 void oracle_sincos2pi_u24(uint32_t j, float* s, float* c) { sincos2pi_u24(j, s, c); }
@@ -206,16 +296,16 @@ void oracle_stream_u32(uint64_t seed, uint64_t ordinal, uint64_t group, int64_t 
 }
 
 /* One Box-Muller pair.  f32: 23-bit uniforms and the portable kernels (bit-identical to the
- * device); f64: 32-bit uniforms and libm. */
+ * device); f64: 32-bit uniforms and the log_u32 / sincos2pi_u32 sequences above (bit-identical). */
 static void normal_pair(mwc64x* g, int is_f64, double* z0, double* z1) {
   const uint32_t a = mwc_next(g), b = mwc_next(g);
   if (is_f64) {
-    const double u1 = ((double)a + 1.0) * 0x1p-32;
-    const double u2 = (double)b * 0x1p-32;
-    const double r = sqrt(-2.0 * log(u1));
-    const double th = 6.283185307179586476925286766559 * u2;
-    *z0 = r * cos(th);
-    *z1 = r * sin(th);
+    /* u1 = (a + 1) 2^-32, angle b 2^-32 revolutions: smc_math.h log_u32 / sincos2pi_u32 */
+    const double r = sqrt(-2.0 * log_u32(a));
+    double sn, cs;
+    sincos2pi_u32(b, &sn, &cs);
+    *z0 = r * cs;
+    *z1 = r * sn;
   } else {
     /* u1 = 2 - (1.m) with m = a >> 9: (0, 1] on the 2^-23 grid, exact; angle (b >> 9) 2^-23 rev */
     const float u1 = 2.0f - u2f(0x3F800000u | (a >> 9));

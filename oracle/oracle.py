@@ -73,6 +73,11 @@ def lib() -> ctypes.CDLL:
                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_basket_cholesky.argtypes = [ctypes.c_int32, ctypes.c_double, ctypes.c_void_p]
+        L.oracle_log_u32.argtypes = [ctypes.c_uint32]
+        L.oracle_log_u32.restype = ctypes.c_double
+        L.oracle_exp_f64.argtypes = [ctypes.c_double]
+        L.oracle_exp_f64.restype = ctypes.c_double
+        L.oracle_sincos2pi_u32.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_log_pos.argtypes = [ctypes.c_float]
         L.oracle_log_pos.restype = ctypes.c_float
         L.oracle_exp2.argtypes = [ctypes.c_float]
@@ -103,6 +108,23 @@ def stream_u32(seed: int, ordinal: int, group: int, n: int) -> np.ndarray:
     out = np.empty(n, dtype=np.uint32)
     lib().oracle_stream_u32(seed, ordinal, group, n, _ptr(out))
     return out
+
+
+def log_u32(a: int) -> float:
+    """ln((a + 1) 2^-32): the f64 Box-Muller radius' log (csrc/smc_math.h log_u32)."""
+    return float(lib().oracle_log_u32(a))
+
+
+def sincos2pi_u32(b: int) -> tuple[float, float]:
+    """(sin, cos)(2 pi b 2^-32) (csrc/smc_math.h sincos2pi_u32)."""
+    s, c = ctypes.c_double(), ctypes.c_double()
+    lib().oracle_sincos2pi_u32(b, ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+def exp_f64(y: float) -> float:
+    """e^y as the f64 device path recursion computes it (csrc/smc_math.h exp_f64)."""
+    return float(lib().oracle_exp_f64(y))
 
 
 def normals(seed: int, ordinal: int, rows: int, cols: int, dtype: str = "float32") -> np.ndarray:

@@ -168,7 +168,7 @@ struct Stepper {
     if constexpr (LOG_EULER) {
       if constexpr (sizeof(Real) == 4 && HW) return x * __builtin_amdgcn_exp2f(fmaf(b, z, a));
       else if constexpr (sizeof(Real) == 4) return x * math::exp2_any(fmaf(b, z, a));
-      else return x * exp(fma(b, z, a));
+      else return x * math::exp_f64(fma(b, z, a));
     }
     if constexpr (sizeof(Real) == 4) return fabsf(fmaf(x, fmaf(b, z, a), x));
     else return fabs(fma(x, fma(b, z, a), x));
@@ -289,21 +289,21 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
 // odd T's last pair is drawn and discarded) and the arithmetic are lane_paths'; x and the generator
 // stay in registers from row to row (no replay of earlier rows, no per-row branches).  STORE_ALL:
 // row t at row_base + t * pitch; else only the terminal row, at row_base.  The lane's 4 terminal
-// values go to x_out and their f32 sum (in f64) is added to acc.
-template <bool LOG_EULER, bool HW, bool STORE_ALL>
-__device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<float, LOG_EULER, HW>& step, float x0,
-                                          uint64_t ordinal, int64_t chunk, float* contract_base, int T, int64_t pitch,
-                                          double& acc, float (&x_out)[kPathsPerLane]) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
+// values go to x_out and their sum (f32 sum for f32 paths, then f64) is added to acc.
+template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
+__device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
+                                          uint64_t ordinal, int64_t chunk, Real* contract_base, int T, int64_t pitch,
+                                          double& acc, Real (&x_out)[kPathsPerLane]) {
+  using V4 = typename Vec4T<Real>::type;
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));
-  constexpr bool kPacked = HW && LOG_EULER;
-  float x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
+  constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
+  Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
 #pragma unroll
   for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
-  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(float)) * threadIdx.x;
+  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(Real)) * threadIdx.x;
   const char* row = reinterpret_cast<const char*>(contract_base + chunk);
-  const int64_t rstride = STORE_ALL ? pitch * static_cast<int64_t>(sizeof(float)) : 0;
+  const int64_t rstride = STORE_ALL ? pitch * static_cast<int64_t>(sizeof(Real)) : 0;
   auto draw = [&] {
     if constexpr (kPacked) {
       s.hw_log_increments4(step.b, step.a, zl, zh);
@@ -312,7 +312,7 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<flo
       for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
     }
   };
-  auto advance = [&](const float (&z)[kPathsPerLane]) {
+  auto advance = [&](const Real (&z)[kPathsPerLane]) {
     if constexpr (kPacked) {
       advance_packed(x, z);
     } else {
@@ -320,7 +320,14 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<flo
       for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], z[j]);
     }
   };
-  auto store = [&] { store_row(row, lane_off, float4{x[0], x[1], x[2], x[3]}); };
+  auto store = [&] {
+    V4 v;
+    v.x = x[0];
+    v.y = x[1];
+    v.z = x[2];
+    v.w = x[3];
+    store_row(row, lane_off, v);
+  };
 #pragma unroll 1
   for (int t = 0; t + 1 < T; t += 2) {
     draw();
@@ -337,7 +344,7 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<flo
     if constexpr (STORE_ALL) store();
   }
   if constexpr (!STORE_ALL) store();
-  float part = 0.0f;
+  Real part = 0;
 #pragma unroll
   for (int j = 0; j < kPathsPerLane; ++j) {
     part += x[j];
@@ -666,10 +673,12 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void contract_kernel(Engi
 // cf_kernel then streams all terminal rows back at full read bandwidth, one workgroup per
 // contract.  Same arithmetic and orders as contract_kernel: bit-identical targets.
 // f32 scratch only (split_ok): the first 8-B-aligned padding slot after column P of the terminal row
+// (f64 scratch: the first element after column P)
+template <typename Real = float>
 __device__ __forceinline__ double* pad_sum(const EngineArgs& a, int64_t b) {
   const int64_t pitch = a.pitch ? a.pitch : a.P;
   const int64_t row = a.store == SMC_STORE_ALL ? (b * a.T + (a.T - 1)) * pitch : b * pitch;
-  return reinterpret_cast<double*>(static_cast<float*>(a.paths) + row + a.P + (a.P & 1));
+  return reinterpret_cast<double*>(static_cast<Real*>(a.paths) + row + a.P + (sizeof(Real) == 4 ? (a.P & 1) : 0));
 }
 
 // STRAIGHT (T == 16, P a multiple of 2048): only the straight-line 16-row block is compiled in
@@ -720,7 +729,43 @@ __global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
   extern __shared__ double lds[];
   const int64_t b = blockIdx.x;
   const Contract c = load_contract(a.contracts + b * 6);
-  cf_targets_contract<Real>(a, c, b, *pad_sum(a, b), lds);
+  cf_targets_contract<Real>(a, c, b, *pad_sum<Real>(a, b), lds);
+}
+
+// rows_kernel: the split pair's path kernel for any T (f64 and the f32 shapes the resident kernel
+// does not take): persistent workgroups (contracts blockIdx.x, + gridDim.x, ...), every lane's 4 paths
+// of each 2048-path chunk through all T rows in registers (lane_rows: no replay, one rolled loop), the
+// f64 terminal-row sum into the row padding for cf_kernel.  Terminal-sum order: lane over its chunks,
+// wave butterfly, waves 0..7 (oracle kernel mode, wg = 512; paths_kernel's order).
+template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
+__global__ __launch_bounds__(kThreads) void rows_kernel(EngineArgs a) {
+  extern __shared__ double lds[];
+  const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
+  const int64_t pitch = a.pitch ? a.pitch : a.P;
+  const int T = a.T;
+  int parity = 0;
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x, parity ^= 1) {
+    const Contract c = load_contract(a.contracts + b * 6);
+    const Stepper<Real, LOG_EULER, HW> step(c, T);
+    const Real x0 = static_cast<Real>(c.X0);
+    Real* base = static_cast<Real*>(a.paths) + (STORE_ALL ? b * T * pitch : b * pitch);
+    double acc = 0.0;
+    for (int64_t chunk = 0; chunk < a.P; chunk += kChunk) {
+      Real xt[kPathsPerLane];
+      lane_rows<Real, LOG_EULER, HW, STORE_ALL>(a, step, x0, static_cast<uint64_t>(ord0 + b), chunk, base, T, pitch,
+                                                acc, xt);
+    }
+    // wave sums in a double-buffered LDS slot: the next contract writes the other slot
+    const double w = wave_sum(acc);
+    double* ws = lds + parity * kWaves;
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = w;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      double tot = 0.0;
+      for (int k = 0; k < kWaves; ++k) tot += ws[k];
+      *pad_sum<Real>(a, b) = tot;
+    }
+  }
 }
 
 // ---- resident_kernel: the terminal row never leaves the chip -----------------------------------
@@ -899,7 +944,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
             a, step, x0, static_cast<uint64_t>(ord0 + b), p0 + static_cast<int64_t>(ch) * kResChunk, kPathsPerLane,
             0, kRowBlock, base, acc, xt);
       else
-        lane_rows<LOG_EULER, HW, STORE_ALL>(a, step, x0, static_cast<uint64_t>(ord0 + b),
+        lane_rows<float, LOG_EULER, HW, STORE_ALL>(a, step, x0, static_cast<uint64_t>(ord0 + b),
                                             p0 + static_cast<int64_t>(ch) * kResChunk, base, T, pitch, acc[0], xt);
       if (ch < kResLdsChunks) {
         term_lds[ch * kResThreads + tid] = v4f{xt[0], xt[1], xt[2], xt[3]};
@@ -1068,6 +1113,14 @@ ResSyncLayout res_sync_layout(int32_t W, int32_t N, int cus) {
 bool split_ok(const EngineArgs& a, bool f32) {
   const int64_t pitch = a.pitch ? a.pitch : a.P;
   return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && pitch >= a.P + (a.P & 1) + 2;
+}
+
+// rows_kernel + cf_kernel: whole 2048-path chunks, padding for the f64 terminal sum (f32: 2 floats
+// after an 8-B-aligned column P; f64: one element)
+bool rows_ok(const EngineArgs& a, bool f32) {
+  const int64_t pitch = a.pitch ? a.pitch : a.P;
+  return a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T >= 1 && a.P % kChunk == 0 &&
+         pitch >= a.P + (f32 ? (a.P & 1) + 2 : 1) && (a.store == SMC_STORE_ALL || a.store == SMC_STORE_TERMINAL);
 }
 
 // Sliced contracts on persistent workgroups.  Contract b belongs to queue b mod 8; a workgroup
@@ -1279,6 +1332,25 @@ int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
   return check_launch("cf_kernel");
 }
 
+template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
+int32_t launch_rows_k(const EngineArgs& a, hipStream_t stream) {
+  const size_t lds1 = 2 * kWaves * sizeof(double), lds2 = lds_bytes(a.T, a.N, true);
+  auto k1 = rows_kernel<Real, LOG_EULER, HW, STORE_ALL>;
+  auto k2 = cf_kernel<Real>;
+  if (lds2 > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(k2),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               static_cast<int>(lds2)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "cf_kernel: cannot raise the dynamic LDS limit");
+  }
+  unsigned grid1 = 0;
+  if (int32_t st = resident_grid(reinterpret_cast<const void*>(k1), kThreads, lds1, a.B, &grid1)) return st;
+  hipLaunchKernelGGL(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
+  if (int32_t st = check_launch("rows_kernel")) return st;
+  hipLaunchKernelGGL(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
+  return check_launch("cf_kernel");
+}
+
 template <bool LOG_EULER, bool HW, bool STORE_ALL>
 int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
   auto kernel = a.T == kRowBlock ? resident_kernel<LOG_EULER, HW, STORE_ALL, true>
@@ -1332,10 +1404,13 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
       SMC_RES(false, false, false)
 #undef SMC_RES
     }
-    if (SMC_TRAIN_MODE >= 2 && split_ok(a, true)) {
+    // the split pair: the straight-line T = 16 paths_kernel, or (ragged chunks) simulate_contract;
+    // other whole-chunk shapes take rows_kernel below
+    const bool straight_split = a.T == kRowBlock && a.P % kChunk == 0;
+    if (SMC_TRAIN_MODE >= 2 && split_ok(a, true) && (straight_split || !rows_ok(a, true))) {
       const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
       const bool hw = (a.scheme & SMC_MATH_HW) != 0;
-      const bool straight = a.T == kRowBlock && a.P % kChunk == 0;
+      const bool straight = straight_split;
       const bool sa = a.store == SMC_STORE_ALL;
 #define SMC_SPLIT(LE, HWM, ST, SA) \
   if (log_euler == LE && hw == HWM && straight == ST && (!ST || sa == SA)) return launch_split_k<LE, HWM, ST, SA>(a, stream);
@@ -1353,6 +1428,24 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
       SMC_SPLIT(false, false, false, true)
 #undef SMC_SPLIT
     }
+  }
+  if (SMC_TRAIN_MODE >= 2 && rows_ok(a, sizeof(Real) == 4)) {
+    const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+    const bool hw = (a.scheme & SMC_MATH_HW) != 0 && sizeof(Real) == 4;
+    const bool sa = a.store == SMC_STORE_ALL;
+#define SMC_ROWS(LE, HWM, SA) \
+  if (log_euler == LE && hw == HWM && sa == SA) return launch_rows_k<Real, LE, HWM, SA>(a, stream);
+    SMC_ROWS(true, false, true)
+    SMC_ROWS(true, false, false)
+    SMC_ROWS(false, false, true)
+    SMC_ROWS(false, false, false)
+    if constexpr (sizeof(Real) == 4) {
+      SMC_ROWS(true, true, true)
+      SMC_ROWS(true, true, false)
+      SMC_ROWS(false, true, true)
+      SMC_ROWS(false, true, false)
+    }
+#undef SMC_ROWS
   }
   if (a.slices < 1 || !a.simulate) a.slices = 1;
   if (a.slices > 1 && (!a.partials || !a.arrivals || !a.queues))
@@ -1661,8 +1754,11 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.pitch = path_pitch;
   a.slices = slices_for(n_paths, sliced != 0);
   a.store = SMC_STORE_ALL;
-  if (SMC_TRAIN_MODE == 3 && resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "resident_kernel";
-  if (SMC_TRAIN_MODE >= 2 && split_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "paths_kernel+cf_kernel";
+  const bool f32 = (dtype & 0xff) == SMC_DTYPE_F32;
+  if (SMC_TRAIN_MODE == 3 && resident_ok(a, f32)) return "resident_kernel";
+  if (SMC_TRAIN_MODE >= 2 && split_ok(a, f32) && a.T == kRowBlock && a.P % kChunk == 0) return "paths_kernel+cf_kernel";
+  if (SMC_TRAIN_MODE >= 2 && rows_ok(a, f32)) return "rows_kernel+cf_kernel";
+  if (SMC_TRAIN_MODE >= 2 && split_ok(a, f32)) return "paths_kernel+cf_kernel";
   return a.slices > 1 ? "queue_kernel" : "contract_kernel";
 }
 

@@ -39,6 +39,15 @@ __device__ __forceinline__ void store_row(const void* row_base, uint32_t off, fl
   const v4f w = {v.x, v.y, v.z, v.w};
   __builtin_amdgcn_raw_buffer_store_b128(w, row_rsrc(row_base), off, 0, 0);
 }
+// 4 doubles (32 B) of an f64 path row: two 16-B pieces at off and off + 16.
+__device__ __forceinline__ void store_row(const void* row_base, uint32_t off, double4 v) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  const v2d lo = {v.x, v.y}, hi = {v.z, v.w};
+  const __amdgpu_buffer_rsrc_t r = row_rsrc(row_base);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, lo), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, hi), r, off + 16, 0, 0);
+}
 template <typename U>
 __device__ __forceinline__ void put_sc1(U* p, U v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -107,14 +107,8 @@ __device__ __forceinline__ float exp2_any(float y) {
 __device__ __forceinline__ float exp_any(float x) { return exp2_any(x * 1.44269502f); }
 
 // ---- f64: twiddles cos/sin(2 pi j / N) of the N-point DFT -------------------------------
-// Exact integer reduction to the nearest quarter turn, then Taylor series in x = 2 pi r,
-// |x| <= pi/4 (terms to x^17 / x^18: truncation < 1e-19).
-__device__ __forceinline__ void twiddle(int64_t j, int64_t N, double& s_out, double& c_out) {
-  const int64_t num = 4 * j;
-  const int64_t k = (2 * num + N) / (2 * N);         // round(4 j / N)
-  const int64_t rem = num - k * N;                    // |rem| <= N / 2
-  const double r = static_cast<double>(rem) / static_cast<double>(4 * N);
-  const double x = r * 6.283185307179586;
+// (sin, cos)(x) for |x| <= pi/4: Taylor series to x^17 / x^18 (truncation < 1e-19)
+__device__ __forceinline__ void sincos_series(double x, double& s_out, double& c_out) {
   const double u = x * x;
   double s = 2.8114572543455206e-15;                   // 1/17!
   s = fma(s, -u, 7.647163731819816e-13);               // 1/15!
@@ -125,7 +119,7 @@ __device__ __forceinline__ void twiddle(int64_t j, int64_t N, double& s_out, dou
   s = fma(s, -u, 0.008333333333333333);                // 1/5!
   s = fma(s, -u, 0.16666666666666666);                 // 1/3!
   s = fma(s, -u, 1.0);
-  s = s * x;
+  s_out = s * x;
   double c = 1.5619206968586225e-16;                   // 1/18!
   c = fma(c, -u, 4.779477332387385e-14);               // 1/16!
   c = fma(c, -u, 1.1470745597729725e-11);              // 1/14!
@@ -135,12 +129,99 @@ __device__ __forceinline__ void twiddle(int64_t j, int64_t N, double& s_out, dou
   c = fma(c, -u, 0.001388888888888889);                // 1/6!
   c = fma(c, -u, 0.041666666666666664);                // 1/4!
   c = fma(c, -u, 0.5);                                 // 1/2!
-  c = fma(c, -u, 1.0);
+  c_out = fma(c, -u, 1.0);
+}
+
+// Exact integer reduction to the nearest quarter turn, then Taylor series in x = 2 pi r,
+// |x| <= pi/4 (terms to x^17 / x^18: truncation < 1e-19).
+__device__ __forceinline__ void twiddle(int64_t j, int64_t N, double& s_out, double& c_out) {
+  const int64_t num = 4 * j;
+  const int64_t k = (2 * num + N) / (2 * N);         // round(4 j / N)
+  const int64_t rem = num - k * N;                    // |rem| <= N / 2
+  const double r = static_cast<double>(rem) / static_cast<double>(4 * N);
+  const double x = r * 6.283185307179586;
+  double s, c;
+  sincos_series(x, s, c);
   const int q = static_cast<int>(k & 3);
   const bool odd = (q & 1) != 0;
   const double sb = odd ? c : s, cb = odd ? s : c;
   s_out = (q & 2) ? -sb : sb;
   c_out = ((q + 1) & 2) ? -cb : cb;
+}
+
+// ---- f64 path engine: the Box-Muller transcendentals of 32-bit uniforms and exp ------------
+// Fixed IEEE-754 sequences (fma, +, -, *, correctly rounded / and sqrt, rint, exact ldexp and bit
+// manipulation), restated op for op by oracle/gbm_oracle.c, so f64 normals are bit-identical on the
+// CPU.  Each is a fraction of the generic OCML routine's VALU work (log 98, sincospi 71, exp 42
+// instructions) because the argument domain is known: the uniforms are 32-bit integers.
+
+// ln((a + 1) 2^-32) for a 32-bit a: m = a + 1 = 2^e f exactly, f folded into [sqrt(1/2), sqrt(2)),
+// ln f = 2 atanh(s), s = (f - 1) / (f + 1), |s| <= 0.1716: 2 s + s t P(t), t = s^2, P to t^10
+// (truncation < 2e-19); then + (e - 32) ln 2, ln 2 as a double plus its 2.3e-17 remainder, fused.
+__device__ __forceinline__ double log_u32(uint32_t a) {
+  const double m = static_cast<double>(a) + 1.0;  // exact: a + 1 <= 2^32
+  const uint64_t bits = __double_as_longlong(m);
+  int e = static_cast<int>(bits >> 52) - 1023;
+  uint64_t fb = (bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;  // f in [1, 2)
+  const bool hi = fb > 0x3FF6A09E667F3BCDull;                            // f > sqrt(2): f / 2, e + 1
+  fb -= hi ? 0x0010000000000000ull : 0ull;
+  e += hi ? 1 : 0;
+  const double f = __longlong_as_double(static_cast<long long>(fb));
+  const double sn = (f - 1.0) / (f + 1.0);
+  const double t = sn * sn;
+  double p = 0.08695652173913043;      // 2/23
+  p = fma(p, t, 0.09523809523809523);  // 2/21
+  p = fma(p, t, 0.10526315789473684);  // 2/19
+  p = fma(p, t, 0.11764705882352941);  // 2/17
+  p = fma(p, t, 0.13333333333333333);  // 2/15
+  p = fma(p, t, 0.15384615384615385);  // 2/13
+  p = fma(p, t, 0.18181818181818182);  // 2/11
+  p = fma(p, t, 0.2222222222222222);   // 2/9
+  p = fma(p, t, 0.2857142857142857);   // 2/7
+  p = fma(p, t, 0.4);                  // 2/5
+  p = fma(p, t, 0.6666666666666666);   // 2/3
+  const double lf = fma(sn * t, p, 2.0 * sn);
+  const double k = static_cast<double>(e - 32);
+  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, lf));
+}
+
+// (sin, cos)(2 pi b 2^-32) for a 32-bit b: exact quarter-turn reduction in integers (nearest
+// quarter k = round(b / 2^30), rem = b - k 2^30 in [-2^29, 2^29)), x = 2 pi rem 2^-32 (|x| <= pi/4;
+// rem 2^-32 exact), the series, then the rotation by k quarter turns.
+__device__ __forceinline__ void sincos2pi_u32(uint32_t b, double& s_out, double& c_out) {
+  const uint32_t k = (b + (1u << 29)) >> 30;  // 0..3 (b near 2^32 wraps to quarter 0)
+  const int32_t rem = static_cast<int32_t>(b - (k << 30));
+  const double x = static_cast<double>(rem) * 0x1p-32 * 6.283185307179586;
+  double s, c;
+  sincos_series(x, s, c);
+  const bool odd = (k & 1u) != 0u;
+  const double sb = odd ? c : s, cb = odd ? s : c;
+  s_out = (k & 2u) ? -sb : sb;
+  c_out = ((k + 1u) & 2u) ? -cb : cb;
+}
+
+// e^y: n = rint(y / ln 2), r = y - n ln2 (Cody-Waite: fdlibm's ln2_hi, 21 trailing zero bits, and
+// ln2_lo, each a fused step), e^r by Taylor terms to r^13 / 13! (|r| <= 0.347: truncation < 5e-18),
+// exact ldexp.  No overflow handling: the path recursion's exponents stay within |y| < 700.
+__device__ __forceinline__ double exp_f64(double y) {
+  const double n = rint(y * 1.4426950408889634);
+  double r = fma(-n, 0.6931471803691238, y);
+  r = fma(-n, 1.9082149292705877e-10, r);
+  double p = 1.6059043836821613e-10;  // 1/13!
+  p = fma(p, r, 2.08767569878681e-09);      // 1/12!
+  p = fma(p, r, 2.505210838544172e-08);     // 1/11!
+  p = fma(p, r, 2.755731922398589e-07);     // 1/10!
+  p = fma(p, r, 2.7557319223985893e-06);    // 1/9!
+  p = fma(p, r, 2.48015873015873e-05);      // 1/8!
+  p = fma(p, r, 0.0001984126984126984);     // 1/7!
+  p = fma(p, r, 0.001388888888888889);      // 1/6!
+  p = fma(p, r, 0.008333333333333333);      // 1/5!
+  p = fma(p, r, 0.041666666666666664);      // 1/4!
+  p = fma(p, r, 0.16666666666666666);       // 1/3!
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, static_cast<int>(n));
 }
 
 }  // namespace math

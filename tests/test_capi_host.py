@@ -165,9 +165,10 @@ def test_path_pitch_is_an_odd_multiple_of_4k() -> None:
 
 def test_train_targets_kernel_choice() -> None:
     """Which path/CF kernels smc_train_targets runs: the sliced queue kernel with a workspace;
-    resident_kernel for the f32 training shapes it covers (T = 16, 4096 | P <= 65,536, N | 4096,
-    N <= 1024); else the split pair paths_kernel + cf_kernel (terminal-row sum parked in the scratch
-    row's padding, so it needs a padded pitch such as smc_path_pitch); contract_kernel otherwise."""
+    resident_kernel for the f32 training shapes it covers (any T, 4096 | P <= 65,536, N | 4096,
+    N <= 1024); else a split pair with the terminal-row sum parked in the scratch row's padding (so it
+    needs a padded pitch such as smc_path_pitch): the straight-line paths_kernel + cf_kernel at T = 16,
+    rows_kernel + cf_kernel for other T and for f64; contract_kernel otherwise."""
     L = _lib.lib()
     split = b"paths_kernel+cf_kernel"
     assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 0) == b"resident_kernel"    # C2
@@ -176,9 +177,13 @@ def test_train_targets_kernel_choice() -> None:
     assert L.smc_train_targets_kernel(16, 1024, 262144, 0, L.smc_path_pitch(262144, 0), 0) == split  # C3
     assert L.smc_train_targets_kernel(16, 1024, 262144, 0, 0, 0) == b"contract_kernel"      # no padding
     assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 1) == b"queue_kernel"
-    assert L.smc_train_targets_kernel(17, 256, 65536, 0, 0, 0) == b"contract_kernel"
-    assert L.smc_train_targets_kernel(17, 256, 65536, 0, 66560, 0) == split                 # generic block
-    assert L.smc_train_targets_kernel(16, 256, 65536, 1, 66560, 0) == b"contract_kernel"    # f64
+    rows = b"rows_kernel+cf_kernel"
+    assert L.smc_train_targets_kernel(17, 256, 65536, 0, 0, 0) == b"resident_kernel"        # any T
+    assert L.smc_train_targets_kernel(1, 16, 65536, 0, 66560, 0) == b"resident_kernel"      # lock-step shape
+    assert L.smc_train_targets_kernel(17, 2048, 65536, 0, 66560, 0) == rows                 # N > 1024, T != 16
+    assert L.smc_train_targets_kernel(17, 2048, 65536, 0, 0, 0) == b"contract_kernel"       # no padding
+    assert L.smc_train_targets_kernel(16, 256, 65536, 1, 66048, 0) == rows                  # f64
+    assert L.smc_train_targets_kernel(16, 256, 65536, 1, 0, 0) == b"contract_kernel"        # f64, no padding
     assert L.smc_train_targets_kernel(16, 6, 6144, 0, 6144, 0) == b"contract_kernel"        # pitch == P
     assert L.smc_train_targets_kernel(16, 6, 6144, 0, 7168, 0) == split                     # N not | 4096
 

@@ -75,6 +75,37 @@ def test_oracle_stream_bits_are_uniform(oracle) -> None:
         assert abs(((bits >> b) & 1).mean() - 0.5) < 4e-3, b
 
 
+def test_f64_uniform_transcendentals_are_accurate(oracle) -> None:
+    """The f64 normals' ln / sin / cos of 32-bit uniforms and the f64 recursion's exp (csrc/smc_math.h,
+    restated in the oracle) against numpy's libm at the edges of their domains and on random points:
+    within 2 ulp (log, exp); sin / cos within 2^-52 absolute of an x87 long-double evaluation of the
+    exactly reduced angle (the integer b is reduced to the nearest quarter turn before any rounding)."""
+    two_pi = np.longdouble("6.283185307179586476925286766559005768")
+
+    def sincos_ld(b: int) -> tuple[float, float]:
+        k = (b + 2**29) // 2**30
+        x = two_pi * np.longdouble(b - k * 2**30) / np.longdouble(2**32)
+        s_, c_ = np.sin(x), np.cos(x)
+        for _ in range(k % 4):
+            s_, c_ = c_, -s_
+        return float(s_), float(c_)
+
+    rng = np.random.default_rng(5)
+    a_vals = [0, 1, 2, 3, 0x7FFFFFFF, 0xB504F333, 0xFFFFFFFE, 0xFFFFFFFF] + [int(x) for x in rng.integers(0, 2**32, 2000)]
+    for a in a_vals:
+        want = math.log((a + 1) / 2.0**32)
+        got = oracle.log_u32(a)
+        assert abs(got - want) <= 2 * math.ulp(want) + (0.0 if want else 1e-300), a
+    for b in [0, 1, 2**29 - 1, 2**29, 2**30, 3 * 2**29, 2**31, 2**32 - 2**29, 2**32 - 1] + \
+            [int(x) for x in rng.integers(0, 2**32, 2000)]:
+        s, c = oracle.sincos2pi_u32(b)
+        ws, wc = sincos_ld(b)
+        assert abs(s - ws) <= 2.0**-52 and abs(c - wc) <= 2.0**-52, b
+    for y in [-700.0, -50.0, -1e-300, 0.0, 1e-12, 0.34657, 0.5, 1.0, 50.0, 700.0] + list(rng.uniform(-60, 60, 2000)):
+        want = math.exp(y)
+        assert abs(oracle.exp_f64(float(y)) - want) <= 2 * math.ulp(want), y
+
+
 def test_oracle_normals_are_standard(oracle) -> None:
     z = oracle.normals(7, 3, 16, 65536).astype(np.float64)
     assert abs(z.mean()) < 5e-3
