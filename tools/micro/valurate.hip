@@ -57,7 +57,13 @@ __global__ __launch_bounds__(1024) void probe(uint32_t* sink, uint64_t* cyc) {
   if constexpr (K == 25) asm volatile("v_lshlrev_b32 %0, 9, %0" : "+v"(v##i));                        \
   if constexpr (K == 26) asm volatile("v_rcp_f32 %0, %0" : "+v"(v##i));                               \
   if constexpr (K == 27) asm volatile("v_exp_f16 %0, %0" : "+v"(v##i));                               \
-  if constexpr (K == 28) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(v##i) : "v"(v1), "v"(v2));
+  if constexpr (K == 28) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(v##i) : "v"(v1), "v"(v2)); \
+  if constexpr (K == 29) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(d##i) : "v"(e2), "v"(e3));   \
+  if constexpr (K == 30) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(d##i) : "v"(e2));                \
+  if constexpr (K == 31) asm volatile("v_ldexp_f64 %0, %0, %1" : "+v"(d##i) : "v"(v1));              \
+  if constexpr (K == 32) asm volatile("v_rndne_f64 %0, %0" : "+v"(d##i));                            \
+  if constexpr (K == 33) asm volatile("v_rcp_f64 %0, %0" : "+v"(d##i));                              \
+  if constexpr (K == 34) asm volatile("v_add_f64 %0, %0, %1" : "+v"(d##i) : "v"(e2));
     R8(ONE) R8(ONE) R8(ONE) R8(ONE)
 #undef ONE
   }
@@ -125,6 +131,12 @@ int main() {
   run<19>("v_lshlrev_b64", sink, cyc, host, cus);
   run<21>("v_lshl_add_u64", sink, cyc, host, cus);
   run<11>("v_cvt_f32_u32", sink, cyc, host, cus);
+  run<29>("v_fma_f64", sink, cyc, host, cus);
+  run<30>("v_mul_f64", sink, cyc, host, cus);
+  run<34>("v_add_f64", sink, cyc, host, cus);
+  run<31>("v_ldexp_f64", sink, cyc, host, cus);
+  run<32>("v_rndne_f64", sink, cyc, host, cus);
+  run<33>("v_rcp_f64", sink, cyc, host, cus);
   run<22>("v_cvt_f32_ubyte1", sink, cyc, host, cus);
   return 0;
 }
