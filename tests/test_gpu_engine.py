@@ -232,6 +232,43 @@ def test_sliced_f64_and_chunked_launches(oracle, golden) -> None:
     np.testing.assert_array_equal(a, b)
 
 
+ROWS_CASES = [  # (B, T, N, M, scheme, normalize, dtype, store, hw): shapes rows_kernel + cf_kernel take
+    (7, 17, 2048, 32, 0, 1, "float32", _lib.STORE_ALL, 0),    # f32, T != 16, N > 1024
+    (6, 17, 2048, 32, 0, 1, "float32", _lib.STORE_ALL, 1),    # the same in hw math
+    (5, 16, 64, 64, 0, 1, "float64", _lib.STORE_ALL, 0),      # f64 (any f64 shape with whole chunks)
+    (5, 5, 128, 32, 1, 0, "float64", _lib.STORE_TERMINAL, 0),  # f64, odd T, simple Euler, RAW, terminal rows
+    (3, 33, 64, 64, 0, 1, "float64", _lib.STORE_ALL, 0),      # f64, T > 16
+]
+
+
+@pytest.mark.parametrize("B,T,N,M,scheme,normalize,dtype,store,hw", ROWS_CASES)
+def test_rows_kernel_matches_oracle_and_contract_kernel(oracle, golden, B, T, N, M, scheme, normalize, dtype, store,
+                                                        hw) -> None:
+    """rows_kernel + cf_kernel (persistent, every row in registers, terminal sum through the row
+    padding): f32 portable bit-exact with the kernel-mode oracle (512-lane order) and hw within 1e-5 of
+    the reference mode; f64 within 1e-10 of the reference mode (its exp differs from libm by <= 2 ulp)
+    and bit-identical to contract_kernel at an unpadded pitch (same paths, same reduction order)."""
+    c = _contracts(oracle, golden, B, seed=3)
+    P = N * M
+    dcode = 0 if dtype == "float32" else 1
+    pitch = int(_L().smc_path_pitch(P, dcode))
+    assert _L().smc_train_targets_kernel(T, N, P, dcode, pitch, 0) == b"rows_kernel+cf_kernel"
+    flags = _lib.MATH_HW if hw else 0
+    got, _, paths = _run_targets(c, T, N, M, scheme, normalize, dtype, store, ordinal0=9, with_rowsum=False,
+                                 flags=flags, pitch=pitch)
+    want = oracle.training_targets(c, T, N, M, seed=7, ordinal0=9, scheme=scheme, normalize=bool(normalize),
+                                   dtype=dtype)
+    assert _norm_rel(got, want) < (1e-5 if dtype == "float32" else 1e-10)
+    if dtype == "float32" and not hw:
+        kt, _ = oracle.kernel_targets(c, T, N, M, seed=7, ordinal0=9, scheme=scheme, normalize=bool(normalize))
+        np.testing.assert_array_equal(got, kt)
+    if dtype == "float64":
+        assert _L().smc_train_targets_kernel(T, N, P, dcode, 0, 0) == b"contract_kernel"
+        ref, _, ref_paths = _run_targets(c, T, N, M, scheme, normalize, dtype, store, ordinal0=9, with_rowsum=False)
+        np.testing.assert_array_equal(got, ref)
+        np.testing.assert_array_equal(paths.cpu().numpy(), ref_paths.cpu().numpy())
+
+
 MANY_CONTRACT_CASES = [
     # (B, T, N, M, scheme, normalize): more contracts than the resident grid (512 workgroups on
     # MI355X), so the one-workgroup-per-contract launch runs several rounds
