@@ -818,6 +818,20 @@ __device__ uint64_t g_trace[1024 * kTraceStride];
 #else
 #define SMC_TRACE(slot) do {} while (0)
 #endif
+// SMC_EXPERIMENT_TRACE_CF (with SMC_EXPERIMENT_TRACE): the CF phase's sub-steps of rounds 0..5 at
+// slots 2 + 6 r + k instead (k = 0 simulation done, 1 column sums in LDS, 2 M-mean done, 3 FFT done)
+#if defined(SMC_EXPERIMENT_TRACE_CF)
+#define SMC_TRACE_R(k, slot2) \
+  do {                        \
+    if (round < 6) SMC_TRACE(2 + 6 * round + (k)); \
+  } while (0)
+#else
+#define SMC_TRACE_R(k, slot2) \
+  do {                        \
+    if ((k) == 0 || (k) == 3) \
+      if (round < 18) SMC_TRACE(slot2); \
+  } while (0)
+#endif
 
 template <bool LOG_EULER, bool HW, bool STORE_ALL, bool T16>
 __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
@@ -960,7 +974,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     const double w = wave_sum(acc[0]);
     if (lane == 0) wsum[wave] = w;
     lds_barrier();
-    if (round < 18) SMC_TRACE(2 + 2 * round);  // simulation of this contract done
+    SMC_TRACE_R(0, 2 + 2 * round);  // simulation of this contract done
 #if defined(SMC_RESIDENT_NO_CF)  // tools/micro decomposition builds only: no payoff / M-mean / FFT
     lds_barrier();
     continue;
@@ -1019,6 +1033,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
 #pragma unroll
     for (int j = 0; j < kPathsPerLane; ++j) part[g * N + 4 * q + j] = colsum[j];
     lds_barrier();
+    SMC_TRACE_R(1, 0);
     if (W == 1) {
       for (int n = tid; n < N; n += kResThreads) {
         double t = 0.0;
@@ -1049,9 +1064,10 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       for (int n = tid; n < N; n += kResThreads) avg[n] = ordered_sum_wt(xcol, n, W, N) / static_cast<double>(M);
     }
     lds_barrier();
+    SMC_TRACE_R(2, 0);
     fft_row<float, kResThreads, true>(avg, cs, sn, N, part, part + N, static_cast<float2*>(a.targets) + b * N);
     lds_barrier();  // part (= term_lds) / avg / wsum / row are reused by the next contract
-    if (round < 18) SMC_TRACE(3 + 2 * round);  // CF of this contract done
+    SMC_TRACE_R(3, 3 + 2 * round);  // CF of this contract done
   }
   SMC_TRACE(39);
   if (a.done && tid == 0) {
@@ -1509,7 +1525,12 @@ using namespace smc;
 
 extern "C" {
 #if defined(SMC_EXPERIMENT_TRACE)
+// n < 0: zero the trace (before the launch to be traced), else copy its first n words to host
 __attribute__((visibility("default"))) int32_t smc_debug_trace(uint64_t* host, int64_t n) {
+  if (n < 0) {
+    static uint64_t zeros[1024 * kTraceStride];
+    return hipMemcpyToSymbol(HIP_SYMBOL(smc::g_trace), zeros, sizeof(zeros)) == hipSuccess ? 0 : 1;
+  }
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(smc::g_trace), static_cast<size_t>(n) * sizeof(uint64_t)) == hipSuccess
              ? 0 : 1;
 }

@@ -30,6 +30,7 @@ def main() -> None:
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--budget-gb", type=float, default=40.0, help="path scratch budget (engine default)")
+    ap.add_argument("--trace", default="", help="save per-workgroup timestamps (SMC_EXPERIMENT_TRACE builds)")
     a = ap.parse_args()
     B, T, N, M = SHAPES[a.config]
     B = a.B or B
@@ -66,6 +67,12 @@ def main() -> None:
 
     step()
     torch.cuda.synchronize()
+    if a.trace:  # the trace keeps the last launch only: zero it before the timed launches
+        import ctypes
+        fn = getattr(L, "smc_debug_trace")
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        assert fn(None, -1) == 0
+        a.iters = 1
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.iters):
@@ -73,6 +80,13 @@ def main() -> None:
     e1.record()
     torch.cuda.synchronize()
     assert _lib.sync_status(sync) == 0
+    if a.trace:  # gbm.hip g_trace: [workgroup][40] s_memrealtime stamps of the last launch
+        import ctypes
+        buf = np.zeros((1024, 40), dtype=np.uint64)
+        fn = getattr(L, "smc_debug_trace")
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        assert fn(buf.ctypes.data, buf.size) == 0
+        np.save(a.trace, buf)
     name = L.smc_train_step_kernel(T, N, M, dcode, pitch).decode()
     ms = e0.elapsed_time(e1) / a.iters
     print(f"{a.config} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
