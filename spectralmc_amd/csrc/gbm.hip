@@ -231,6 +231,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   // wave-uniform row base (SGPR pair) + 32-bit per-lane byte offset
   const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(Real)) * threadIdx.x;
   Real* chunk_base = contract_base + chunk;
+  const __amdgpu_buffer_rsrc_t contract_rsrc = row_rsrc(contract_base);
 #pragma unroll
   for (int i = 0; i < kRowBlock; ++i) {
     if (FULLBLOCK || i < nrows) {
@@ -251,7 +252,20 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
         char* row = reinterpret_cast<char*>(chunk_base + (store_all ? static_cast<int64_t>(t) * pitch : 0));
         // the terminal row is read back by the CF phase (maybe another workgroup's): write-through
         const bool handoff = last && (STRAIGHT || a.targets != nullptr);
-        if constexpr (!MASKED) {
+#if defined(SMC_EXPERIMENT_FLAT_STORES)  // tools/micro A/B builds only: 64-bit VALU row addresses
+        if constexpr (false) {
+#else
+        if constexpr (STRAIGHT && !MASKED && sizeof(Real) == 4) {
+#endif
+          // one buffer descriptor on the contract base; the row offset goes in soffset (SALU adds), so
+          // a row store costs no 64-bit VALU address add
+          typedef float v4f __attribute__((ext_vector_type(4)));
+          const v4f v4 = {x[0], x[1], x[2], x[3]};
+          const uint32_t soff = static_cast<uint32_t>((chunk + (store_all ? static_cast<int64_t>(t) * pitch : 0)) *
+                                                      static_cast<int64_t>(sizeof(Real)));
+          if (handoff) __builtin_amdgcn_raw_buffer_store_b128(v4, contract_rsrc, lane_off, soff, 16 /* sc1 */);
+          else __builtin_amdgcn_raw_buffer_store_b128(v4, contract_rsrc, lane_off, soff, 0);
+        } else if constexpr (!MASKED) {
           V4 v4;
           v4.x = x[0];
           v4.y = x[1];
@@ -790,6 +804,20 @@ __global__ __launch_bounds__(kThreads) void rows_kernel(EngineArgs a) {
 // the group's counter; sc1 loads after the poll matched or the add returned
 // (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms, first table row).  Counters
 // are monotonic within a launch (W per contract round) and reset by the last workgroup.
+// Sum over g < G of part[g * N + n] in g order from 0.0, the LDS reads issued 8 at a time
+__device__ __forceinline__ double group_sum(const double* part, int n, int G, int N) {
+  double t = 0.0;
+  for (int g0 = 0; g0 < G; g0 += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(g0 + u < G ? g0 + u : G - 1) * N + n];  // clamped: straight-line
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (g0 + u < G) t += v[u];
+  }
+  return t;
+}
+
 constexpr int kResThreads = 1024;
 constexpr int kResWaves = kResThreads / 64;
 constexpr int kResChunk = kResThreads * kPathsPerLane;  // 4096 paths
@@ -870,6 +898,9 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
                                           // [8] the next dynamically handed-out contract;
   double* pre = row + 9;                  // [kResPreDraw][6] Sobol rows of the first static contracts
   SMC_TRACE(0);
+#if defined(SMC_EXPERIMENT_TRACE_CF)  // core-clock counter at start / end: the workgroup's mean clock
+  if (tid == 0 && blockIdx.x < 1024) g_trace[blockIdx.x * kTraceStride + 36] = __builtin_amdgcn_s_memtime();
+#endif
 #if defined(SMC_EXPERIMENT_TRACE)
   if (tid == 0 && blockIdx.x < 1024) {
     unsigned xcc;
@@ -979,8 +1010,15 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     lds_barrier();
     continue;
 #endif
+    // LDS reads batched ahead of the in-order sums (the CF phase is a chain of LDS round trips)
     double tot = 0.0;
-    for (int k = 0; k < kResWaves; ++k) tot += wsum[k];
+    {
+      double wv[kResWaves];
+#pragma unroll
+      for (int k = 0; k < kResWaves; ++k) wv[k] = wsum[k];
+#pragma unroll
+      for (int k = 0; k < kResWaves; ++k) tot += wv[k];
+    }
     // this round's [W + 1] slots: the W slice sums, then the group's next contract (dynamic tail)
     const int64_t xslot = (static_cast<int64_t>(grp) * 2 + (round & 1)) * (W + 1);
     if (W > 1) {
@@ -1014,12 +1052,16 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     }
     const Payoff<float> pay(a, c, tot);
     double colsum[kPathsPerLane] = {0.0, 0.0, 0.0, 0.0};
+    {
+      v4f v[kResLdsChunks];  // every slot read (unused ones too), so the 8 reads are in flight together
 #pragma unroll
-    for (int ch = 0; ch < kResLdsChunks; ++ch) {
-      if (ch < nch) {
-        const v4f v = term_lds[ch * kResThreads + tid];
+      for (int ch = 0; ch < kResLdsChunks; ++ch) v[ch] = term_lds[ch * kResThreads + tid];
 #pragma unroll
-        for (int j = 0; j < kPathsPerLane; ++j) colsum[j] += static_cast<double>(pay(v[j]));
+      for (int ch = 0; ch < kResLdsChunks; ++ch) {
+        if (ch < nch) {
+#pragma unroll
+          for (int j = 0; j < kPathsPerLane; ++j) colsum[j] += static_cast<double>(pay(v[ch][j]));
+        }
       }
     }
 #pragma unroll
@@ -1036,16 +1078,14 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     SMC_TRACE_R(1, 0);
     if (W == 1) {
       for (int n = tid; n < N; n += kResThreads) {
-        double t = 0.0;
-        for (int gg = 0; gg < G; ++gg) t += part[gg * N + n];
+        const double t = group_sum(part, n, G, N);
         avg[n] = t / static_cast<double>(M);
       }
     } else {
       // column-sum exchange: the slice's G group sums per column, published by wave 0; the last
       // slice to arrive adds the W column sums in slice order and runs the FFT
       for (int n = tid; n < N; n += kResThreads) {
-        double t = 0.0;
-        for (int gg = 0; gg < G; ++gg) t += part[gg * N + n];
+        const double t = group_sum(part, n, G, N);
         avg[n] = t;
       }
       lds_barrier();
@@ -1070,6 +1110,9 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     SMC_TRACE_R(3, 3 + 2 * round);  // CF of this contract done
   }
   SMC_TRACE(39);
+#if defined(SMC_EXPERIMENT_TRACE_CF)
+  if (tid == 0 && blockIdx.x < 1024) g_trace[blockIdx.x * kTraceStride + 37] = __builtin_amdgcn_s_memtime();
+#endif
   if (a.done && tid == 0) {
     // every workgroup read the cursor (and made its last exchange) before it arrives here: the last
     // one advances the cursor and resets the exchange counters

@@ -30,6 +30,7 @@ def main() -> None:
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--budget-gb", type=float, default=40.0, help="path scratch budget (engine default)")
+    ap.add_argument("--pitch", type=int, default=0, help="row pitch in elements (0: smc_path_pitch)")
     ap.add_argument("--trace", default="", help="save per-workgroup timestamps (SMC_EXPERIMENT_TRACE builds)")
     a = ap.parse_args()
     B, T, N, M = SHAPES[a.config]
@@ -40,7 +41,7 @@ def main() -> None:
     f64 = a.dtype == "f64"
     dcode = _lib.DTYPE_F64 if f64 else _lib.DTYPE_F32
     store = _lib.STORE_ALL if a.store == "all" else _lib.STORE_TERMINAL
-    pitch = int(L.smc_path_pitch(P, dcode))
+    pitch = a.pitch or int(L.smc_path_pitch(P, dcode))
     esz = 8 if f64 else 4
     per = (T if store == _lib.STORE_ALL else 1) * pitch * esz
     chunk = max(1, min(B, int(a.budget_gb * (1 << 30)) // per))
@@ -89,7 +90,7 @@ def main() -> None:
         np.save(a.trace, buf)
     name = L.smc_train_step_kernel(T, N, M, dcode, pitch).decode()
     ms = e0.elapsed_time(e1) / a.iters
-    print(f"{a.config} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
+    print(f"{a.config} pitch={pitch} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
           f"({launches} launch(es) of {chunk}), checksum {float(t.abs().double().mean()):.6g}")
 
 

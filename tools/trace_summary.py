@@ -34,6 +34,10 @@ def main() -> None:
         m = xcc == x
         print(f"  XCC {x}: {m.sum()} WGs, end {end[m].min():.1f}..{end[m].max():.1f} us")
     if a.cf:
+        ghz = (t[:, 37] - t[:, 36]) / ((t[:, 39] - t[:, 0]) * 10.0)  # s_memtime cycles / ns
+        for x in sorted(set(xcc.tolist())):
+            m = xcc == x
+            print(f"  XCC {x}: mean core clock {ghz[m].mean():.3f} GHz (min {ghz[m].min():.3f})")
         prev = t[:, 0]
         for r in range(6):
             k = [t[:, 2 + 6 * r + i] for i in range(4)]
