@@ -76,6 +76,10 @@ def parse() -> argparse.Namespace:
                     help="network kernels (default: bf16 for c3, auto otherwise)")
     ap.add_argument("--overlap", default="on", choices=["on", "off"],
                     help="MC part of step s+1 on its own stream beside step s's network part (pricer.overlap_mc)")
+    ap.add_argument("--priority", default="network", choices=["network", "mc", "none"],
+                    help="stream with the high queue priority (pricer.high_priority_stream)")
+    ap.add_argument("--lanes", type=int, default=1, help="MC lanes (pricer.mc_lanes): consecutive path launches "
+                    "on alternating streams, each starting in the previous one's tail")
     ap.add_argument("--graphs", default="on", choices=["on", "off"], help="replay the step as hipGraphs")
     ap.add_argument("--kernel-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -241,6 +245,8 @@ def main() -> None:
     pricer.warmup_steps = max(1, min(2, args.warmup)) if args.graphs == "on" else 0
     pricer.network_compute = args.network or NETWORK_COMPUTE.get(args.config, "auto")
     pricer.overlap_mc = args.overlap == "on"
+    pricer.high_priority_stream = args.priority
+    pricer.mc_lanes = args.lanes
     if n_assets:
         from spectralmc_amd.basket import BasketConfig, use_basket_engine
 
@@ -304,6 +310,15 @@ def main() -> None:
     # (Sobol draw + path/CF kernel + cursor update; the path/CF kernel is >99 % of it)
     live = [a.elapsed_time(b_) for a, b_ in (session.mc_events or [])]
     live_ms = (sum(live) / len(live) / launches_per_call) if live else kernel_ms
+    lanes = getattr(eng, "lanes", 1)
+    steady_ms = None
+    if lanes > 1 and live:
+        # MC lanes: step s + 1's launch starts in step s's tail, so an event pair around one launch also
+        # spans its wait for CUs; the launch duration is the isolated one, and the MC part's steady
+        # rate is the span of all live launches over their number
+        ev = session.mc_events
+        steady_ms = ev[0][0].elapsed_time(ev[-1][1]) / len(ev) / launches_per_call
+        live_ms = kernel_ms
     achieved = bytes_launch / (live_ms * 1e-3) / 1e9
 
     # ---- network part alone (fused HIP kernels), HIP events on its own stream ------------
@@ -338,9 +353,10 @@ def main() -> None:
                    "frac": flops / (net_ms * 1e-3) / 1e12 / peak,
                    "peak_note": "dense MFMA peak of the operand type (bf16 2.52 PF; f32 MFMA = f32 VALU "
                                 "157.3 TF), MI355X_MICROARCH.md",
-                   "note": "small complex GEMMs (K = 12..512) plus the targets read; enqueued on its own "
-                           "stream, it runs in the gaps between consecutive path kernels (the path kernel "
-                           "holds every CU's registers while it runs)"}
+                   "note": "small complex GEMMs (K = 12..512) plus the targets read, timed alone; in the "
+                           "step it is enqueued on its own high-priority stream and its workgroups take the "
+                           "CUs the path kernels free in their tails (a path kernel holds every CU while its "
+                           "contract queue lasts)"}
 
     # ---- measured HBM ceilings on this device (STREAM-style, 8 GiB buffers) --------------
     stream_gbs = {}
@@ -412,6 +428,11 @@ def main() -> None:
                      # bytes the kernel actually moved (PMC) over its live time, against the same peak
                      "frac_moved": (traffic / (live_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                      "kernel_ms": live_ms, "kernel_ms_isolated": kernel_ms, "live_launches": len(live),
+                     "mc_lanes": lanes,
+                     # lanes > 1: consecutive launches overlap; the MC part's steady
+                     # time per launch and the fraction of peak it corresponds to
+                     "kernel_ms_steady": steady_ms,
+                     "frac_steady": (bytes_launch / (steady_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if steady_ms else None,
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "contracts_per_launch": contracts_per_launch,
                      "measured_stream_gbs": stream_gbs,

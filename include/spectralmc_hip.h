@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 10
+#define SMC_ABI_VERSION 11
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -60,6 +60,10 @@ extern "C" {
 #define SMC_MATH_HW          0x100  /* flag, OR into `scheme` (engine calls) or `dtype` (smc_normals):
                                       f32 hardware transcendentals (v_exp/v_log/v_sin/v_cos/v_sqrt)
                                       instead of the portable, CPU-reproducible kernels */
+#define SMC_TRAIN_DYNAMIC    0x200  /* flag, OR into smc_train_step's `scheme`: the whole-contract resident
+                                      launch hands out every contract from its contract queue (default:
+                                      the first three quarters of the rounds statically), for launches that
+                                      may start while the previous step's launch still holds CUs */
 #define SMC_STORE_TERMINAL       1  /* keep only the terminal row [B][P] (scratch)        */
 #define SMC_STORE_ALL            2  /* materialise the full path matrix [B][T][P]         */
 

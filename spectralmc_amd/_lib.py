@@ -35,9 +35,10 @@ DTYPE_F32 = 0
 DTYPE_F64 = 1
 STORE_TERMINAL = 1
 MATH_HW = 0x100
+TRAIN_DYNAMIC = 0x200
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 

@@ -102,6 +102,9 @@ struct EngineArgs {
   // handed out from this counter (zero between launches) instead of statically, so workgroups on
   // XCDs with more write bandwidth take more contracts (NULL: all static)
   uint32_t* res_queue;
+  // share of the contract rounds assigned statically, in quarters (the rest from res_queue); 0 with
+  // SMC_TRAIN_DYNAMIC: every contract from the queue
+  int32_t res_static_q = 3;
   // sliced resident_kernel: the sync area's sticky status word (SMC_SYNC_STATUS_OFFSET), the poll
   // budget of an exchange and the smc_test_exchange_fault hook (withhold: slice W-1 of group 0 skips
   // its first terminal-sum arrival)
@@ -918,10 +921,8 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   // (sliced, W > 1: slice 0 takes the group's next contract during the current contract's
   // terminal-sum exchange, and the partners read it with the sums; only once every group has a
   // static contract, n_static > 0)
-#ifndef SMC_RES_STATIC_QUARTERS
-#define SMC_RES_STATIC_QUARTERS 3  // statically assigned share of the contract rounds, in quarters
-#endif
-  const int64_t n_static0 = (a.B / groups) * SMC_RES_STATIC_QUARTERS / 4 * groups;
+  // (a.res_static_q: the statically assigned share of the contract rounds, in quarters)
+  const int64_t n_static0 = (a.B / groups) * a.res_static_q / 4 * groups;
   const bool dyn = a.res_queue != nullptr && (W == 1 || n_static0 > 0);
   const int64_t n_static = dyn ? n_static0 : a.B;
   auto grab = [&]() -> int64_t {
@@ -1674,6 +1675,8 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   if (!sobol_tables_dev || !lower_dev || !upper_dev || !cursor_dev || !contracts_dev || !sync_dev)
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_step: NULL buffer");
   if (dim != 6) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_step: dim must be 6 (BlackScholes.Inputs)");
+  const bool dynamic = (scheme & SMC_TRAIN_DYNAMIC) != 0;  // every contract of the resident launch from the queue
+  scheme &= ~SMC_TRAIN_DYNAMIC;
   if (index_offset < 0 || advance < 0) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_train_step: negative offset");
   if (network_size <= 0 || batches_per_mc_run <= 0)
     return fail(SMC_ERR_INVALID_SHAPE, "smc_train_step: network_size and batches_per_mc_run must be > 0");
@@ -1705,6 +1708,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   a.done = reinterpret_cast<uint32_t*>(sync);
   a.status = reinterpret_cast<uint32_t*>(sync + SMC_SYNC_STATUS_OFFSET);
   a.res_queue = reinterpret_cast<uint32_t*>(sync + 64);
+  a.res_static_q = dynamic ? 0 : 3;
   a.spin_limit = exchange_spin_limit();
   a.withhold = exchange_fault().withhold;
   if (a.res_slices > 1) {

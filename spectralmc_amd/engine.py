@@ -60,7 +60,7 @@ class TrainingEngine:
     def __init__(self, cfg: BlackScholesConfig, sampler: SobolSampler, batch_size: int, *, model_dtype: torch.dtype,
                  device: torch.device, rank: int = 0, world_size: int = 1, store_paths: bool = True,
                  path_buffer_bytes: int | None = None, math: str = "portable",
-                 sliced: bool = False) -> None:
+                 sliced: bool = False, lanes: int = 1) -> None:
         _lib.require_device()
         sp = cfg.sim_params
         self.cfg = cfg
@@ -91,8 +91,6 @@ class TrainingEngine:
         self.tables = torch.from_numpy(sampler.engine.tables().view("int32")).to(device)
         self.lower = torch.from_numpy(lo).to(device)
         self.upper = torch.from_numpy(hi).to(device)
-        # [global Sobol index of the step's first contract, global normal ordinal of it]
-        self.cursor = torch.zeros(2, dtype=torch.int64, device=device)
 
         B = batch_size
         contracts = torch.empty((B, self.dim), dtype=torch.float64, device=device)
@@ -112,9 +110,6 @@ class TrainingEngine:
                 max_chunk -= max_chunk % slots
         launches = -(-B // max_chunk)
         self.chunk = -(-B // launches)  # equal launches: no small trailing launch
-        shape = (self.chunk, self.T, self.pitch) if store_paths else (self.chunk, self.pitch)
-        self._paths_buf = torch.empty(shape, dtype=sim_torch, device=device)
-        self.paths = self._paths_buf[..., :self.P]  # (chunk, T, P) / (chunk, P) strided view
         # sliced=True: each contract runs as several workgroups (slice row sums + arrival counters
         # in a workspace); the default one-workgroup-per-contract launch takes the
         # contract_kernel
@@ -125,14 +120,6 @@ class TrainingEngine:
         # smc_train_step's sync area (arrival counters; the sliced resident kernel's exchanged sums),
         # zero-filled once; every step leaves its counters zeroed
         self._uses_train_step = self._f32_in and self.dim == 6 and self._workspace is None
-        self._sync: torch.Tensor | None = None
-        self._sync_bytes = 0
-        if self._uses_train_step:
-            sync = int(_lib.lib().smc_train_step_sync_bytes(self.T, self.N, self.M, self._dtype_code, self.pitch))
-            if sync < 0:
-                raise RuntimeError("smc_train_step_sync_bytes: device query failed")
-            self._sync = torch.zeros(max(sync, 8), dtype=torch.uint8, device=device)
-            self._sync_bytes = sync
         # the path/CF kernel the step runs for this shape (bench labels, rocprof cross-check)
         if self._uses_train_step:
             self.kernel_name = _lib.lib().smc_train_step_kernel(self.T, self.N, self.M, self._dtype_code,
@@ -140,20 +127,52 @@ class TrainingEngine:
         else:
             self.kernel_name = _lib.lib().smc_train_targets_kernel(
                 self.T, self.N, self.P, self._dtype_code, self.pitch, 1 if ws else 0).decode()
+        # MC lanes: consecutive steps alternate over `lanes` sets of {cursor, sync area, path scratch}, so
+        # a caller may run step s + 1's launch on another stream while step s's is still in its tail
+        # (the next launch's workgroups take the CUs the last contracts free).
+        # Lane k's cursor is the position of the next step that uses lane k; each launch advances it by
+        # lanes * global_batch.  Only for one whole-contract resident launch per step (no exchange
+        # between workgroups, which needs every workgroup of a group co-resident) within the budget.
+        self.lanes = 1
+        if (lanes > 1 and self._uses_train_step and self.kernel_name == "resident_kernel" and self.chunk >= B
+                and lanes * per_contract * self.chunk <= budget):
+            self.lanes = lanes
+        self._next_lane = 0
+        # per lane: [global Sobol index of the lane's next step's first contract, its global normal ordinal]
+        self.cursors = torch.zeros((self.lanes, 2), dtype=torch.int64, device=device)
+        self.cursor = self.cursors[0]
+        shape = (self.chunk, self.T, self.pitch) if store_paths else (self.chunk, self.pitch)
+        self._paths_bufs = [torch.empty(shape, dtype=sim_torch, device=device) for _ in range(self.lanes)]
+        self._paths_buf = self._paths_bufs[0]
+        self.paths = self._paths_buf[..., :self.P]  # (chunk, T, P) / (chunk, P) strided view (lane 0)
+        self._syncs: list[torch.Tensor | None] = [None] * self.lanes
+        self._sync_bytes = 0
+        if self._uses_train_step:
+            sync = int(_lib.lib().smc_train_step_sync_bytes(self.T, self.N, self.M, self._dtype_code, self.pitch))
+            if sync < 0:
+                raise RuntimeError("smc_train_step_sync_bytes: device query failed")
+            self._syncs = [torch.zeros(max(sync, 8), dtype=torch.uint8, device=device) for _ in range(self.lanes)]
+            self._sync_bytes = sync
+        self._sync = self._syncs[0]
 
     def check_status(self, stream: torch.cuda.Stream | None = None) -> None:
         """Raise SmcError(SMC_ERR_EXCHANGE_TIMEOUT) if a launch since the last check gave up waiting
         for a partner workgroup (its targets hold NaN); clears the sticky status word.  Waits for
         ``stream`` (default: the current stream)."""
-        check_sync_status(self._sync, stream)
+        for sync in self._syncs:
+            check_sync_status(sync, stream)
 
     @property
     def global_batch(self) -> int:
         return self.B * self.world_size
 
     def set_position(self, sobol_index: int, ordinal: int) -> None:
-        """Host -> device cursor (outside any captured region)."""
-        self.cursor.copy_(torch.tensor([sobol_index, ordinal], dtype=torch.int64), non_blocking=False)
+        """Host -> device cursors (outside any captured region): the next step runs on lane 0 at
+        (sobol_index, ordinal), lane k's next step k global batches later."""
+        gb = self.global_batch
+        self.cursors.copy_(torch.tensor([[sobol_index + k * gb, ordinal + k * gb] for k in range(self.lanes)],
+                                        dtype=torch.int64), non_blocking=False)
+        self._next_lane = 0
 
     def make_slot(self) -> StepBuffers:
         """Another set of step outputs (contracts, CVNN input, targets) the step can write into
@@ -163,20 +182,26 @@ class TrainingEngine:
         return StepBuffers(contracts=torch.empty_like(b.contracts), real_in=torch.empty_like(b.real_in),
                            imag_in=b.imag_in, targets=torch.empty_like(b.targets))
 
-    def enqueue_step(self, out: StepBuffers | None = None) -> StepBuffers:
+    def enqueue_step(self, out: StepBuffers | None = None, lane: int | None = None) -> StepBuffers:
         """Launch contracts + targets of the next step on the current stream into ``out`` (default:
-        the engine's own buffers), advance the cursor."""
+        the engine's own buffers), advance the cursor.  ``lane``: the lane of this step (default: the
+        next in turn); steps must use the lanes in turn, 0, 1, ..., so a lane's cursor stays the
+        position of its next step."""
         stream = _lib.stream_handle()
         b = out if out is not None else self.buffers
         offset = self.rank * self.B
+        k = self._next_lane if lane is None else lane % self.lanes
+        self._next_lane = (k + 1) % self.lanes
         if self._uses_train_step:
             # draw + targets + cursor advance: one launch per chunk where the resident kernel takes the shape
             _lib.check(_lib.lib().smc_train_step(
-                _lib.ptr(self.tables), self.dim, _lib.ptr(self.lower), _lib.ptr(self.upper), _lib.ptr(self.cursor),
-                offset, self.global_batch, _lib.ptr(b.contracts), _lib.ptr(b.real_in), self.B, self.T, self.N,
-                self.M, self.seed, self._scheme, self._norm, self._dtype_code, self.store_mode,
-                _lib.ptr(self._paths_buf), self.pitch, self.chunk, _lib.ptr(b.targets), _lib.ptr(self._sync),
-                self._sync_bytes, stream))
+                _lib.ptr(self.tables), self.dim, _lib.ptr(self.lower), _lib.ptr(self.upper),
+                _lib.ptr(self.cursors[k]), offset, self.lanes * self.global_batch, _lib.ptr(b.contracts),
+                _lib.ptr(b.real_in), self.B, self.T, self.N, self.M, self.seed,
+                # lanes: a launch may start while the previous one holds CUs, so no static contract share
+                self._scheme | (_lib.TRAIN_DYNAMIC if self.lanes > 1 else 0), self._norm,
+                self._dtype_code, self.store_mode, _lib.ptr(self._paths_bufs[k]), self.pitch, self.chunk,
+                _lib.ptr(b.targets), _lib.ptr(self._syncs[k]), self._sync_bytes, stream))
             return b
         draw_device(self.tables, self.dim, self.cursor[0:1], offset, self.B, self.lower, self.upper, b.contracts,
                     b.real_in if self._f32_in else None)

@@ -443,3 +443,37 @@ def test_batchnorm_residual_model_trains_on_torch_path(oracle) -> None:
     ref = oracle.torch_step(cpu_model, x, torch.zeros_like(x), torch.from_numpy(targets),
                             torch.optim.Adam(cpu_model.parameters(), lr=1e-2))
     assert res.final_loss == pytest.approx(ref.loss, rel=1e-4)
+
+
+def test_mc_lanes_match_one_stream() -> None:
+    """MC lanes (consecutive path launches on alternating streams, each with its own cursor, sync area
+    and scratch; engine.py) give bit-identical training to the sequential one-stream program, eager
+    and graph-replayed, on a shape the resident kernel takes (P = 4096, N | 4096)."""
+    sp = make_simulation_params(timesteps=16, network_size=256, batches_per_mc_run=16, threads_per_block=256,
+                                mc_seed=7, buffer_size=512, dtype=Precision.float32)
+
+    def pricer(overlap: bool, lanes: int):
+        model = make_test_cvnn(n_inputs=6, n_outputs=256, seed=5, dtype=torch.float32)
+        cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                                   domain_bounds=make_domain_bounds())
+        p = expect_success(GbmCVNNPricer.create(cfg))
+        p.overlap_mc, p.mc_lanes, p.math_mode = overlap, lanes, "hw"
+        return p, model
+
+    cfg = make_training_config(num_batches=9, batch_size=96)
+    seq, m_s = pricer(False, 1)
+    r_s = expect_success(seq.train(cfg))
+    lan, m_l = pricer(True, 2)
+    sess = expect_success(lan.open_session(cfg))
+    assert sess.engine.lanes == 2 and len(sess.mc_streams) == 2
+    for _ in range(9):
+        expect_success(sess.step())
+    st = sess.close()
+    assert st.global_step == 9 and st.sobol_skip == 9 * 96
+    assert max_param_diff(m_s, m_l) == 0.0
+    assert st.loss == r_s.final_loss and st.grad_norm == r_s.final_grad_norm
+    for sync in sess.engine._syncs:  # every launch leaves its lane's counters zeroed
+        assert int(sync.count_nonzero()) == 0
+    # lanes interleave the Sobol stream: lane k's cursor is k global batches past lane 0's
+    cur = sess.engine.cursors.cpu().tolist()
+    assert cur[1][0] - cur[0][0] in (96, -96)

@@ -16,6 +16,7 @@ from tests.helpers import (expect_success, make_black_scholes_config, make_domai
 
 
 def main() -> None:
+    lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     B, T, N, M = 4096, 16, 256, 256
     sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=M, threads_per_block=256, mc_seed=7,
                                 buffer_size=512, dtype=Precision.float32)
@@ -24,6 +25,8 @@ def main() -> None:
     cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
                                domain_bounds=make_domain_bounds())
     pricer = expect_success(GbmCVNNPricer.create(cfg))
+    pricer.mc_lanes = lanes
+    pricer.math_mode = "hw"
     session = expect_success(pricer.open_session(make_training_config(num_batches=40, batch_size=B, learning_rate=1e-2)))
     for _ in range(4):
         expect_success(session.step())
@@ -40,7 +43,7 @@ def main() -> None:
     torch.cuda.synchronize()
     t_all = (time.perf_counter() - t0) * 1e3
     print("host ms per step() call:", " ".join(f"{x:.2f}" for x in ts))
-    print(f"enqueue of 20 steps {t_enq:.1f} ms, until done {t_all:.1f} ms ({t_all / 20:.3f} ms/step)")
+    print(f"lanes={lanes}: enqueue of 20 steps {t_enq:.1f} ms, until done {t_all:.1f} ms ({t_all / 20:.3f} ms/step)")
     session.close()
 
 

@@ -31,6 +31,9 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--budget-gb", type=float, default=40.0, help="path scratch budget (engine default)")
     ap.add_argument("--pitch", type=int, default=0, help="row pitch in elements (0: smc_path_pitch)")
+    ap.add_argument("--lanes", type=int, default=1, help="launches alternate over this many streams, each with "
+                    "its own cursor, sync area and path scratch (consecutive launches may overlap)")
+    ap.add_argument("--dynamic", action="store_true", help="SMC_TRAIN_DYNAMIC: every contract from the queue")
     ap.add_argument("--trace", default="", help="save per-workgroup timestamps (SMC_EXPERIMENT_TRACE builds)")
     a = ap.parse_args()
     B, T, N, M = SHAPES[a.config]
@@ -47,26 +50,33 @@ def main() -> None:
     chunk = max(1, min(B, int(a.budget_gb * (1 << 30)) // per))
     launches = -(-B // chunk)
     chunk = -(-B // launches)
-    paths = torch.empty((chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch),
-                        dtype=torch.float64 if f64 else torch.float32, device=dev)
+    lanes = a.lanes
+    pathss = [torch.empty((chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch),
+                          dtype=torch.float64 if f64 else torch.float32, device=dev) for _ in range(lanes)]
     eng = SobolEngine(6, 7, 0)
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(dev)
     lo = torch.tensor([0.001, 0.001, 0.0, -0.2, -0.2, 0.0], dtype=torch.float64, device=dev)
     hi = torch.tensor([1e4, 2e4, 10.0, 0.2, 0.2, 2.0], dtype=torch.float64, device=dev)
-    cur = torch.zeros(2, dtype=torch.int64, device=dev)
+    cur = torch.tensor([[k * B, k * B] for k in range(lanes)], dtype=torch.int64, device=dev)
     c = torch.empty((B, 6), dtype=torch.float64, device=dev)
     f = torch.empty((B, 6), dtype=torch.float32, device=dev)
     t = torch.empty((B, N), dtype=torch.complex128 if f64 else torch.complex64, device=dev)
     nsync = int(L.smc_train_step_sync_bytes(T, N, M, dcode, pitch))
-    sync = torch.zeros(max(nsync, 8), dtype=torch.uint8, device=dev)
-    scheme = _lib.SCHEME_LOG_EULER | (_lib.MATH_HW if a.math == "hw" else 0)
+    syncs = [torch.zeros(max(nsync, 8), dtype=torch.uint8, device=dev) for _ in range(lanes)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(lanes - 1)]
+    scheme = _lib.SCHEME_LOG_EULER | (_lib.MATH_HW if a.math == "hw" else 0) | (_lib.TRAIN_DYNAMIC if a.dynamic else 0)
+    n_launched = [0]
 
     def step():
-        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B, _lib.ptr(c),
-                                    None if f64 else _lib.ptr(f), B, T, N, M, 7, scheme, _lib.NORM_NORMALIZE, dcode,
-                                    store, _lib.ptr(paths), pitch, chunk, _lib.ptr(t), _lib.ptr(sync), nsync, None))
+        k = n_launched[0] % lanes
+        n_launched[0] += 1
+        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur[k]), 0, lanes * B,
+                                    _lib.ptr(c), None if f64 else _lib.ptr(f), B, T, N, M, 7, scheme,
+                                    _lib.NORM_NORMALIZE, dcode, store, _lib.ptr(pathss[k]), pitch, chunk, _lib.ptr(t),
+                                    _lib.ptr(syncs[k]), nsync, _lib.stream_handle(streams[k])))
 
-    step()
+    for _ in range(lanes):
+        step()
     torch.cuda.synchronize()
     if a.trace:  # the trace keeps the last launch only: zero it before the timed launches
         import ctypes
@@ -76,11 +86,15 @@ def main() -> None:
         a.iters = 1
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
+    for s_ in streams[1:]:
+        s_.wait_stream(torch.cuda.current_stream())
     for _ in range(a.iters):
         step()
+    for s_ in streams[1:]:
+        torch.cuda.current_stream().wait_stream(s_)
     e1.record()
     torch.cuda.synchronize()
-    assert _lib.sync_status(sync) == 0
+    assert all(_lib.sync_status(sy) == 0 for sy in syncs)
     if a.trace:  # gbm.hip g_trace: [workgroup][40] s_memrealtime stamps of the last launch
         import ctypes
         buf = np.zeros((1024, 40), dtype=np.uint64)
