@@ -113,8 +113,9 @@ struct OpF32 {
 struct MLayer {
   int32_t ni, no, act, win, wout, kx;  // kx = roundup(2 ni + 1, 16): rows of Z^T (ones row at 2 ni)
   int64_t w_re, w_im, b_re, b_im, act_bias;
-  int64_t wc, wct;   // Op offsets: Wc [wout][win], Wc^T [win][wout]
+  int64_t wc, wct;   // Op offsets: Wc [wout][win] (layered: [wout][kx] with the bias column at 2 ni), Wc^T [win][wout]
   int64_t zt, gt;    // Op offsets: Z^T [kx][bp], dU^T [wout][bp]
+  int64_t zr, dr;    // layered only: Z [bp][kx], dU [bp][wout] (row-major GEMM operands)
   int64_t pre;       // f32 offset of the pre-activation [R][2 no] in the workgroup's LDS (hidden layers
                      // with an activation), or -1
   int64_t cpart;     // f32 offset of the modReLU-bias partials [nwg][no], or -1
@@ -130,6 +131,8 @@ struct MArgs {
   int32_t segs;      // batch segments of the weight gradients
   int32_t zs, gs;    // LDS row strides (Op elements) of the activation and output-gradient buffers
   int32_t pre_global;  // pre-activations in the f32 workspace [bp][2 no] instead of LDS [R][2 no]
+  int32_t layered;   // wide layers: one MFMA GEMM launch per layer and direction (lgemm_kernel) instead of fb_kernel
+  int32_t lpb;       // loss partials per batch block of `rows` rows (1; layered: feature blocks of the last layer)
   int64_t n_params;
   int64_t pack_elems;
   const float* params;
@@ -509,6 +512,31 @@ __global__ __launch_bounds__(kFbThreads) void fb_kernel(MArgs a) {
 // during the current stage's MFMAs); wave w computes the 32 x 32 quarter (w / 2, w % 2) as 2 x 2
 // tiles.  Workgroups past the tile blocks sum the loss and modReLU-bias partials of one segment
 // per wave.
+// Bookkeeping items of the weight-gradient launch: wave w of bookkeeping workgroup `item` sums the
+// loss and modReLU-bias partials of batch segment 4 item + w into that segment's partials row.
+__device__ void wgrad_bookkeeping(const MArgs& a, int64_t item, int wave, int lane) {
+  const int64_t sg = item * kWaves + wave;
+  if (sg >= a.segs) return;
+  const int s = static_cast<int>(sg);
+  const int64_t seg_rows = a.bp / a.segs;
+  const int w0 = static_cast<int>(s * (seg_rows / a.rows)), w1 = static_cast<int>((s + 1) * (seg_rows / a.rows));
+  float* part = a.partials + s * (a.n_params + 1);
+  if (lane == 0) {
+    double t = 0.0;
+    for (int w = w0 * a.lpb; w < w1 * a.lpb; ++w) t += a.lossp[w];
+    part[a.n_params] = static_cast<float>(t / (static_cast<double>(a.batch) * a.layer[a.n_layers - 1].no));
+  }
+  for (int ll = 0; ll < a.n_layers; ++ll) {
+    const MLayer& ly = a.layer[ll];
+    if (ly.cpart < 0) continue;
+    for (int j = lane; j < ly.no; j += 64) {
+      double t = 0.0;
+      for (int w = w0; w < w1; ++w) t += a.fws[ly.cpart + static_cast<int64_t>(w) * ly.no + j];
+      part[ly.act_bias + j] = static_cast<float>(t);
+    }
+  }
+}
+
 constexpr int kWgBlock = 64;  // output block edge
 constexpr int kWgStage = 64;  // batch rows per K stage (bf16; 32 for f32: the same 36 KiB of LDS)
 
@@ -531,26 +559,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
   int l = 0;
   while (l < a.n_layers && item >= a.layer[l].items) item -= a.layer[l].items, ++l;
   if (l == a.n_layers) {
-    // bookkeeping: wave w of bookkeeping workgroup i sums segment 4 i + w
-    const int64_t sg = item * kWaves + wave;
-    if (sg >= a.segs) return;
-    const int s = static_cast<int>(sg);
-    const int w0 = static_cast<int>(s * (seg_rows / a.rows)), w1 = static_cast<int>((s + 1) * (seg_rows / a.rows));
-    float* part = a.partials + s * stride;
-    if (lane == 0) {
-      double t = 0.0;
-      for (int w = w0; w < w1; ++w) t += a.lossp[w];
-      part[a.n_params] = static_cast<float>(t / (static_cast<double>(a.batch) * a.layer[a.n_layers - 1].no));
-    }
-    for (int ll = 0; ll < a.n_layers; ++ll) {
-      const MLayer& ly = a.layer[ll];
-      if (ly.cpart < 0) continue;
-      for (int j = lane; j < ly.no; j += 64) {
-        double t = 0.0;
-        for (int w = w0; w < w1; ++w) t += a.fws[ly.cpart + static_cast<int64_t>(w) * ly.no + j];
-        part[ly.act_bias + j] = static_cast<float>(t);
-      }
-    }
+    wgrad_bookkeeping(a, item, wave, lane);
     return;
   }
   const MLayer& ly = a.layer[l];
@@ -642,6 +651,295 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
   }
 }
 
+// ---- layered step for wide layers (round 3) ----------------------------------------------------
+// fb_kernel keeps 16 batch rows on chip through every layer, so each of its workgroups streams every
+// weight matrix from L2: at H = 256 (1 MB per hidden layer) that is ~1 GB of L2 reads per step and the
+// step ran at 0.26 of the f32 MFMA peak.  Wide networks instead run one GEMM launch per layer and
+// direction over 128-feature x 64-row tiles, both operands staged through LDS in 64-deep K stages
+// (double-buffered, the next stage's global loads and the next 16-deep block's LDS fragments in flight
+// during the MFMAs; tools/micro/lgemm.hip: 0.55 of the f32 peak on the 512 x 4096 x 512 GEMM), with
+// the bias as an extra weight column against Z's ones column and the epilogues of fb_kernel fused:
+//   kLFwd  (hidden layer l): pre-activations -> workspace, activation -> Z_{l+1} (row-major and ^T)
+//   kLLast (last layer): prediction, loss partial, output gradient -> dU_L (row-major and ^T)
+//   kLBwd  (layer l, l >= 1): dZ_l = dU_l Wc_l, layer l-1's activation backward -> dU_{l-1}
+// wgrad_kernel then reads the ^T copies exactly as after fb_kernel (same partials, same reduction).
+#ifndef SMC_LGEMM_K
+#define SMC_LGEMM_K 64
+#endif
+constexpr int kLM = 128, kLN = 64, kLK = SMC_LGEMM_K, kLLd = kLK + 4;  // tile (features x batch rows), K stage, LDS stride
+constexpr int kLThreads = 256;                                // 4 waves x (32 features x 64 rows)
+constexpr int kLTM = kLM / 4 / 16, kLTN = kLN / 16;           // 16 x 16 tiles per wave
+enum { kLFwd = 0, kLLast = 1, kLBwd = 2 };
+
+// Wc [wout][kx] with the bias column, Wc^T [win][wout], and Z_0 / Z_0^T from the inputs (+ ones
+// column): blockIdx.y = region (2 l: Wc_l, 2 l + 1: Wc_l^T, 2 L: Z_0, 2 L + 1: Z_0^T), a grid-stride
+// loop over the region's rows and columns
+__global__ __launch_bounds__(kThreads) void lpack_kernel(MArgs a) {
+  float* ws = static_cast<float*>(a.opws);
+  const int reg = blockIdx.y;
+  const int L = a.n_layers;
+  if (reg < 2 * L) {
+    const MLayer& ly = a.layer[reg >> 1];
+    const bool transposed = reg & 1;
+    const int rows = transposed ? ly.win : ly.wout, cols = transposed ? ly.wout : ly.kx;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < static_cast<int64_t>(rows) * cols;
+         e += static_cast<int64_t>(gridDim.x) * kThreads) {
+      const int rr = static_cast<int>(e / cols), cc = static_cast<int>(e % cols);
+      const int f = transposed ? cc : rr, k = transposed ? rr : cc;
+      const int j = f >> 1, kk = k >> 1, ra = f & 1, rb = k & 1;
+      float v = 0.0f;
+      if (j < ly.no && kk < ly.ni) {
+        const float wa = a.params[ly.w_re + static_cast<int64_t>(j) * ly.ni + kk];
+        const float wb = a.params[ly.w_im + static_cast<int64_t>(j) * ly.ni + kk];
+        v = ra == rb ? wa : (ra == 0 ? -wb : wb);
+      } else if (j < ly.no && !transposed && k == 2 * ly.ni) {  // bias column: (b_re, b_im) of output j
+        const int64_t bo = ra == 0 ? ly.b_re : ly.b_im;
+        v = bo >= 0 ? a.params[bo + j] : 0.0f;
+      }
+      ws[(transposed ? ly.wct : ly.wc) + e] = v;
+    }
+    return;
+  }
+  // Z_0 [bp][kx] and Z_0^T [kx][bp]: interleaved (re, im) inputs, the ones column at 2 ni, zeros
+  const MLayer& l0 = a.layer[0];
+  const bool transposed = reg == 2 * L + 1;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; e < a.bp * l0.kx;
+       e += static_cast<int64_t>(gridDim.x) * kThreads) {
+    const int64_t row = transposed ? e % a.bp : e / l0.kx;
+    const int k = static_cast<int>(transposed ? e / a.bp : e % l0.kx);
+    float v = k == 2 * l0.ni ? 1.0f : 0.0f;
+    if (k < 2 * l0.ni && row < a.batch) {
+      const int64_t i = row * l0.ni + (k >> 1);
+      v = (k & 1) ? (a.in_im ? a.in_im[i] : 0.0f) : a.in_re[i];
+    }
+    ws[(transposed ? l0.zt : l0.zr) + e] = v;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
+  __shared__ __attribute__((aligned(16))) float sa[2][kLM * kLLd];
+  __shared__ __attribute__((aligned(16))) float sb[2][kLN * kLLd];
+  __shared__ double red[kLThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, c = lane & 15;
+  float* ws = static_cast<float*>(a.opws);
+  const float* P = a.params;
+  // C[m][n] = sum_k A[m][k] B[n][k]: fwd / last A = Wc [wout][kx], B = Z_l [bp][kx];
+  // bwd A = Wc^T [win][wout], B = dU_l [bp][wout]
+  const int mb = blockIdx.x, nb = blockIdx.y;
+  const int64_t kbeg = 0;
+  const MLayer& ly = a.layer[l];
+  const bool bwd = MODE == kLBwd;
+  const float* A = ws + (bwd ? ly.wct : ly.wc);
+  const float* B = ws + (bwd ? ly.dr : ly.zr);
+  const int K = bwd ? ly.wout : ly.kx;
+  const int64_t lda = K, ldb = K;
+  const int Mrows = bwd ? ly.win : ly.wout;
+  const int64_t Nrows = a.bp;
+  const int m0 = mb * kLM;
+  const int64_t n0 = static_cast<int64_t>(nb) * kLN;
+  constexpr int AV = kLM * kLK / 4 / kLThreads, BV = kLN * kLK / 4 / kLThreads;
+  f32x4 ra[AV], rb[BV];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      const int i = v * kLThreads + tid, r = i / (kLK / 4), q = i % (kLK / 4);
+      const bool ok = m0 + r < Mrows && k0 + 4 * q < K;
+      ra[v] = ok ? *reinterpret_cast<const f32x4*>(A + static_cast<int64_t>(m0 + r) * lda + kbeg + k0 + 4 * q)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      const int i = v * kLThreads + tid, r = i / (kLK / 4), q = i % (kLK / 4);
+      rb[v] = n0 + r < Nrows && k0 + 4 * q < K ? *reinterpret_cast<const f32x4*>(B + (n0 + r) * ldb + kbeg + k0 + 4 * q)
+                                               : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      const int i = v * kLThreads + tid, r = i / (kLK / 4), q = i % (kLK / 4);
+      *reinterpret_cast<f32x4*>(&sa[buf][r * kLLd + 4 * q]) = ra[v];
+    }
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      const int i = v * kLThreads + tid, r = i / (kLK / 4), q = i % (kLK / 4);
+      *reinterpret_cast<f32x4*>(&sb[buf][r * kLLd + 4 * q]) = rb[v];
+    }
+  };
+  f32x4 acc[kLTM][kLTN];
+#pragma unroll
+  for (int i = 0; i < kLTM; ++i)
+#pragma unroll
+    for (int j = 0; j < kLTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nst = (K + kLK - 1) / kLK;
+  fetch(0);
+  put(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1, k0 = st * kLK;
+    if (st + 1 < nst) fetch(k0 + kLK);
+    f32x4 af[2][kLTM], bf[2][kLTN];
+    auto ld = [&](int s, int kb) {
+#pragma unroll
+      for (int i = 0; i < kLTM; ++i)
+        af[s][i] = *reinterpret_cast<const f32x4*>(&sa[buf][((wave * kLTM + i) * 16 + c) * kLLd + kb + 4 * g]);
+#pragma unroll
+      for (int j = 0; j < kLTN; ++j)
+        bf[s][j] = *reinterpret_cast<const f32x4*>(&sb[buf][(j * 16 + c) * kLLd + kb + 4 * g]);
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int kb = 0; kb < kLK; kb += 16) {
+      const int s = (kb / 16) & 1;
+      if (kb + 16 < kLK) ld(s ^ 1, kb + 16);
+      if (k0 + kb < K) {  // uniform: K is a multiple of 16
+#pragma unroll
+        for (int i = 0; i < kLTM; ++i)
+#pragma unroll
+          for (int j = 0; j < kLTN; ++j) acc[i][j] = OpF32::mmav(acc[i][j], af[s][i], bf[s][j]);
+      }
+    }
+    if (st + 1 < nst) put(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue, through LDS: the accumulators go to a [feature][row] tile; each thread then takes
+  // 4 features of one batch row (row-major outputs, 16-B stores along the features) and finally whole
+  // 64-row feature lines (the ^T copies, 16-B stores along the batch): every global store is a full
+  // 16-B piece of a contiguous line instead of 4-B pieces of 16 lines
+  constexpr int TLD = kLM + 4;  // tile row stride (floats): [row][feature], 16-B pieces conflict-free
+  static_assert(kLN * TLD <= 2 * kLM * kLLd, "tile fits the A stage buffers");
+  float* tile = &sa[0][0];      // [kLN][TLD] over both A stage buffers, free after the K loop
+#pragma unroll
+  for (int i = 0; i < kLTM; ++i)
+#pragma unroll
+    for (int j = 0; j < kLTN; ++j)
+      *reinterpret_cast<f32x4*>(&tile[(j * 16 + c) * TLD + (wave * kLTM + i) * 16 + 4 * g]) = acc[i][j];
+  __syncthreads();
+#if defined(SMC_EXPERIMENT_LGEMM_NO_EPILOGUE)  // tools/micro decomposition builds only: the GEMM alone
+  if (tile[tid] == 1234.5f) a.fws[0] = 0.0f;
+  return;
+#endif
+  const int64_t bp = a.bp;
+  const int64_t blk = blockIdx.y;  // batch block of kLN rows (= a.rows)
+  // the layer whose output (or output gradient) this launch writes, and its row-major / ^T buffers
+  const MLayer& lo = MODE == kLBwd ? a.layer[l - 1] : ly;
+  const MLayer& nx = MODE == kLFwd ? a.layer[l + 1] : ly;
+  const int64_t rm_off = MODE == kLFwd ? nx.zr : lo.dr;
+  const int64_t tr_off = MODE == kLFwd ? nx.zt : lo.gt;
+  const int rm_ld = MODE == kLFwd ? nx.kx : lo.wout;  // row-major row length
+  const int nvalid = MODE == kLFwd ? ly.wout : lo.wout;  // features this launch writes
+  const int N = lo.no;
+  const float scale = 2.0f / static_cast<float>(static_cast<double>(a.batch) * ly.no);
+  // phase B: thread -> features 4q .. 4q + 3 (2 complex outputs) of rows rb, rb + 8, ..., in order
+  const int q = tid % (kLM / 4), rb0 = tid / (kLM / 4);
+  const int f0 = m0 + 4 * q;
+  double loss = 0.0;
+  float dcs[2] = {0.0f, 0.0f};
+  // the row loop's global inputs (targets / pre-activations) loaded ahead of its stores: one wave per
+  // SIMD cannot hide a load latency per row
+  constexpr int kRows = kLN / (kLThreads / (kLM / 4));  // rows per thread (8)
+  float2 in[kRows][2];
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const int64_t b = n0 + rb0 + k * (kLThreads / (kLM / 4));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int jj = (f0 >> 1) + h;
+      in[k][h] = float2{0.0f, 0.0f};
+      if (MODE == kLLast && jj < N && b < a.batch) in[k][h] = *reinterpret_cast<const float2*>(a.targets + (b * N + jj) * 2);
+      if (MODE == kLBwd && jj < N && lo.pre >= 0) in[k][h] = *reinterpret_cast<const float2*>(a.fws + lo.pre + b * (2 * N) + 2 * jj);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const int rr = rb0 + k * (kLThreads / (kLM / 4));
+    const int64_t b = n0 + rr;
+    const f32x4 x = *reinterpret_cast<const f32x4*>(&tile[rr * TLD + 4 * q]);
+    float o[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int jj = (f0 >> 1) + h;
+      const float u = x[2 * h], v = x[2 * h + 1];
+      o[2 * h] = o[2 * h + 1] = 0.0f;
+      if constexpr (MODE == kLFwd) {
+        if (jj < ly.no) {
+          if (ly.pre >= 0) *reinterpret_cast<float2*>(a.fws + ly.pre + b * (2 * ly.no) + 2 * jj) = float2{u, v};
+          Act::fwd(ly.act, ly.act == SMC_ACT_MODRELU ? P[ly.act_bias + jj] : 0.0f, u, v, o[2 * h], o[2 * h + 1]);
+        } else {
+          o[2 * h] = 2 * jj == 2 * ly.no ? 1.0f : 0.0f;  // Z_{l+1}'s ones column, then zeros
+        }
+      } else if (jj < N && (MODE == kLBwd || b < a.batch)) {
+        const float cb = lo.act == SMC_ACT_MODRELU ? P[lo.act_bias + jj] : 0.0f;
+        float dc;
+        if constexpr (MODE == kLLast) {
+          float pr, pi;
+          Act::fwd(lo.act, cb, u, v, pr, pi);
+          const float2 t = in[k][h];
+          const float dr = pr - t.x, di = pi - t.y;
+          loss += static_cast<double>(dr * dr) + static_cast<double>(di * di);
+          Act::bwd(lo.act, cb, u, v, scale * dr, scale * di, o[2 * h], o[2 * h + 1], dc);
+        } else {
+          const float2 pre = in[k][h];
+          Act::bwd(lo.act, cb, pre.x, pre.y, u, v, o[2 * h], o[2 * h + 1], dc);
+        }
+        dcs[h] += dc;
+      }
+    }
+    if (f0 < nvalid) *reinterpret_cast<f32x4*>(ws + rm_off + b * rm_ld + f0) = f32x4{o[0], o[1], o[2], o[3]};
+    *reinterpret_cast<f32x4*>(&tile[rr * TLD + 4 * q]) = f32x4{o[0], o[1], o[2], o[3]};  // the ^T copy's values
+  }
+  if constexpr (MODE != kLFwd) {
+    // modReLU bias share of the block's kLN rows: each thread's rows in order, then the kLN / 8 row
+    // groups in order (through LDS, after the ^T tile is complete)
+    float* part = sb[0];  // [8][kLM / 2] complex outputs
+    if (lo.cpart >= 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) part[rb0 * (kLM / 2) + 2 * q + h] = dcs[h];
+    }
+    if constexpr (MODE == kLLast) {  // block loss partial: thread sums, wave butterfly, waves in order
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) loss += __shfl_xor(loss, off, 64);
+      if (lane == 0) red[wave] = loss;
+    }
+    __syncthreads();
+    if (lo.cpart >= 0 && tid < kLM / 2) {
+      const int jj = m0 / 2 + tid;
+      float s = 0.0f;
+      for (int w = 0; w < kLThreads / (kLM / 4); ++w) s += part[w * (kLM / 2) + tid];
+      if (jj < N) a.fws[lo.cpart + blk * N + jj] = s;
+    }
+    if (MODE == kLLast && tid == 0) {
+      double t = 0.0;
+      for (int w = 0; w < kLThreads / 64; ++w) t += red[w];
+      a.lossp[blk * a.lpb + blockIdx.x] = t;
+    }
+  } else {
+    __syncthreads();
+  }
+  // phase C: the ^T copy, whole 64-row lines of each feature
+  for (int e = tid; e < kLM * (kLN / 4); e += kLThreads) {
+    const int fr = e / (kLN / 4), q4 = e % (kLN / 4);
+    if (m0 + fr < nvalid)
+      *reinterpret_cast<f32x4*>(ws + tr_off + static_cast<int64_t>(m0 + fr) * bp + n0 + 4 * q4) =
+          f32x4{tile[(4 * q4) * TLD + fr], tile[(4 * q4 + 1) * TLD + fr], tile[(4 * q4 + 2) * TLD + fr],
+                tile[(4 * q4 + 3) * TLD + fr]};
+  }
+  if constexpr (MODE == kLFwd) {
+    // columns [wout, kx_{l+1}) of Z_{l+1} (the ones column when 2 no is a multiple of 16)
+    if (blockIdx.x == gridDim.x - 1) {
+      for (int e = tid; e < (nx.kx - ly.wout) * kLN; e += kLThreads) {
+        const int k = ly.wout + e / kLN;
+        const int64_t b = n0 + e % kLN;
+        const float v = k == 2 * ly.no ? 1.0f : 0.0f;
+        ws[nx.zr + b * nx.kx + k] = v;
+        ws[nx.zt + static_cast<int64_t>(k) * bp + b] = v;
+      }
+    }
+  }
+}
+
 // ---- host plan ---------------------------------------------------------------------------------
 struct Plan {
   MArgs a;
@@ -688,6 +986,9 @@ int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, 
     wmax = m.win > wmax ? m.win : wmax;
   }
   const int wlast = a.layer[n_layers - 1].wout;
+  // wide layers (2 H >= 256, f32): the layered GEMM launches instead of fb_kernel
+  a.layered = !bf16 && wmax >= 256 ? 1 : 0;
+  a.lpb = 1;
   // LDS: split-K scratch [waves][RT][64] f32x4, two activation / gradient buffers [R][zs] and the last
   // layer's output gradient [R][gs]; row strides are odd multiples of 16 bytes (conflict-free
   // 16-byte fragment reads)
@@ -702,10 +1003,18 @@ int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, 
     a.pre_global = 1;
     per16 -= 16 * pre_floats * 4;
   }
-  if (per16 > kLdsCap) return fail(SMC_ERR_INVALID_SHAPE, "cvnn mfma: layer widths exceed the LDS budget");
-  p.rt = 2 * per16 <= kLdsPair && batch >= 4096 ? 2 : 1;
-  a.rows = 16 * p.rt;
-  p.lds = per16 * p.rt;
+  if (a.layered) {
+    a.pre_global = 1;
+    p.rt = 1;
+    a.rows = kLN;  // batch rows per block (modReLU and loss partials)
+    p.lds = 0;
+    a.lpb = (wlast + kLM - 1) / kLM;
+  } else {
+    if (per16 > kLdsCap) return fail(SMC_ERR_INVALID_SHAPE, "cvnn mfma: layer widths exceed the LDS budget");
+    p.rt = 2 * per16 <= kLdsPair && batch >= 4096 ? 2 : 1;
+    a.rows = 16 * p.rt;
+    p.lds = per16 * p.rt;
+  }
   // batch segments of the weight gradients: powers of two, >= kSegmentRows rows each, until the
   // (feature tile, column-tile group, segment) items fill the chip
   int64_t blocks = 0;  // weight-gradient output blocks (64 x 64) of one segment
@@ -722,12 +1031,14 @@ int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, 
   a.pack_elems = 0;
   for (int l = 0; l < n_layers; ++l) {
     MLayer& m = a.layer[l];
+    const int64_t kc = a.layered ? m.kx : m.win;  // layered: Wc with the bias column
     m.wc = op;
-    op += static_cast<int64_t>(m.wout) * m.win;
+    op += static_cast<int64_t>(m.wout) * kc;
     m.wct = op;
     op += static_cast<int64_t>(m.wout) * m.win;
-    a.pack_elems += 2LL * m.wout * m.win;
+    a.pack_elems += static_cast<int64_t>(m.wout) * (kc + m.win);
   }
+  if (a.layered) a.pack_elems += 2 * a.bp * a.layer[0].kx;  // Z_0 and Z_0^T
   for (int l = 0; l < n_layers; ++l) {
     MLayer& m = a.layer[l];
     op = roundup(op, 64);
@@ -736,6 +1047,15 @@ int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, 
     op = roundup(op, 64);
     m.gt = op;
     op += static_cast<int64_t>(m.wout) * a.bp;
+    m.zr = m.dr = -1;
+    if (a.layered) {
+      op = roundup(op, 64);
+      m.zr = op;
+      op += static_cast<int64_t>(m.kx) * a.bp;
+      op = roundup(op, 64);
+      m.dr = op;
+      op += static_cast<int64_t>(m.wout) * a.bp;
+    }
   }
   p.op_bytes = roundup(op * static_cast<int64_t>(es), 256);
   int64_t f = 0, pre_off = 0;
@@ -760,7 +1080,7 @@ int32_t make_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, 
   }
   p.f32_off = p.op_bytes;
   p.f64_off = roundup(p.f32_off + f * 4, 256);
-  p.ws_bytes = p.f64_off + static_cast<int64_t>(a.nwg) * 8;
+  p.ws_bytes = p.f64_off + static_cast<int64_t>(a.nwg) * a.lpb * 8;
   int64_t items = (a.segs + kWaves - 1) / kWaves;  // bookkeeping workgroups (one segment per wave)
   for (int l = 0; l < n_layers; ++l) items += a.layer[l].items;
   p.fb_grid = static_cast<unsigned>(a.nwg);
@@ -784,8 +1104,32 @@ int32_t launch_fb(const Plan& p, hipStream_t s) {
   return SMC_OK;
 }
 
+int32_t launch_layered(const Plan& p, hipStream_t s) {
+  const MArgs& a = p.a;
+  hipLaunchKernelGGL(lpack_kernel, dim3(256, 2 * a.n_layers + 2), dim3(kThreads), 0, s, a);
+  if (int32_t rc = check_launch("cvnn lpack_kernel")) return rc;
+  const unsigned by = static_cast<unsigned>(a.bp / kLN);
+  const int L = a.n_layers;
+  for (int l = 0; l < L; ++l) {
+    const dim3 grid(static_cast<unsigned>((a.layer[l].wout + kLM - 1) / kLM), by);
+    if (l + 1 < L) hipLaunchKernelGGL(lgemm_kernel<kLFwd>, grid, dim3(kLThreads), 0, s, a, l);
+    else hipLaunchKernelGGL(lgemm_kernel<kLLast>, grid, dim3(kLThreads), 0, s, a, l);
+    if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
+  }
+  for (int l = L - 1; l >= 1; --l) {
+    const dim3 grid(static_cast<unsigned>((a.layer[l].win + kLM - 1) / kLM), by);
+    hipLaunchKernelGGL(lgemm_kernel<kLBwd>, grid, dim3(kLThreads), 0, s, a, l);
+    if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
+  }
+  // weight gradients from the ^T copies, as after fb_kernel (its 64 x 64 blocks measured faster here
+  // than this file's GEMM tile over batch segments: 70 vs 74-81 us at C2/H=256)
+  hipLaunchKernelGGL(wgrad_kernel<OpF32>, dim3(p.wgrad_grid), dim3(kThreads), 0, s, a);
+  return check_launch("cvnn wgrad_kernel");
+}
+
 template <class Op>
 int32_t launch_all(const Plan& p, hipStream_t s) {
+  if (p.a.layered) return launch_layered(p, s);
   hipLaunchKernelGGL(pack_kernel<Op>, dim3(p.pack_grid), dim3(kThreads), 0, s, p.a);
   if (int32_t rc = check_launch("cvnn pack_kernel")) return rc;
   if (int32_t rc = p.rt == 2 ? launch_fb<Op, 2>(p, s) : launch_fb<Op, 1>(p, s)) return rc;

@@ -42,7 +42,14 @@ def build(arch: str, n_out: int) -> torch.nn.Module:
     if arch == "lastact":
         torch.manual_seed(6)
         return ComplexSequential(ComplexLinear(6, 32), modReLU(32), ComplexLinear(32, n_out), modReLU(n_out)).to(DEV)
-    width = 256 if arch == "h256" else 32
+    if arch == "widelast":  # wide (layered GEMM path), a width that is not a multiple of the 128 tile
+        torch.manual_seed(7)
+        return ComplexSequential(ComplexLinear(6, 160), modReLU(160), ComplexLinear(160, n_out), modReLU(n_out)).to(DEV)
+    if arch == "widez":
+        torch.manual_seed(8)
+        return ComplexSequential(ComplexLinear(6, 128), zReLU(), ComplexLinear(128, 144), modReLU(144),
+                                 ComplexLinear(144, n_out)).to(DEV)
+    width = {"h256": 256, "h128": 128}.get(arch, 32)
     return make_test_cvnn(n_inputs=6, n_outputs=n_out, seed=123, dtype=torch.float32, device=DEV,
                           hidden_layers=2, hidden_width=width)
 
@@ -70,8 +77,9 @@ def gpu_grads(model, compute: str, x: torch.Tensor, t: torch.Tensor) -> tuple[Fu
     return step, flat.cpu()
 
 
+# h256 / h128 / widelast / widez take the layered GEMM launches (2 H >= 256, csrc/cvnn_mfma.hip lgemm_kernel)
 CASES = [("c2", 256, 4096), ("c2", 256, 1000), ("c3", 1024, 2048), ("h256", 256, 4096), ("zrelu", 64, 21),
-         ("lastact", 96, 333)]
+         ("lastact", 96, 333), ("h256", 256, 1000), ("h128", 64, 777), ("widelast", 200, 333), ("widez", 64, 500)]
 
 
 @pytest.mark.parametrize("compute", ["mfma", "bf16"])
@@ -101,10 +109,11 @@ def test_mfma_step_matches_oracle(compute, arch, n_out, B) -> None:
         off += k
 
 
-@pytest.mark.parametrize("compute", ["mfma", "bf16"])
-def test_mfma_step_bit_reproducible(compute) -> None:
-    model = build("c3", 1024)
-    x, t = data(4096, 1024, seed=3)
+@pytest.mark.parametrize("compute,arch", [("mfma", "c3"), ("bf16", "c3"), ("mfma", "h256")])
+def test_mfma_step_bit_reproducible(compute, arch) -> None:
+    n_out = 1024 if arch == "c3" else 256
+    model = build(arch, n_out)
+    x, t = data(4096, n_out, seed=3)
     _, a = gpu_grads(model, compute, x, t)
     _, b = gpu_grads(model, compute, x, t)
     assert torch.equal(a, b)

@@ -24,8 +24,6 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BK = 32;          // K per LDS stage
-constexpr int LDK = BK + 4;     // LDS row stride (floats): 144 B, an odd multiple of 16 B
 
 __device__ __forceinline__ f32x4 mma4(f32x4 acc, f32x4 a, f32x4 b) {
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], acc, 0, 0, 0);
@@ -36,11 +34,12 @@ __device__ __forceinline__ f32x4 mma4(f32x4 acc, f32x4 a, f32x4 b) {
 
 // BM x BN tile per workgroup of NT threads; waves WM x WN, each (BM/WM) x (BN/WN) of 16x16 tiles.
 // TA / TB: the operand is stored [K][M] / [K][N] in global memory (transposed staging into LDS).
-template <int BM, int BN, int WM, int WN, bool TA, bool TB>
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int BK = 32, bool PF = false>
 __global__ __launch_bounds__(64 * WM * WN) void lgemm(const float* __restrict__ A, const float* __restrict__ B,
                                                        float* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                        int ksplit) {
   constexpr int NT = 64 * WM * WN;
+  constexpr int LDK = BK + 4;  // LDS row stride (floats): an odd multiple of 16 B
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 16x16 tiles per wave
   __shared__ __attribute__((aligned(16))) float sa[2][BM * LDK];
   __shared__ __attribute__((aligned(16))) float sb[2][BN * LDK];
@@ -113,19 +112,41 @@ __global__ __launch_bounds__(64 * WM * WN) void lgemm(const float* __restrict__ 
   for (int st = 0; st < nst; ++st) {
     const int buf = st & 1;
     if (st + 1 < nst) fetch(kbeg + (st + 1) * BK);
+    if constexpr (!PF) {
 #pragma unroll
-    for (int kb = 0; kb < BK; kb += 16) {
-      f32x4 af[TM], bf[TN];
+      for (int kb = 0; kb < BK; kb += 16) {
+        f32x4 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const f32x4*>(&sa[buf][((wm * TM + i) * 16 + c) * LDK + kb + 4 * g]);
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const f32x4*>(&sa[buf][((wm * TM + i) * 16 + c) * LDK + kb + 4 * g]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bf[j] = *reinterpret_cast<const f32x4*>(&sb[buf][((wn * TN + j) * 16 + c) * LDK + kb + 4 * g]);
+        for (int j = 0; j < TN; ++j)
+          bf[j] = *reinterpret_cast<const f32x4*>(&sb[buf][((wn * TN + j) * 16 + c) * LDK + kb + 4 * g]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mma4(acc[i][j], af[i], bf[j]);
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma4(acc[i][j], af[i], bf[j]);
+      }
+    } else {  // fragments of k block kb + 16 read while block kb's MFMAs issue
+      f32x4 af[2][TM], bf[2][TN];
+      auto ld = [&](int s, int kb) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[s][i] = *reinterpret_cast<const f32x4*>(&sa[buf][((wm * TM + i) * 16 + c) * LDK + kb + 4 * g]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bf[s][j] = *reinterpret_cast<const f32x4*>(&sb[buf][((wn * TN + j) * 16 + c) * LDK + kb + 4 * g]);
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int kb = 0; kb < BK; kb += 16) {
+        const int s = (kb / 16) & 1;
+        if (kb + 16 < BK) ld(s ^ 1, kb + 16);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma4(acc[i][j], af[s][i], bf[s][j]);
+      }
     }
     if (st + 1 < nst) put(buf ^ 1);
     __syncthreads();
@@ -142,11 +163,11 @@ __global__ __launch_bounds__(64 * WM * WN) void lgemm(const float* __restrict__ 
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB>
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int BK = 32, bool PF = false>
 float run(const char* name, const float* A, const float* B, float* C, int M, int N, int K, int lda, int ldb,
           int ksplit, const std::vector<float>& ha, const std::vector<float>& hb) {
   dim3 grid(M / BM, N / BN, ksplit);
-  auto launch = [&] { lgemm<BM, BN, WM, WN, TA, TB><<<grid, 64 * WM * WN>>>(A, B, C, M, N, K, lda, ldb, ksplit); };
+  auto launch = [&] { lgemm<BM, BN, WM, WN, TA, TB, BK, PF><<<grid, 64 * WM * WN>>>(A, B, C, M, N, K, lda, ldb, ksplit); };
   launch();
   (void)hipDeviceSynchronize();
   // spot check against a host dot product (split-K partials summed)
@@ -185,7 +206,7 @@ float run(const char* name, const float* A, const float* B, float* C, int M, int
 
 int main() {
   const int M = 512, N = 4096, K = 512;
-  std::vector<float> ha(static_cast<size_t>(4096) * 544), hb(static_cast<size_t>(4096) * 544);
+  std::vector<float> ha(static_cast<size_t>(4096) * 4096), hb(static_cast<size_t>(4096) * 4096);
   for (size_t i = 0; i < ha.size(); ++i) ha[i] = static_cast<float>((i * 2654435761u) % 1000) / 1000.f - 0.5f;
   for (size_t i = 0; i < hb.size(); ++i) hb[i] = static_cast<float>((i * 40503u + 7) % 1000) / 1000.f - 0.5f;
   float *A, *B, *C;
@@ -195,16 +216,18 @@ int main() {
   CK(hipMemcpy(A, ha.data(), ha.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(B, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
   // fwd / bwd-input: A [512][512] weights, B [4096][512] activations
-  run<64, 64, 2, 2, false, false>("NN 64x64 w2x2", A, B, C, M, N, K, K, K, 1, ha, hb);
-  run<128, 64, 2, 2, false, false>("NN 128x64 w2x2", A, B, C, M, N, K, K, K, 1, ha, hb);
-  run<64, 128, 2, 2, false, false>("NN 64x128 w2x2", A, B, C, M, N, K, K, K, 1, ha, hb);
-  run<128, 128, 2, 2, false, false>("NN 128x128 w2x2", A, B, C, M, N, K, K, K, 1, ha, hb);
-  run<128, 128, 2, 4, false, false>("NN 128x128 w2x4", A, B, C, M, N, K, K, K, 1, ha, hb);
-  run<64, 64, 1, 2, false, false>("NN 64x64 w1x2", A, B, C, M, N, K, K, K, 1, ha, hb);
-  // wgrad: A = dU stored [4096][512] (K-major), B = Z stored [4096][528 -> 512 here]
-  run<64, 64, 2, 2, true, true>("TT 64x64 w2x2 split8", A, B, C, 512, 512, 4096, 512, 512, 8, ha, hb);
-  run<64, 64, 2, 2, true, true>("TT 64x64 w2x2 split4", A, B, C, 512, 512, 4096, 512, 512, 4, ha, hb);
-  run<128, 64, 2, 2, true, true>("TT 128x64 w2x2 split8", A, B, C, 512, 512, 4096, 512, 512, 8, ha, hb);
-  run<128, 128, 2, 2, true, true>("TT 128x128 w2x2 split16", A, B, C, 512, 512, 4096, 512, 512, 16, ha, hb);
+  run<64, 64, 2, 2, false, false>("NN 64x64 w2x2 bk32", A, B, C, M, N, K, K, K, 1, ha, hb);
+  run<64, 64, 2, 2, false, false, 64>("NN 64x64 w2x2 bk64", A, B, C, M, N, K, K, K, 1, ha, hb);
+  run<64, 64, 2, 2, false, false, 32, true>("NN 64x64 w2x2 bk32 pf", A, B, C, M, N, K, K, K, 1, ha, hb);
+  run<64, 64, 2, 2, false, false, 64, true>("NN 64x64 w2x2 bk64 pf", A, B, C, M, N, K, K, K, 1, ha, hb);
+  run<128, 64, 2, 2, false, false, 64, true>("NN 128x64 w2x2 bk64 pf", A, B, C, M, N, K, K, K, 1, ha, hb);
+  run<64, 128, 2, 2, false, false, 64, true>("NN 64x128 w2x2 bk64 pf", A, B, C, M, N, K, K, K, 1, ha, hb);
+  run<128, 64, 4, 1, false, false, 64, true>("NN 128x64 w4x1 bk64 pf", A, B, C, M, N, K, K, K, 1, ha, hb);
+  run<64, 64, 1, 1, false, false, 64, true>("NN 64x64 w1x1 bk64 pf", A, B, C, M, N, K, K, K, 1, ha, hb);
+  run<32, 64, 1, 2, false, false, 64, true>("NN 32x64 w1x2 bk64 pf", A, B, C, M, N, K, K, K, 1, ha, hb);
+  // wgrad with K-contiguous copies (Z^T, dU^T written by the producing epilogue): NN over the batch
+  run<64, 64, 2, 2, false, false, 64, true>("wgrad NN 64x64 bk64 pf split8", A, B, C, 512, 512, 4096, 4096, 4096, 8, ha, hb);
+  run<64, 64, 2, 2, false, false, 64, true>("wgrad NN 64x64 bk64 pf split4", A, B, C, 512, 512, 4096, 4096, 4096, 4, ha, hb);
+  run<64, 64, 2, 2, true, true, 32, true>("wgrad TT 64x64 bk32 pf split8", A, B, C, 512, 512, 4096, 512, 512, 8, ha, hb);
   return 0;
 }
