@@ -343,11 +343,15 @@ def main() -> None:
         net_ms = n0.elapsed_time(n1) / args.kernel_iters
         kern = fused.kernels
         peak = 78.6 if (f64 and kern == "valu") else MFMA_PEAK_TFLOPS[kern]  # f64 vector peak (dense)
+        layered = kern == "mfma_f32" and 2 * max(widths) >= 256  # csrc/cvnn_mfma.hip make_plan
         desc_k = {"mfma_bf16": "pack + fb + wgrad (csrc/cvnn_mfma.hip, v_mfma_f32_16x16x32_bf16, bf16 operands, "
                                "f32 accumulate / master weights) + reduce/Adam + finalize",
                   "mfma_f32": "pack + fb + wgrad (csrc/cvnn_mfma.hip, v_mfma_f32_16x16x4_f32) + reduce/Adam + "
                               "finalize",
                   "valu": "forward_backward + reduce/Adam + finalize (csrc/cvnn.hip), VALU f32"}[kern]
+        if layered:
+            desc_k = ("lpack + one lgemm_kernel per layer and direction (v_mfma_f32_16x16x4_f32, 128x64 tiles, "
+                      "fused epilogues) + wgrad + reduce/Adam + finalize (csrc/cvnn_mfma.hip)")
         network = {"kernels": desc_k, "compute": kern, "flops_per_step": flops, "ms": net_ms,
                    "achieved": flops / (net_ms * 1e-3) / 1e12, "peak": peak, "unit": "TFLOP/s",
                    "frac": flops / (net_ms * 1e-3) / 1e12 / peak,
