@@ -78,8 +78,10 @@ def parse() -> argparse.Namespace:
                     help="MC part of step s+1 on its own stream beside step s's network part (pricer.overlap_mc)")
     ap.add_argument("--priority", default="network", choices=["network", "mc", "none"],
                     help="stream with the high queue priority (pricer.high_priority_stream)")
-    ap.add_argument("--lanes", type=int, default=1, help="MC lanes (pricer.mc_lanes): consecutive path launches "
+    ap.add_argument("--lanes", type=int, default=2, help="MC lanes (pricer.mc_lanes): consecutive path launches "
                     "on alternating streams, each starting in the previous one's tail")
+    ap.add_argument("--net-cus", type=int, default=32, help="CUs reserved for the network (pricer.network_cus)")
+    ap.add_argument("--net-cu-pattern", default="low", choices=["spread", "low"])
     ap.add_argument("--graphs", default="on", choices=["on", "off"], help="replay the step as hipGraphs")
     ap.add_argument("--kernel-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -247,6 +249,8 @@ def main() -> None:
     pricer.overlap_mc = args.overlap == "on"
     pricer.high_priority_stream = args.priority
     pricer.mc_lanes = args.lanes
+    pricer.network_cus = args.net_cus
+    pricer.network_cu_pattern = args.net_cu_pattern
     if n_assets:
         from spectralmc_amd.basket import BasketConfig, use_basket_engine
 

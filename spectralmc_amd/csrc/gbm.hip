@@ -1281,7 +1281,23 @@ size_t lds_bytes(int T, int N, bool cf) {
 
 // Resident workgroups of a persistent kernel on the current device (occupancy x CUs, cached
 // per (device, kernel)); grid = min(work items, that).
-int32_t resident_grid(const void* kernel, int threads, size_t lds, int64_t items, unsigned* grid) {
+// CUs a stream may use: the popcount of its CU mask (hipExtStreamCreateWithCUMask), else the device's
+int stream_cus(hipStream_t stream, int cus) {
+  if (!stream) return cus;
+  uint32_t mask[16] = {};
+  if (hipExtStreamGetCUMask(stream, 16, mask) != hipSuccess) {
+    (void)hipGetLastError();
+    return cus;
+  }
+  int n = 0;
+  for (int i = 0; i < 16 && i * 32 < cus; ++i) n += __builtin_popcount(mask[i]);
+  return n > 0 && n < cus ? n : cus;
+}
+
+// Persistent grid: the kernel's resident slots on the CUs `stream` may use (a CU-masked stream's
+// launch is sized to its mask, so every workgroup is resident at once), at most `items`.
+int32_t resident_grid(const void* kernel, int threads, size_t lds, int64_t items, unsigned* grid,
+                      hipStream_t stream = nullptr) {
   struct Entry {
     int dev;
     const void* kernel;
@@ -1304,6 +1320,15 @@ int32_t resident_grid(const void* kernel, int threads, size_t lds, int64_t items
     }
     slots = static_cast<unsigned>((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1));
     if (used < 32) cache[used++] = Entry{dev, kernel, lds, slots};
+  }
+  if (stream) {  // per CU = slots / all CUs; the stream's share
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
+      const int n = stream_cus(stream, cus);
+      if (n < cus) slots = slots / static_cast<unsigned>(cus) * static_cast<unsigned>(n);
+    } else {
+      (void)hipGetLastError();
+    }
   }
   *grid = static_cast<unsigned>(items < slots ? items : slots);
   return SMC_OK;
@@ -1424,7 +1449,8 @@ int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
   }
   const int W = a.res_slices > 1 ? a.res_slices : 1;
   unsigned grid = 0;
-  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kResThreads, lds, a.B * W, &grid)) return st;
+  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kResThreads, lds, a.B * W, &grid, stream))
+    return st;
   if (W > 1) {
     // whole groups of W co-resident workgroups (every slice of a group waits for the others),
     // in multiples of 8 W where possible so a group's slices share an XCD

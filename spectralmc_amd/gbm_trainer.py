@@ -413,11 +413,16 @@ class GbmCVNNPricer:
     #: "mc" or "none"
     high_priority_stream: str = "network"
     #: with overlap_mc: MC launches of consecutive steps alternate over this many streams (engine
-    #: lanes: own cursor, sync area and path scratch each), so step s + 1's path kernel may start on
-    #: the CUs step s's frees in its tail.  Back-to-back path launches gain 3 % from it (C2: 3.015 ->
-    #: 2.935 ms per launch), the training step nothing: the network kernels take those CUs first
-    #:, so the default is one MC stream
-    mc_lanes: int = 1
+    #: lanes: own cursor, sync area and path scratch each, every contract from the launch's queue), so
+    #: step s + 1's path kernel starts on the CUs step s's frees in its tail.  Taken only where the
+    #: engine allows it (one whole-contract resident launch per step); with the network on its own
+    #: CUs (network_cus) C2 runs 3.08 -> 2.98 ms/step
+    mc_lanes: int = 2
+    #: with engine lanes: CUs reserved for the network part (CU-masked HIP streams, the path kernels on
+    #: the rest; 0: none) and their choice of CU ids ("low": the lowest logical ids, which measured
+    #: best; "spread": evenly over the id range)
+    network_cus: int = 32
+    network_cu_pattern: str = "low"
     #: network forward/backward/Adam on the fused HIP kernels (csrc/cvnn.hip) when the CVNN is a
     #: ComplexLinear + modReLU/zReLU chain; False (or other architectures): torch-ROCm modules
     fused_network: bool = True
@@ -777,15 +782,25 @@ class TrainingSession:
         self.steps = 0
         self.engine.set_position(self.sobol_skip, pricer._mc_engine.ordinal)
         cur = torch.cuda.current_stream(dev)
+        self._hip_streams: list[int] = []  # CU-masked streams this session created (destroyed at close)
         if pricer.overlap_mc:
             # the network part is a few short launches: a high-priority queue lets its workgroups
             # take CU slots as the long MC kernel frees them instead of queueing behind it
             hi = pricer.high_priority_stream
-            self.stream = torch.cuda.Stream(device=dev, priority=-1 if hi == "network" else 0)
-            # one MC stream per engine lane: step s + 1's path launch may start on the CUs step s's
-            # launch frees in its tail (TrainingEngine lanes)
-            self.mc_streams = [torch.cuda.Stream(device=dev, priority=-1 if hi == "mc" else 0)
-                               for _ in range(getattr(self.engine, "lanes", 1))]
+            lanes = getattr(self.engine, "lanes", 1)
+            if pricer.network_cus > 0 and getattr(self.engine, "kernel_name", "") == "resident_kernel":
+                # the network on its own CUs beside the path kernels (CU-masked HIP streams); the path
+                # kernel sizes its persistent grid to its stream's CUs (gbm.hip resident_grid).  Only for
+                # the whole-contract resident launch (C2, the lock-step shape)
+                net_mask, mc_mask = _cu_masks(dev, pricer.network_cus, pricer.network_cu_pattern)
+                self.stream = _masked_stream(dev, net_mask, self._hip_streams)
+                self.mc_streams = [_masked_stream(dev, mc_mask, self._hip_streams) for _ in range(lanes)]
+            else:
+                self.stream = torch.cuda.Stream(device=dev, priority=-1 if hi == "network" else 0)
+                # one MC stream per engine lane: step s + 1's path launch may start on the CUs step s's
+                # launch frees in its tail (TrainingEngine lanes)
+                self.mc_streams = [torch.cuda.Stream(device=dev, priority=-1 if hi == "mc" else 0)
+                                   for _ in range(lanes)]
         else:
             self.stream = torch.cuda.Stream(device=dev)
             self.mc_streams = [self.stream]
@@ -890,16 +905,20 @@ class TrainingSession:
         for ms in self.mc_streams:
             ms.synchronize()
         dev = self.pricer._torch_device
-        torch.cuda.current_stream(dev).wait_stream(self.stream)
-        for ms in self.mc_streams:
-            torch.cuda.current_stream(dev).wait_stream(ms)
+        if not self._hip_streams:  # (masked streams: synchronised above, destroyed below)
+            torch.cuda.current_stream(dev).wait_stream(self.stream)
+            for ms in self.mc_streams:
+                torch.cuda.current_stream(dev).wait_stream(ms)
         loss, gn = (float(self.program.loss), float(self.program.grad_norm)) if self.steps else (0.0, 0.0)
         for p in self.params:  # detach the flat-buffer grad views from the parameters
             p.grad = p.grad.clone()
         self.sampler.skip(self.sobol_skip - self.sobol_skip0)
         check = getattr(self.engine, "check_status", None)
-        if check is not None:  # after the bookkeeping: the session is closed either way
-            check(self.mc_stream)
+        try:
+            if check is not None:  # after the bookkeeping: the session is closed either way
+                check(torch.cuda.current_stream(dev))  # every stream of the session is idle by now
+        finally:
+            _destroy_streams(self._hip_streams)
         return _BatchState(self.sobol_skip, self.global_step, loss, gn)
 
 
@@ -911,9 +930,52 @@ class TrainingSession:
         self.stream.synchronize()
         for ms in self.mc_streams:
             ms.synchronize()
+        _destroy_streams(self._hip_streams)
         for p in self.params:
             if p.grad is not None:
                 p.grad = p.grad.clone()
+
+
+def _cu_masks(dev: torch.device, n_net: int, pattern: str) -> tuple[list[int], list[int]]:
+    """32-bit mask words (hipExtStreamCreateWithCUMask) of the network's n_net CUs and of the rest."""
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    net = set(range(n_net)) if pattern == "low" else {(i * cus) // n_net for i in range(n_net)}
+    words = (cus + 31) // 32
+    nm, mm = [0] * words, [0] * words
+    for c in range(cus):
+        if c in net:
+            nm[c // 32] |= 1 << (c % 32)
+        else:
+            mm[c // 32] |= 1 << (c % 32)
+    return nm, mm
+
+
+def _hip():
+    import ctypes
+
+    return ctypes.CDLL("libamdhip64.so")
+
+
+def _masked_stream(dev: torch.device, mask: list[int], owned: list[int]) -> torch.cuda.ExternalStream:
+    """A HIP stream restricted to the CUs in `mask` (hipExtStreamCreateWithCUMask), as a torch stream;
+    its handle is appended to `owned` (the session destroys it at close)."""
+    import ctypes
+
+    handle = ctypes.c_void_p()
+    arr = (ctypes.c_uint32 * len(mask))(*mask)
+    with torch.cuda.device(dev):
+        if _hip().hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(mask)), arr) != 0:
+            raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+    owned.append(handle.value)
+    return torch.cuda.ExternalStream(handle.value, device=dev)
+
+
+def _destroy_streams(owned: list[int]) -> None:
+    import ctypes
+
+    for h in owned:
+        _hip().hipStreamDestroy(ctypes.c_void_p(h))
+    owned.clear()
 
 
 def _bounds_always_valid(lower: np.ndarray) -> bool:
