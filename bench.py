@@ -441,6 +441,11 @@ def main() -> None:
                      # time per launch and the fraction of peak it corresponds to
                      "kernel_ms_steady": steady_ms,
                      "frac_steady": (bytes_launch / (steady_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if steady_ms else None,
+                     "mc_note": ("consecutive path launches overlap (2 MC lanes on the CUs the network's 32 "
+                                 "masked CUs leave); kernel_ms = the launch alone on the whole chip, "
+                                 "kernel_ms_steady = launch spacing in the timed region; a rocprofv3 trace "
+                                 "of this run records each overlapped launch from its dispatch to its end"
+                                 if lanes > 1 else None),
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "contracts_per_launch": contracts_per_launch,
                      "measured_stream_gbs": stream_gbs,

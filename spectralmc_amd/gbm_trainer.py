@@ -937,8 +937,14 @@ class TrainingSession:
 
 
 def _cu_masks(dev: torch.device, n_net: int, pattern: str) -> tuple[list[int], list[int]]:
-    """32-bit mask words (hipExtStreamCreateWithCUMask) of the network's n_net CUs and of the rest."""
+    """32-bit mask words (hipExtStreamCreateWithCUMask) of the network's n_net CUs and of the rest.
+    Logical CU ids interleave the XCDs (ids 0..31 are 4 CUs of each of the 8 XCDs, one per shader
+    engine: tools/xcc_probe.py), and the dispatcher deals a grid's workgroups round-robin over them,
+    so "low" takes n_net / 32 CUs from every shader engine when n_net is a multiple of 32."""
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    if n_net % 32 or n_net >= cus:
+        raise ValueError(f"network_cus must be a multiple of 32 below {cus} (one CU per shader engine each), "
+                         f"got {n_net}")
     net = set(range(n_net)) if pattern == "low" else {(i * cus) // n_net for i in range(n_net)}
     words = (cus + 31) // 32
     nm, mm = [0] * words, [0] * words

@@ -18,4 +18,6 @@ for cfg in "$@"; do
   step bench_$cfg 300 python bench.py --config $cfg $extra
   step prof_$cfg 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$cfg -- python3 bench.py --config $cfg --no-cpu-baseline --steps 10
 done
+# the C2 path launch alone (one stream, full chip): the per-launch duration bench.py's roofline uses
+step prof_isolated 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_isolated -- python3 tools/kprof_step.py --config c2 --iters 20
 echo done
