@@ -37,15 +37,17 @@ def _train(batch: int, outfile: str, basket: int = 0) -> None:
         make_training_config,
     )
 
-    m = 32 if basket else M  # the basket engine takes N*M in multiples of 2048
+    # basket > 0: the basket engine (N*M in multiples of 2048); basket < 0: P = 4096, the shape the
+    # whole-contract resident kernel takes (MC lanes, the network on CU-masked streams)
+    m = 32 if basket > 0 else 64 if basket < 0 else M
     sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=m, mc_seed=7, buffer_size=1,
                                 dtype=Precision.float32)
-    model = make_test_cvnn(n_inputs=3 * basket + 4 if basket else 6, n_outputs=N, seed=123, dtype=torch.float32, device="cuda:0",
+    model = make_test_cvnn(n_inputs=3 * basket + 4 if basket > 0 else 6, n_outputs=N, seed=123, dtype=torch.float32, device="cuda:0",
                            hidden_layers=2)
     cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
                                domain_bounds=make_domain_bounds())
     pricer = expect_success(GbmCVNNPricer.create(cfg))
-    if basket:
+    if basket > 0:
         from spectralmc_amd.basket import BasketConfig, use_basket_engine
 
         use_basket_engine(pricer, BasketConfig(n_assets=basket, timesteps=T, network_size=N, batches_per_mc_run=m))
@@ -67,7 +69,7 @@ def _rank(rank: int, world: int, port: int, outdir: str, basket: int) -> None:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("basket", [0, 4], ids=["single_asset", "basket4"])
+@pytest.mark.parametrize("basket", [0, 4, -1], ids=["single_asset", "basket4", "resident_lanes"])
 def test_two_ranks_match_one_process_with_the_global_batch(tmp_path, basket) -> None:
     ctx = mp.get_context("spawn")
     port = _free_port()
@@ -89,7 +91,7 @@ def test_two_ranks_match_one_process_with_the_global_batch(tmp_path, basket) -> 
             np.testing.assert_allclose(r0[k], s[k], rtol=1e-4, atol=3e-4)
 
 
-def _rccl_single_rank(port: int, outfile: str) -> None:
+def _rccl_single_rank(port: int, outfile: str, shape: int = 0) -> None:
     """One RCCL rank driving the data-parallel step program: the network half as the two
     captured graphs around the eager RCCL all-reduce on the network stream, Adam as its own
     launch (fuse_adam off) — the path an 8-GPU node takes, minus the other ranks."""
@@ -108,12 +110,13 @@ def _rccl_single_rank(port: int, outfile: str) -> None:
         torch.testing.assert_close(flat.cpu(), torch.arange(7, dtype=torch.float32))
         ctx = dp.DataParallel(world_size=1, rank=0)
         dp.current = lambda: ctx  # a 1-rank RCCL group: world_size 1 normally means "no DP"
-        _train(2 * B_LOCAL, outfile)
+        _train(2 * B_LOCAL, outfile, shape)
     finally:
         dist.destroy_process_group()
 
 
-def test_rccl_step_program_single_rank_equals_plain_run(tmp_path) -> None:
+@pytest.mark.parametrize("shape", [0, -1], ids=["p256", "resident_lanes"])
+def test_rccl_step_program_single_rank_equals_plain_run(tmp_path, shape) -> None:
     """The RCCL (backend "nccl") code path on one GPU: init with a device id, the eager
     all-reduce between the fwd/bwd graph and the Adam graph.  A 1-rank all-reduce is the
     identity, so the run must equal the non-DP run up to the separate Adam launch (adam_kernel)
@@ -121,12 +124,12 @@ def test_rccl_step_program_single_rank_equals_plain_run(tmp_path) -> None:
     compilation units, equal to f32 rounding (measured: 32 of 192 weights 1 ulp apart after 4
     steps), and the grad norm's partial sums grouped differently."""
     ctx = mp.get_context("spawn")
-    p = ctx.Process(target=_rccl_single_rank, args=(_free_port(), str(tmp_path / "rccl.npz")))
+    p = ctx.Process(target=_rccl_single_rank, args=(_free_port(), str(tmp_path / "rccl.npz"), shape))
     p.start()
     p.join(timeout=600)
     assert p.exitcode == 0, f"RCCL rank exited with {p.exitcode}"
     plain = tmp_path / "plain.npz"
-    _train(2 * B_LOCAL, str(plain))
+    _train(2 * B_LOCAL, str(plain), shape)
     a, b = np.load(tmp_path / "rccl.npz"), np.load(plain)
     assert int(a["sobol_skip"]) == int(b["sobol_skip"])
     for k in a.files:
