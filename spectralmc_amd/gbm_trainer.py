@@ -788,10 +788,14 @@ class TrainingSession:
             # take CU slots as the long MC kernel frees them instead of queueing behind it
             hi = pricer.high_priority_stream
             lanes = getattr(self.engine, "lanes", 1)
-            if pricer.network_cus > 0 and getattr(self.engine, "kernel_name", "") == "resident_kernel":
+            fused = self.program.fused
+            narrow = fused is not None and max(t.in_features for t in fused.table) < 128
+            if pricer.network_cus > 0 and narrow and getattr(self.engine, "kernel_name", "") == "resident_kernel":
                 # the network on its own CUs beside the path kernels (CU-masked HIP streams); the path
                 # kernel sizes its persistent grid to its stream's CUs (gbm.hip resident_grid).  Only for
-                # the whole-contract resident launch (C2, the lock-step shape)
+                # the whole-contract resident launch (C2, the lock-step shape) and a narrow fused network
+                # (fb_kernel path: ~70 us of whole-chip work at C2); a wide one (C2/H=256: 0.27 ms) on 32
+                # CUs would outlast the path kernel (3.39 vs 3.30 ms/step)
                 net_mask, mc_mask = _cu_masks(dev, pricer.network_cus, pricer.network_cu_pattern)
                 self.stream = _masked_stream(dev, net_mask, self._hip_streams)
                 self.mc_streams = [_masked_stream(dev, mc_mask, self._hip_streams) for _ in range(lanes)]
