@@ -790,7 +790,9 @@ class TrainingSession:
             lanes = getattr(self.engine, "lanes", 1)
             fused = self.program.fused
             narrow = fused is not None and max(t.in_features for t in fused.table) < 128
-            if pricer.network_cus > 0 and narrow and getattr(self.engine, "kernel_name", "") == "resident_kernel":
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            if (pricer.network_cus > 0 and narrow and getattr(self.engine, "kernel_name", "") == "resident_kernel"
+                    and cus >= 4 * pricer.network_cus):
                 # the network on its own CUs beside the path kernels (CU-masked HIP streams); the path
                 # kernel sizes its persistent grid to its stream's CUs (gbm.hip resident_grid).  Only for
                 # the whole-contract resident launch (C2, the lock-step shape) and a narrow fused network
