@@ -179,9 +179,14 @@ static void twiddle(int64_t j, int64_t N, double* s_out, double* c_out) {
 }
 
 /* ---- f64 normals: op-for-op restatement of smc_math.h log_u32 / sincos2pi_u32 ---------- */
+#include "f64_tables.h"
 static inline uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
 static inline double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
 
+/* ln((a + 1) 2^-32): m = a + 1 = 2^e f exactly, f folded into [sqrt(1/2), sqrt(2)); table point
+ * c = 1 + i/64 nearest f (i = rint((f - 1) 64), i = 0 at f = 1 so no cancellation near u = 1),
+ * r = f INV - 1 in one fma, ln(1 + r) to r^8 (|r| <= 0.0078: truncation < 3e-19 of r), then
+ * (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))) with ln 2 as a double plus its remainder. */
 static double log_u32(uint32_t a) {
   const double m = (double)a + 1.0;
   const uint64_t bits = d2u(m);
@@ -190,22 +195,19 @@ static double log_u32(uint32_t a) {
   const int hi = fb > 0x3FF6A09E667F3BCDull;
   if (hi) { fb -= 0x0010000000000000ull; e += 1; }
   const double f = u2d(fb);
-  const double sn = (f - 1.0) / (f + 1.0);
-  const double t = sn * sn;
-  double p = 0.08695652173913043;
-  p = fma(p, t, 0.09523809523809523);
-  p = fma(p, t, 0.10526315789473684);
-  p = fma(p, t, 0.11764705882352941);
-  p = fma(p, t, 0.13333333333333333);
-  p = fma(p, t, 0.15384615384615385);
-  p = fma(p, t, 0.18181818181818182);
-  p = fma(p, t, 0.2222222222222222);
-  p = fma(p, t, 0.2857142857142857);
-  p = fma(p, t, 0.4);
-  p = fma(p, t, 0.6666666666666666);
-  const double lf = fma(sn * t, p, 2.0 * sn);
+  const int i = (int)rint((f - 1.0) * 64.0);
+  const double* t = kF64LogTab[i + 32];
+  const double r = fma(f, t[0], -1.0);
+  double q = -0.125;
+  q = fma(q, r, 0.14285714285714285);
+  q = fma(q, r, -0.16666666666666666);
+  q = fma(q, r, 0.2);
+  q = fma(q, r, -0.25);
+  q = fma(q, r, 0.3333333333333333);
+  q = fma(q, r, -0.5);
+  const double p = fma(q, r * r, r);
   const double k = (double)(e - 32);
-  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, lf));
+  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, t[1] + (t[2] + p)));
 }
 
 static void sincos_series(double x, double* s_out, double* c_out) {
@@ -232,38 +234,46 @@ static void sincos_series(double x, double* s_out, double* c_out) {
   *c_out = fma(c, -u, 1.0);
 }
 
+/* (sin, cos)(2 pi b 2^-32): nearest table angle j = round(b / 2^24) (mod 256), rem = b - j 2^24 in
+ * [-2^23, 2^23) exactly, x = 2 pi rem 2^-32 (|x| <= pi/256), sin x to x^7, cos x to x^6, then the
+ * rotation by the table's (sin, cos)(2 pi j / 256). */
 static void sincos2pi_u32(uint32_t b, double* s_out, double* c_out) {
-  const uint32_t k = (b + (1u << 29)) >> 30;
-  const int32_t rem = (int32_t)(b - (k << 30));
+  const uint32_t j = ((b + (1u << 23)) >> 24) & 255u;
+  const int32_t rem = (int32_t)(b - (j << 24));
   const double x = (double)rem * 0x1p-32 * 6.283185307179586;
-  double s, c;
-  sincos_series(x, &s, &c);
-  const int odd = (k & 1u) != 0u;
-  const double sb = odd ? c : s, cb = odd ? s : c;
-  *s_out = (k & 2u) ? -sb : sb;
-  *c_out = ((k + 1u) & 2u) ? -cb : cb;
+  const double u = x * x;
+  double sp = -0.0001984126984126984;
+  sp = fma(sp, u, 0.008333333333333333);
+  sp = fma(sp, u, -0.16666666666666666);
+  const double sx = fma(sp * u, x, x);
+  double cp = -0.001388888888888889;
+  cp = fma(cp, u, 0.041666666666666664);
+  cp = fma(cp, u, -0.5);
+  const double cx = fma(cp, u, 1.0);
+  const double S = kF64SinCosTab[j][0], C = kF64SinCosTab[j][1];
+  *s_out = fma(S, cx, C * sx);
+  *c_out = fma(C, cx, -(S * sx));
 }
 
-/* e^y as smc_math.h exp_f64 (the f64 device recursion; the oracle's reference mode keeps libm exp) */
+/* e^y as smc_math.h exp_f64 (the f64 device recursion; the oracle's reference mode keeps libm exp):
+ * n = rint(y 64 / ln 2) = 64 m + j, r = y - n ln2/64 (Cody-Waite: ln2/64 with 17 trailing zero bits
+ * plus its remainder, each a fused step; |r| <= 0.0055), e^r - 1 to r^6, 2^(j/64) from the table,
+ * exact ldexp by m. */
 double oracle_exp_f64(double y) {
-  const double n = rint(y * 1.4426950408889634);
-  double r = fma(-n, 0.6931471803691238, y);
-  r = fma(-n, 1.9082149292705877e-10, r);
-  double p = 1.6059043836821613e-10;
-  p = fma(p, r, 2.08767569878681e-09);
-  p = fma(p, r, 2.505210838544172e-08);
-  p = fma(p, r, 2.755731922398589e-07);
-  p = fma(p, r, 2.7557319223985893e-06);
-  p = fma(p, r, 2.48015873015873e-05);
-  p = fma(p, r, 0.0001984126984126984);
-  p = fma(p, r, 0.001388888888888889);
-  p = fma(p, r, 0.008333333333333333);
-  p = fma(p, r, 0.041666666666666664);
-  p = fma(p, r, 0.16666666666666666);
-  p = fma(p, r, 0.5);
-  p = fma(p, r, 1.0);
-  p = fma(p, r, 1.0);
-  return ldexp(p, (int)n);
+  const double n = rint(y * 92.33248261689366);
+  const int ni = (int)n;
+  const int j = ni & 63;
+  const int mm = (ni - j) / 64;
+  double r = fma(-n, 0.010830424696223417, y);
+  r = fma(-n, 2.572804622327669e-14, r);
+  double q = 0.001388888888888889;
+  q = fma(q, r, 0.008333333333333333);
+  q = fma(q, r, 0.041666666666666664);
+  q = fma(q, r, 0.16666666666666666);
+  q = fma(q, r, 0.5);
+  const double em1 = fma(q, r * r, r);
+  const double T = kF64Exp2Tab[j];
+  return ldexp(fma(T, em1, T), mm);
 }
 double oracle_log_u32(uint32_t a) { return log_u32(a); }
 void oracle_sincos2pi_u32(uint32_t b, double* s, double* c) { sincos2pi_u32(b, s, c); }

@@ -679,6 +679,7 @@ template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
 __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void contract_kernel(EngineArgs a) {
   extern __shared__ double lds[];
   __shared__ int flag;
+  if constexpr (sizeof(Real) == 8) math::f64_tables_load();
   run_slice<Real, LOG_EULER, HW, ALLROWS>(a, blockIdx.x, 0, lds, &flag);
 }
 
@@ -757,6 +758,7 @@ __global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __global__ __launch_bounds__(kThreads) void rows_kernel(EngineArgs a) {
   extern __shared__ double lds[];
+  if constexpr (sizeof(Real) == 8) math::f64_tables_load();
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
   const int64_t pitch = a.pitch ? a.pitch : a.P;
   const int T = a.T;
@@ -1195,6 +1197,7 @@ __global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void queue_kernel(EngineA
   extern __shared__ double lds[];
   __shared__ int flag;
   __shared__ int64_t next_item;
+  if constexpr (sizeof(Real) == 8) math::f64_tables_load();
   const int W = a.slices;
   uint32_t* queues = a.queues;
   unsigned xcc;
@@ -1249,6 +1252,7 @@ __global__ __launch_bounds__(256) void normalize_kernel(const double* __restrict
 template <typename Real, bool HW>
 __global__ __launch_bounds__(256) void normals_kernel(uint64_t seed, uint64_t ordinal, int32_t rows,
                                                       int64_t cols, Real* __restrict__ out) {
+  if constexpr (sizeof(Real) == 8) math::f64_tables_load();  // before any thread leaves
   const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;  // path group
   if (g * kPathsPerLane >= cols) return;
   PathStream s(seed, ordinal, static_cast<uint64_t>(g));

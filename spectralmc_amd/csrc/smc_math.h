@@ -18,6 +18,8 @@
 
 #include <cstdint>
 
+#include "smc_f64_tables.h"
+
 #pragma clang fp contract(off)
 
 namespace smc {
@@ -150,14 +152,37 @@ __device__ __forceinline__ void twiddle(int64_t j, int64_t N, double& s_out, dou
 }
 
 // ---- f64 path engine: the Box-Muller transcendentals of 32-bit uniforms and exp ------------
-// Fixed IEEE-754 sequences (fma, +, -, *, correctly rounded / and sqrt, rint, exact ldexp and bit
-// manipulation), restated op for op by oracle/gbm_oracle.c, so f64 normals are bit-identical on the
-// CPU.  Each is a fraction of the generic OCML routine's VALU work (log 98, sincospi 71, exp 42
-// instructions) because the argument domain is known: the uniforms are 32-bit integers.
+// Fixed IEEE-754 sequences (fma, +, -, *, rint, exact ldexp and bit manipulation) over tables
+// (smc_f64_tables.h: generated in 60-digit decimal arithmetic, rounded to double), restated op for op
+// by oracle/gbm_oracle.c, so f64 normals and paths are bit-identical on the CPU.  Accuracy against libm
+// (tests/test_oracle.py): ln within 1 ulp, (sin, cos) within 2^-53 absolute, exp within 1 ulp.  Round 3
+// replaced the division-based ln series, the 9/10-term sin/cos series and the 14-term exp series (≈ 80
+// VALU instructions per path-step) by table point + short polynomial.  The kernels that run them copy
+// the tables into LDS first (f64_tables_load): a global load on the path loop would wait for the
+// wave's outstanding path stores (one vmcnt counter).
+struct F64Tables {
+  double log[64][3];   // INV, -ln(INV) hi, lo at c = 1 + i/64, i = -32..31
+  double sc[256][2];   // (sin, cos)(2 pi j / 256)
+  double ex[64];       // 2^(j / 64)
+};
 
-// ln((a + 1) 2^-32) for a 32-bit a: m = a + 1 = 2^e f exactly, f folded into [sqrt(1/2), sqrt(2)),
-// ln f = 2 atanh(s), s = (f - 1) / (f + 1), |s| <= 0.1716: 2 s + s t P(t), t = s^2, P to t^10
-// (truncation < 2e-19); then + (e - 32) ln 2, ln 2 as a double plus its 2.3e-17 remainder, fused.
+__device__ __forceinline__ F64Tables& f64_lds() {
+  __shared__ F64Tables t;
+  return t;
+}
+
+// Every thread of the workgroup, before the workgroup's first f64 path math.
+__device__ inline void f64_tables_load() {
+  F64Tables& t = f64_lds();
+  for (int k = threadIdx.x; k < 64 * 3; k += blockDim.x) (&t.log[0][0])[k] = (&kF64LogTab[0][0])[k];
+  for (int k = threadIdx.x; k < 256 * 2; k += blockDim.x) (&t.sc[0][0])[k] = (&kF64SinCosTab[0][0])[k];
+  for (int k = threadIdx.x; k < 64; k += blockDim.x) t.ex[k] = kF64Exp2Tab[k];
+  __syncthreads();
+}
+
+// ln((a + 1) 2^-32): m = a + 1 = 2^e f exactly, f folded into [sqrt(1/2), sqrt(2)); table point
+// c = 1 + i/64 nearest f (i = 0 at f = 1: no cancellation near u = 1), r = f INV - 1 in one fma,
+// ln(1 + r) to r^8 (|r| <= 0.0078), then (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))).
 __device__ __forceinline__ double log_u32(uint32_t a) {
   const double m = static_cast<double>(a) + 1.0;  // exact: a + 1 <= 2^32
   const uint64_t bits = __double_as_longlong(m);
@@ -167,61 +192,60 @@ __device__ __forceinline__ double log_u32(uint32_t a) {
   fb -= hi ? 0x0010000000000000ull : 0ull;
   e += hi ? 1 : 0;
   const double f = __longlong_as_double(static_cast<long long>(fb));
-  const double sn = (f - 1.0) / (f + 1.0);
-  const double t = sn * sn;
-  double p = 0.08695652173913043;      // 2/23
-  p = fma(p, t, 0.09523809523809523);  // 2/21
-  p = fma(p, t, 0.10526315789473684);  // 2/19
-  p = fma(p, t, 0.11764705882352941);  // 2/17
-  p = fma(p, t, 0.13333333333333333);  // 2/15
-  p = fma(p, t, 0.15384615384615385);  // 2/13
-  p = fma(p, t, 0.18181818181818182);  // 2/11
-  p = fma(p, t, 0.2222222222222222);   // 2/9
-  p = fma(p, t, 0.2857142857142857);   // 2/7
-  p = fma(p, t, 0.4);                  // 2/5
-  p = fma(p, t, 0.6666666666666666);   // 2/3
-  const double lf = fma(sn * t, p, 2.0 * sn);
+  const int i = static_cast<int>(rint((f - 1.0) * 64.0));
+  const double* t = f64_lds().log[i + 32];
+  const double r = fma(f, t[0], -1.0);
+  double q = -0.125;
+  q = fma(q, r, 0.14285714285714285);
+  q = fma(q, r, -0.16666666666666666);
+  q = fma(q, r, 0.2);
+  q = fma(q, r, -0.25);
+  q = fma(q, r, 0.3333333333333333);
+  q = fma(q, r, -0.5);
+  const double p = fma(q, r * r, r);
   const double k = static_cast<double>(e - 32);
-  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, lf));
+  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, t[1] + (t[2] + p)));
 }
 
-// (sin, cos)(2 pi b 2^-32) for a 32-bit b: exact quarter-turn reduction in integers (nearest
-// quarter k = round(b / 2^30), rem = b - k 2^30 in [-2^29, 2^29)), x = 2 pi rem 2^-32 (|x| <= pi/4;
-// rem 2^-32 exact), the series, then the rotation by k quarter turns.
+// (sin, cos)(2 pi b 2^-32): nearest table angle j = round(b / 2^24) (mod 256), rem = b - j 2^24 in
+// [-2^23, 2^23) exactly, x = 2 pi rem 2^-32 (|x| <= pi/256), sin x to x^7, cos x to x^6, then the
+// rotation by the table's (sin, cos)(2 pi j / 256).
 __device__ __forceinline__ void sincos2pi_u32(uint32_t b, double& s_out, double& c_out) {
-  const uint32_t k = (b + (1u << 29)) >> 30;  // 0..3 (b near 2^32 wraps to quarter 0)
-  const int32_t rem = static_cast<int32_t>(b - (k << 30));
+  const uint32_t j = ((b + (1u << 23)) >> 24) & 255u;
+  const int32_t rem = static_cast<int32_t>(b - (j << 24));
   const double x = static_cast<double>(rem) * 0x1p-32 * 6.283185307179586;
-  double s, c;
-  sincos_series(x, s, c);
-  const bool odd = (k & 1u) != 0u;
-  const double sb = odd ? c : s, cb = odd ? s : c;
-  s_out = (k & 2u) ? -sb : sb;
-  c_out = ((k + 1u) & 2u) ? -cb : cb;
+  const double u = x * x;
+  double sp = -0.0001984126984126984;
+  sp = fma(sp, u, 0.008333333333333333);
+  sp = fma(sp, u, -0.16666666666666666);
+  const double sx = fma(sp * u, x, x);
+  double cp = -0.001388888888888889;
+  cp = fma(cp, u, 0.041666666666666664);
+  cp = fma(cp, u, -0.5);
+  const double cx = fma(cp, u, 1.0);
+  const double* sc = f64_lds().sc[j];
+  s_out = fma(sc[0], cx, sc[1] * sx);
+  c_out = fma(sc[1], cx, -(sc[0] * sx));
 }
 
-// e^y: n = rint(y / ln 2), r = y - n ln2 (Cody-Waite: fdlibm's ln2_hi, 21 trailing zero bits, and
-// ln2_lo, each a fused step), e^r by Taylor terms to r^13 / 13! (|r| <= 0.347: truncation < 5e-18),
-// exact ldexp.  No overflow handling: the path recursion's exponents stay within |y| < 700.
+// e^y: n = rint(y 64 / ln 2) = 64 m + j, r = y - n ln2/64 (Cody-Waite: ln2/64 with 17 trailing zero bits
+// plus its remainder, each a fused step; |r| <= 0.0055), e^r - 1 to r^6, 2^(j/64) from the table, exact
+// ldexp by m.  No overflow handling: the path recursion's exponents stay within |y| < 700.
 __device__ __forceinline__ double exp_f64(double y) {
-  const double n = rint(y * 1.4426950408889634);
-  double r = fma(-n, 0.6931471803691238, y);
-  r = fma(-n, 1.9082149292705877e-10, r);
-  double p = 1.6059043836821613e-10;  // 1/13!
-  p = fma(p, r, 2.08767569878681e-09);      // 1/12!
-  p = fma(p, r, 2.505210838544172e-08);     // 1/11!
-  p = fma(p, r, 2.755731922398589e-07);     // 1/10!
-  p = fma(p, r, 2.7557319223985893e-06);    // 1/9!
-  p = fma(p, r, 2.48015873015873e-05);      // 1/8!
-  p = fma(p, r, 0.0001984126984126984);     // 1/7!
-  p = fma(p, r, 0.001388888888888889);      // 1/6!
-  p = fma(p, r, 0.008333333333333333);      // 1/5!
-  p = fma(p, r, 0.041666666666666664);      // 1/4!
-  p = fma(p, r, 0.16666666666666666);       // 1/3!
-  p = fma(p, r, 0.5);
-  p = fma(p, r, 1.0);
-  p = fma(p, r, 1.0);
-  return ldexp(p, static_cast<int>(n));
+  const double n = rint(y * 92.33248261689366);
+  const int ni = static_cast<int>(n);
+  const int j = ni & 63;
+  const int mm = (ni - j) / 64;
+  double r = fma(-n, 0.010830424696223417, y);
+  r = fma(-n, 2.572804622327669e-14, r);
+  double q = 0.001388888888888889;
+  q = fma(q, r, 0.008333333333333333);
+  q = fma(q, r, 0.041666666666666664);
+  q = fma(q, r, 0.16666666666666666);
+  q = fma(q, r, 0.5);
+  const double em1 = fma(q, r * r, r);
+  const double T = f64_lds().ex[j];
+  return ldexp(fma(T, em1, T), mm);
 }
 
 }  // namespace math
