@@ -352,19 +352,23 @@ def main() -> None:
                                "f32 accumulate / master weights) + reduce/Adam + finalize",
                   "mfma_f32": "pack + fb + wgrad (csrc/cvnn_mfma.hip, v_mfma_f32_16x16x4_f32) + reduce/Adam + "
                               "finalize",
-                  "valu": "forward_backward + reduce/Adam + finalize (csrc/cvnn.hip), VALU f32"}[kern]
+                  "valu": "forward_backward + reduce/Adam + finalize (csrc/cvnn.hip), VALU "
+                          + ("f64" if f64 else "f32")}[kern]
         if layered:
             desc_k = ("lpack + one lgemm_kernel per layer and direction (v_mfma_f32_16x16x4_f32, 128x64 tiles, "
                       "fused epilogues) + wgrad + reduce/Adam + finalize (csrc/cvnn_mfma.hip)")
         network = {"kernels": desc_k, "compute": kern, "flops_per_step": flops, "ms": net_ms,
                    "achieved": flops / (net_ms * 1e-3) / 1e12, "peak": peak, "unit": "TFLOP/s",
                    "frac": flops / (net_ms * 1e-3) / 1e12 / peak,
-                   "peak_note": "dense MFMA peak of the operand type (bf16 2.52 PF; f32 MFMA = f32 VALU "
-                                "157.3 TF), MI355X_MICROARCH.md",
-                   "note": "small complex GEMMs (K = 12..512) plus the targets read, timed alone; in the "
-                           "step it is enqueued on its own high-priority stream and its workgroups take the "
-                           "CUs the path kernels free in their tails (a path kernel holds every CU while its "
-                           "contract queue lasts)"}
+                   "peak_note": ("f64 vector peak 78.6 TF (dense), MI355X_MICROARCH.md" if peak == 78.6 else
+                                 "dense MFMA peak of the operand type (bf16 2.52 PF; f32 MFMA = f32 VALU "
+                                 "157.3 TF), MI355X_MICROARCH.md"),
+                   "note": "small complex GEMMs (K = 12..512) plus the targets read, timed alone; " + (
+                       "in the step it runs after the path kernel on the same stream (rows_kernel holds every "
+                       "CU slot for its whole duration; gbm_trainer.py)"
+                       if session.engine.kernel_name == "rows_kernel+cf_kernel" or not pricer.overlap_mc else
+                       "in the step it is enqueued on its own stream and its workgroups take the CUs the path "
+                       "kernels leave (32 CU-masked CUs at C2; else the tails)")}
 
     # ---- measured HBM ceilings on this device (STREAM-style, 8 GiB buffers) --------------
     stream_gbs = {}

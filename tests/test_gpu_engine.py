@@ -470,6 +470,56 @@ def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store, ch
         assert not sync.view(torch.int32).any()  # done counter, status word and contract queue
 
 
+ROWS_STEP_CASES = [  # (B, T, N, M, dtype, store, chunk): smc_train_step shapes on rows_kernel + cf_kernel
+    (None, 16, 64, 64, _lib.DTYPE_F64, _lib.STORE_ALL, None),      # f64, > 4 contracts per workgroup slot
+    (2500, 5, 32, 64, _lib.DTYPE_F64, _lib.STORE_TERMINAL, 900),   # f64, three chunk launches, odd T
+    (None, 3, 64, 32, _lib.DTYPE_F32, _lib.STORE_ALL, None),       # f32, P = 2048 (not a resident shape)
+]
+
+
+@pytest.mark.parametrize("B,T,N,M,dtype,store,chunk", ROWS_STEP_CASES)
+def test_rows_train_step_dynamic_queue_equals_targets(golden, B, T, N, M, dtype, store, chunk) -> None:
+    """smc_train_step on the rows_kernel shapes hands contracts out from the sync area's queue (first
+    contract by workgroup index, the rest from the counter); bit-identical to smc_train_targets'
+    static striding (the oracle-checked path), over three steps; the queue is reset (sync zeroed)."""
+    L = _L()
+    if B is None:
+        B = 4 * 4 * torch.cuda.get_device_properties(0).multi_processor_count + 5
+    chunk = chunk or B
+    P = N * M
+    f64 = dtype == _lib.DTYPE_F64
+    pitch = int(L.smc_path_pitch(P, dtype))
+    assert L.smc_train_step_kernel(T, N, M, dtype, pitch) == b"rows_kernel+cf_kernel"
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
+    lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
+    hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
+    shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
+    paths = torch.empty(shape, dtype=torch.float64 if f64 else torch.float32, device=DEV)
+    ctype = torch.complex128 if f64 else torch.complex64
+    cur_a = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
+    cur_b = cur_a.clone()
+    nsync = int(L.smc_train_step_sync_bytes(T, N, M, dtype, pitch))
+    sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
+    for _ in range(3):
+        ca = torch.empty((B, 6), dtype=torch.float64, device=DEV)
+        fa = torch.empty((B, 6), dtype=torch.float32, device=DEV)
+        ta = torch.empty((B, N), dtype=ctype, device=DEV)
+        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur_a), 0, B,
+                                    _lib.ptr(ca), _lib.ptr(fa), B, T, N, M, 7, _lib.SCHEME_LOG_EULER | _lib.MATH_HW,
+                                    _lib.NORM_NORMALIZE, dtype, store, _lib.ptr(paths), pitch, chunk, _lib.ptr(ta),
+                                    _lib.ptr(sync), nsync, None))
+        tb = torch.empty_like(ta)
+        _lib.check(L.smc_train_targets(_lib.ptr(ca), B, T, N, M, 7, _lib.ptr(cur_b[1:2]), 0,
+                                       _lib.SCHEME_LOG_EULER | _lib.MATH_HW, _lib.NORM_NORMALIZE, dtype, store,
+                                       _lib.ptr(paths), pitch, chunk, None, _lib.ptr(tb), None, 0, None))
+        cur_b.add_(B)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(ta.cpu().numpy(), tb.cpu().numpy())
+        assert cur_a.tolist() == cur_b.tolist()
+        assert not sync.view(torch.int32).any()
+
+
 SLICED_CASES = [  # (B, N, M, store, chunk): shapes with P > 65,536 (W = P / 65,536 slices)
     (None, 1024, 256, _lib.STORE_ALL, None),   # C3 per-contract shape, W = 4, > 1 contract per group
     (70, 1024, 256, _lib.STORE_ALL, 24),       # C3 shape in three chunk launches

@@ -79,6 +79,15 @@ for step in "$@"; do
     kstep:*)  # kstep:<config>[:extra args with , for spaces]
       IFS=: read -r _ cfg extra <<< "$step"
       run "kstep_${cfg}" 300 python tools/kprof_step.py --config "$cfg" ${extra//,/ } ;;
+    pmcf64:*)  # pmcf64:<counters with , for spaces> -> PMC pass over the f64 C2 MC launch
+      IFS=: read -r _ ctrs <<< "$step"; tag=$(echo "$ctrs" | tr ',' '_' | cut -c1-40)
+      cd /tmp && run "pmcf64_$tag" 300 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } -d "$OUT/pmcf64_$tag" -o run --output-format csv -- python "$ROOT/tools/kprof_step.py" --config c2 --dtype f64 --iters 3; cd "$ROOT" ;;
+    benchx:*)  # benchx:<tag>:<bench args with , for spaces> (no CPU leg)
+      IFS=: read -r _ tag args <<< "$step"
+      run "benchx_$tag" 600 python bench.py --no-cpu-baseline ${args//,/ } ;;
+    testk:*)  # testk:<pytest -k expression with , for spaces>
+      IFS=: read -r _ expr <<< "$step"
+      run testk 600 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -rf -k "${expr//,/ }" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
