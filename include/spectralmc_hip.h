@@ -176,8 +176,9 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
                        int64_t path_pitch, int64_t chunk_contracts, void* targets_dev, void* sync_dev,
                        int64_t sync_bytes, void* stream);
 /* Bytes of smc_train_step's sync area for this shape on the current device (128 for whole-contract
- * shapes: a done counter, the status word and the contract queue of the dynamically handed-out last
- * quarter of the rounds; -1 if the device query fails). */
+ * shapes: a done counter, the status word and the contract queue: the resident kernel's dynamically
+ * handed-out last quarter of the rounds, rows_kernel's contracts after each workgroup's first; -1 if
+ * the device query fails). */
 int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
                                   int32_t dtype, int64_t path_pitch);
 /* Name of the kernel smc_train_step launches for this shape ("resident_kernel",
