@@ -666,7 +666,10 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
 #ifndef SMC_LGEMM_K
 #define SMC_LGEMM_K 64
 #endif
-constexpr int kLM = 128, kLN = 64, kLK = SMC_LGEMM_K, kLLd = kLK + 4;  // tile (features x batch rows), K stage, LDS stride
+#ifndef SMC_LGEMM_M
+#define SMC_LGEMM_M 128
+#endif
+constexpr int kLM = SMC_LGEMM_M, kLN = 64, kLK = SMC_LGEMM_K, kLLd = kLK + 4;  // tile (features x batch rows), K stage, LDS stride
 constexpr int kLThreads = 256;                                // 4 waves x (32 features x 64 rows)
 constexpr int kLTM = kLM / 4 / 16, kLTN = kLN / 16;           // 16 x 16 tiles per wave
 enum { kLFwd = 0, kLLast = 1, kLBwd = 2 };
