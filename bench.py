@@ -355,7 +355,7 @@ def main() -> None:
                   "valu": "forward_backward + reduce/Adam + finalize (csrc/cvnn.hip), VALU "
                           + ("f64" if f64 else "f32")}[kern]
         if layered:
-            desc_k = ("lpack + one lgemm_kernel per layer and direction (v_mfma_f32_16x16x4_f32, 128x64 tiles, "
+            desc_k = ("lpack + one lgemm_kernel per layer and direction (v_mfma_f32_16x16x4_f32, 64x64 tiles, "
                       "fused epilogues) + wgrad + reduce/Adam + finalize (csrc/cvnn_mfma.hip)")
         network = {"kernels": desc_k, "compute": kern, "flops_per_step": flops, "ms": net_ms,
                    "achieved": flops / (net_ms * 1e-3) / 1e12, "peak": peak, "unit": "TFLOP/s",
