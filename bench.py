@@ -78,7 +78,7 @@ def parse() -> argparse.Namespace:
                     help="MC part of step s+1 on its own stream beside step s's network part (pricer.overlap_mc)")
     ap.add_argument("--priority", default="network", choices=["network", "mc", "none"],
                     help="stream with the high queue priority (pricer.high_priority_stream)")
-    ap.add_argument("--lanes", type=int, default=2, help="MC lanes (pricer.mc_lanes): consecutive path launches "
+    ap.add_argument("--lanes", type=int, default=2, choices=[1, 2, 4], help="MC lanes (pricer.mc_lanes): consecutive path launches "
                     "on alternating streams, each starting in the previous one's tail")
     ap.add_argument("--net-cus", type=int, default=32, help="CUs reserved for the network (pricer.network_cus)")
     ap.add_argument("--net-cu-pattern", default="low", choices=["spread", "low"])

@@ -78,10 +78,13 @@ const char* smc_last_error_string(void);
 /* Launches whose workgroups exchange sums (the sliced resident kernel, the resident basket kernel)
  * poll for their partners a bounded time (~1 s).  A partner that never arrives (e.g. the group's
  * workgroups were not all co-resident) sets SMC_SYNC_EXCHANGE_TIMEOUT in the 32-bit status word at
- * byte SMC_SYNC_STATUS_OFFSET of the sync area; the launch still completes (every later wait of the
- * launch gives up at once) with NaN targets for the contracts it could not finish.  The word is
+ * byte SMC_SYNC_STATUS_OFFSET of the sync area and the launch's own failure flag (byte
+ * SMC_SYNC_LAUNCH_FAIL_OFFSET); the launch still completes (every later wait of THAT launch sees its
+ * flag and gives up at once) with NaN targets for the contracts it could not finish.  The last
+ * workgroup of the launch clears the flag, so the next launch waits normally; the status word is
  * sticky across launches: the caller reads (and clears) it with smc_sync_status. */
 #define SMC_SYNC_STATUS_OFFSET     32
+#define SMC_SYNC_LAUNCH_FAIL_OFFSET 48
 #define SMC_SYNC_EXCHANGE_TIMEOUT  1u
 /* Waits for `stream`, then copies the status word of sync_dev to *status_out (0: no failure) and,
  * if clear != 0, zeroes it.  The only call of this ABI that synchronises the host. */

@@ -204,6 +204,11 @@ class BasketEngine:
         self.kernel_name = _lib.lib().smc_basket_train_targets_kernel(
             self.A, self.T, self.N, self.M, 1 if self._sync is not None else 0, 1).decode()
 
+    @property
+    def exchanges(self) -> bool:
+        """The step's path launch has workgroups that wait for each other (the resident basket kernel)."""
+        return self.kernel_name == "basket_resident_kernel"
+
     def check_status(self, stream: torch.cuda.Stream | None = None) -> None:
         """SmcError(SMC_ERR_EXCHANGE_TIMEOUT) if a resident launch gave up on a partner slice since the
         last check (engine.check_sync_status)."""

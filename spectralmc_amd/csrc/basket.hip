@@ -334,7 +334,8 @@ constexpr int kRSlots = 4;                   // slice-sum slots (contract j mod 
 constexpr int kRTable = 64;                  // contracts per coefficient table (one per wave-0 lane)
 
 // Sync area of the resident basket launch (bytes): [0, 128) done counter (+0), the sticky status
-// word (+SMC_SYNC_STATUS_OFFSET) and contract queue (+64); per group a 128-B line of slice-sum arrivals; slice sums [groups][4][W A + 1] f64 (the
+// word (+SMC_SYNC_STATUS_OFFSET), the launch's failure flag (+SMC_SYNC_LAUNCH_FAIL_OFFSET) and contract
+// queue (+64); per group a 128-B line of slice-sum arrivals; slice sums [groups][4][W A + 1] f64 (the
 // last entry: the contract of the group's iteration j + 2, dynamic tail); column sums [chunk][W][N].
 struct BasketSyncLayout {
   int64_t groups, xsum_off, xcol_off, bytes;
@@ -367,10 +368,6 @@ struct BasketResArgs {
   uint32_t spin_limit;    // polls of an exchange before it gives up (status word, NaN targets)
   int32_t withhold;       // smc_test_exchange_fault: slice W-1 of group 0 skips its first arrival
 };
-
-#if defined(SMC_EXPERIMENT_TRACE)  // tools/micro decomposition builds only: per-workgroup start/end + XCD
-__device__ uint64_t g_btrace[1024 * 4];
-#endif
 
 template <int A, bool HW, bool STORE_ALL>
 __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArgs ra) {
@@ -423,6 +420,7 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
   const int64_t n_static = dyn ? S * groups : a.B;
   uint32_t* queue = reinterpret_cast<uint32_t*>(ra.sync + 64);
   uint32_t* status = reinterpret_cast<uint32_t*>(ra.sync + SMC_SYNC_STATUS_OFFSET);
+  uint32_t* launch_fail = reinterpret_cast<uint32_t*>(ra.sync + SMC_SYNC_LAUNCH_FAIL_OFFSET);
   auto bof = [&](int64_t jj) -> int64_t { return !dyn || jj < S ? grp + jj * groups : bidx[jj & 3]; };
   auto coefs = [&](int64_t bb, float* e) {  // simulation coefficients of contract bb (f64 Cholesky, rounded once)
     const double* c = a.contracts + bb * width;
@@ -442,15 +440,6 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
       for (int k = 0; k < A; ++k) e[2 * A + i * A + k] = k <= i ? static_cast<float>(bi * L[i * kMaxAssets + k]) : 0.0f;
     }
   };
-#if defined(SMC_EXPERIMENT_TRACE)
-  if (tid == 0 && blockIdx.x < 1024) {
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_btrace[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
-    g_btrace[blockIdx.x * 4 + 1] = xcc;
-    g_btrace[blockIdx.x * 4 + 2] = static_cast<uint64_t>(grp);
-  }
-#endif
 
   // step 0 (wave 0): the payoff constants of contract jj from every slice's terminal sums
   auto gather = [&](int64_t jj) {
@@ -458,13 +447,16 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
     const double* c = a.contracts + b * width;
     const double* xs = xsum + (jj % kRSlots) * XS;
     const uint32_t want = static_cast<uint32_t>(W) * static_cast<uint32_t>(jj + 1);
-    // bounded poll; once any exchange of the launch has failed (status word set) the others stop
+    // bounded poll; once any exchange of this launch has failed (its flag set) the others stop
     // waiting at once, so a failed launch still drains in about one poll budget
     uint32_t spins = 0;
     bool ok;
-    while (!(ok = get_sc1(cnt) >= want) && get_sc1(status) == 0u && ++spins < ra.spin_limit)
+    while (!(ok = get_sc1(cnt) >= want) && get_sc1(launch_fail) == 0u && ++spins < ra.spin_limit)
       __builtin_amdgcn_s_sleep(2);
-    if (!ok && lane == 0) __hip_atomic_fetch_or(status, SMC_SYNC_EXCHANGE_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!ok && lane == 0) {
+      __hip_atomic_fetch_or(status, SMC_SYNC_EXCHANGE_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(launch_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // the W x A slice sums in one round of loads across the wave (<= 4 per lane), parked in part[]
     // (free until the payoff), then lanes 0..A-1 add their asset's W sums in slice order
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -603,9 +595,6 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
       if (lane == 0) wsum[wave * A + i] = w;
     }
     lds_barrier();  // wsum of contract jj, scales of contract jj - 1
-#if defined(SMC_BASKET_RES_NO_EXCHANGE)  // tools/micro decomposition builds only: simulation alone
-    continue;
-#endif
     // 2. contract jj - 1: payoffs and column sums (reads the terminal slots: own lane)
     if (jj > 0) payoff(jj - 1);
 #pragma unroll
@@ -625,16 +614,11 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
     }
     lds_barrier();  // part / wsum are rewritten from here on
   }
-#if !defined(SMC_BASKET_RES_NO_EXCHANGE)
   if (n_iter > 0) {  // the last contract
     if (wave == 0) gather(n_iter - 1);
     lds_barrier();
     payoff(n_iter - 1);
   }
-#endif
-#if defined(SMC_EXPERIMENT_TRACE)
-  if (tid == 0 && blockIdx.x < 1024) g_btrace[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
-#endif
   if (tid == 0) {
     // every workgroup made its last exchange before it arrives here: the last one resets the
     // group counters for the next launch
@@ -643,6 +627,7 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
     if (atomicAdd(done, 1u) == gridDim.x - 1) {
       for (int k = 0; k < groups; ++k) reinterpret_cast<uint32_t*>(ra.sync + 128 + 128 * static_cast<int64_t>(k))[0] = 0u;
       *queue = 0u;
+      *launch_fail = 0u;
       *done = 0u;
     }
   }
@@ -838,13 +823,6 @@ using namespace smc;
 
 extern "C" {
 #pragma GCC visibility push(default)
-#if defined(SMC_EXPERIMENT_TRACE)
-int32_t smc_debug_btrace(uint64_t* host, int64_t n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(smc::g_btrace), static_cast<size_t>(n) * sizeof(uint64_t)) == hipSuccess
-             ? 0 : 1;
-}
-#endif
-
 int32_t smc_basket_train_targets(const double* contracts_dev, int64_t n_contracts, int32_t n_assets,
                                  int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
                                  uint64_t mc_seed, const int64_t* ordinal_dev, int64_t ordinal0, int32_t math,

@@ -110,10 +110,12 @@ struct EngineArgs {
   // share of the contract rounds assigned statically, in quarters (the rest from res_queue); 0 with
   // SMC_TRAIN_DYNAMIC: every contract from the queue
   int32_t res_static_q = 3;
-  // sliced resident_kernel: the sync area's sticky status word (SMC_SYNC_STATUS_OFFSET), the poll
-  // budget of an exchange and the smc_test_exchange_fault hook (withhold: slice W-1 of group 0 skips
-  // its first terminal-sum arrival)
+  // sliced resident_kernel: the sync area's sticky status word (SMC_SYNC_STATUS_OFFSET), this launch's
+  // failure flag (SMC_SYNC_LAUNCH_FAIL_OFFSET, cleared by the last workgroup), the poll budget of an
+  // exchange and the smc_test_exchange_fault hook (withhold: slice W-1 of group 0 skips its first
+  // terminal-sum arrival)
   uint32_t* status;
+  uint32_t* launch_fail;
   uint32_t spin_limit;
   int32_t withhold;
 };
@@ -260,11 +262,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
         char* row = reinterpret_cast<char*>(chunk_base + (store_all ? static_cast<int64_t>(t) * pitch : 0));
         // the terminal row is read back by the CF phase (maybe another workgroup's): write-through
         const bool handoff = last && (STRAIGHT || a.targets != nullptr);
-#if defined(SMC_EXPERIMENT_FLAT_STORES)  // tools/micro A/B builds only: 64-bit VALU row addresses
-        if constexpr (false) {
-#else
         if constexpr (STRAIGHT && !MASKED && sizeof(Real) == 4) {
-#endif
           // one buffer descriptor on the contract base; the row offset goes in soffset (SALU adds), so
           // a row store costs no 64-bit VALU address add
           typedef float v4f __attribute__((ext_vector_type(4)));
@@ -611,10 +609,8 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
     avg[n] = tot / static_cast<double>(M);
   }
   __syncthreads();
-#if !defined(SMC_CF_NO_DFT)  // tools/micro decomposition builds only
   if (use_fft(N)) fft_row<Real, kThreads>(avg, cs, sn, N, part, part + N, static_cast<C2*>(a.targets) + b * N);
   else dft_row<Real>(avg, cs, sn, N, static_cast<C2*>(a.targets) + b * N);
-#endif
 }
 
 // Slice k of contract b (paths [k S, (k+1) S), S = kSliceChunks * kChunk; the whole contract
@@ -667,11 +663,7 @@ __device__ void run_slice(const EngineArgs& a, int64_t b, int k, double* lds, in
     terminal_sum = a.rowsum[b * T + (T - 1)];
   }
   if (!ALLROWS && a.rowsum && threadIdx.x == 0 && a.simulate) a.rowsum[b * T + (T - 1)] = terminal_sum;
-#if defined(SMC_EXPERIMENT_NO_CF)  // tools/micro decomposition builds only
-  if (false) {
-#else
   if (a.targets) {
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's own terminal-row stores
     __syncthreads();
     cf_targets_contract<Real>(a, c, b, terminal_sum, lds_work);
@@ -869,32 +861,6 @@ size_t resident_lds_bytes(int N) {
          (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 9 + 6 * kResPreDraw) * sizeof(double);
 }
 
-#if defined(SMC_EXPERIMENT_TRACE)  // tools/micro decomposition builds only: per-workgroup timestamps
-constexpr int kTraceStride = 40;
-__device__ uint64_t g_trace[1024 * kTraceStride];
-#define SMC_TRACE(slot)                                                                         \
-  do {                                                                                          \
-    if (threadIdx.x == 0 && blockIdx.x < 1024) g_trace[blockIdx.x * kTraceStride + (slot)] =    \
-        __builtin_amdgcn_s_memrealtime();                                                       \
-  } while (0)
-#else
-#define SMC_TRACE(slot) do {} while (0)
-#endif
-// SMC_EXPERIMENT_TRACE_CF (with SMC_EXPERIMENT_TRACE): the CF phase's sub-steps of rounds 0..5 at
-// slots 2 + 6 r + k instead (k = 0 simulation done, 1 column sums in LDS, 2 M-mean done, 3 FFT done)
-#if defined(SMC_EXPERIMENT_TRACE_CF)
-#define SMC_TRACE_R(k, slot2) \
-  do {                        \
-    if (round < 6) SMC_TRACE(2 + 6 * round + (k)); \
-  } while (0)
-#else
-#define SMC_TRACE_R(k, slot2) \
-  do {                        \
-    if ((k) == 0 || (k) == 3) \
-      if (round < 18) SMC_TRACE(slot2); \
-  } while (0)
-#endif
-
 template <bool LOG_EULER, bool HW, bool STORE_ALL, bool T16>
 __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   typedef float v4f __attribute__((ext_vector_type(4)));
@@ -931,17 +897,6 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
                                           // the exchanged terminal sum, [7] the last-arriver flag,
                                           // [8] the next dynamically handed-out contract;
   double* pre = row + 9;                  // [kResPreDraw][6] Sobol rows of the first static contracts
-  SMC_TRACE(0);
-#if defined(SMC_EXPERIMENT_TRACE_CF)  // core-clock counter at start / end: the workgroup's mean clock
-  if (tid == 0 && blockIdx.x < 1024) g_trace[blockIdx.x * kTraceStride + 36] = __builtin_amdgcn_s_memtime();
-#endif
-#if defined(SMC_EXPERIMENT_TRACE)
-  if (tid == 0 && blockIdx.x < 1024) {
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_trace[blockIdx.x * kTraceStride + 1] = xcc;
-  }
-#endif
   for (int j = tid; j < N; j += kResThreads) math::twiddle(j, N, sn[j], cs[j]);
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
   const int64_t sob0 = a.sobol ? a.cursor[0] + a.sobol_index0 : 0;
@@ -1037,11 +992,6 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     const double w = wave_sum(acc[0]);
     if (lane == 0) wsum[wave] = w;
     lds_barrier();
-    SMC_TRACE_R(0, 2 + 2 * round);  // simulation of this contract done
-#if defined(SMC_RESIDENT_NO_CF)  // tools/micro decomposition builds only: no payoff / M-mean / FFT
-    lds_barrier();
-    continue;
-#endif
     // LDS reads batched ahead of the in-order sums (the CF phase is a chain of LDS round trips)
     double tot = 0.0;
     {
@@ -1066,13 +1016,16 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
         if (!(a.withhold && grp == 0 && slc == W - 1 && round == 0))
           __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t want = static_cast<uint32_t>(W) * (round + 1);
-        // bounded poll; once any exchange of the launch has failed (status word set) the others
-        // stop waiting at once, so a failed launch still drains in about one poll budget
+        // bounded poll; once any exchange of this launch has failed (its flag set) the others stop
+        // waiting at once, so a failed launch still drains in about one poll budget
         uint32_t spins = 0;
         bool ok;
-        while (!(ok = get_sc1(cnt) >= want) && get_sc1(a.status) == 0u && ++spins < a.spin_limit)
+        while (!(ok = get_sc1(cnt) >= want) && get_sc1(a.launch_fail) == 0u && ++spins < a.spin_limit)
           __builtin_amdgcn_s_sleep(2);
-        if (!ok) __hip_atomic_fetch_or(a.status, SMC_SYNC_EXCHANGE_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!ok) {
+          __hip_atomic_fetch_or(a.status, SMC_SYNC_EXCHANGE_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.launch_fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         const double t = ordered_sum_wt(a.res_xsum + xslot, 0, W, 1);  // slices in order
         row[6] = ok ? t : __builtin_nan("");
         if (dyn && b + groups >= n_static)
@@ -1107,7 +1060,6 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
 #pragma unroll
     for (int j = 0; j < kPathsPerLane; ++j) part[g * N + 4 * q + j] = colsum[j];
     lds_barrier();
-    SMC_TRACE_R(1, 0);
     if (W == 1) {
       for (int n = tid; n < N; n += kResThreads) {
         const double t = group_sum(part, n, G, N);
@@ -1136,15 +1088,9 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       for (int n = tid; n < N; n += kResThreads) avg[n] = ordered_sum_wt(xcol, n, W, N) / static_cast<double>(M);
     }
     lds_barrier();
-    SMC_TRACE_R(2, 0);
     fft_row<float, kResThreads, true>(avg, cs, sn, N, part, part + N, static_cast<float2*>(a.targets) + b * N);
     lds_barrier();  // part (= term_lds) / avg / wsum / row are reused by the next contract
-    SMC_TRACE_R(3, 3 + 2 * round);  // CF of this contract done
   }
-  SMC_TRACE(39);
-#if defined(SMC_EXPERIMENT_TRACE_CF)
-  if (tid == 0 && blockIdx.x < 1024) g_trace[blockIdx.x * kTraceStride + 37] = __builtin_amdgcn_s_memtime();
-#endif
   if (a.done && tid == 0) {
     // every workgroup read the cursor (and made its last exchange) before it arrives here: the last
     // one advances the cursor and resets the exchange counters
@@ -1153,11 +1099,13 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       a.cursor[0] += a.advance;
       a.cursor[1] += a.advance;
       if (a.res_queue) *a.res_queue = 0u;
-      if (W > 1)
+      if (W > 1) {
         for (int k = 0; k < groups; ++k) {
           a.res_cnt[static_cast<int64_t>(k) * 64] = 0u;
           a.res_cnt[static_cast<int64_t>(k) * 64 + 32] = 0u;
         }
+        *a.launch_fail = 0u;
+      }
       *a.done = 0u;
     }
   }
@@ -1180,14 +1128,15 @@ int32_t resident_slices(int64_t P) {
 }
 
 // smc_train_step sync area: [0, 128) the done counter (+0), the sticky status word
-// (+SMC_SYNC_STATUS_OFFSET) and the contract queue (+64); then per
+// (+SMC_SYNC_STATUS_OFFSET), the launch's failure flag (+SMC_SYNC_LAUNCH_FAIL_OFFSET) and the contract
+// queue (+64); then per
 // group a 256-B record of two 128-B counter lines; then the slice terminal sums + next contract
 // [groups][2][W + 1] and column sums [groups][2][W][N].
 // groups <= 2 #CUs / W (the resident kernel fits one workgroup per CU; twice that for margin).
 struct ResSyncLayout {
   int64_t groups, xsum_off, xcol_off, bytes;
 };
-constexpr int64_t kStepSyncBytes = 128;  // whole contracts: done counter (+0), status (+32), contract queue (+64)
+constexpr int64_t kStepSyncBytes = 128;  // done counter (+0), status (+32), launch failure flag (+48), queue (+64)
 ResSyncLayout res_sync_layout(int32_t W, int32_t N, int cus) {
   ResSyncLayout l{};
   if (W <= 1) {
@@ -1455,6 +1404,7 @@ int32_t launch_rows_k(const EngineArgs& a, hipStream_t stream) {
   const size_t lds1 = 2 * kWaves * sizeof(double), lds2 = lds_bytes(a.T, a.N, true);
   auto k1 = rows_kernel<Real, LOG_EULER, HW, STORE_ALL>;
   auto k2 = cf_kernel<Real>;
+  if (lds2 > kMaxLds) return fail(SMC_ERR_INVALID_SHAPE, "engine: network_size exceeds the LDS budget");
   if (lds2 > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(k2),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                static_cast<int>(lds2)) != hipSuccess) {
@@ -1573,7 +1523,9 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
     return fail(SMC_ERR_INVALID_SHAPE, "engine: more than 2^31-1 workgroups in one launch");
   const bool cf = a.targets != nullptr;
   const size_t lds = lds_bytes(a.T, a.N, cf);
-  if (lds > kMaxLds) return fail(SMC_ERR_INVALID_SHAPE, "engine: timesteps/network_size exceed the LDS budget");
+  // f64 kernels also hold the static table image of the path math (math::F64Tables)
+  if (lds + (sizeof(Real) == 8 ? sizeof(math::F64Tables) : 0) > kMaxLds)
+    return fail(SMC_ERR_INVALID_SHAPE, "engine: timesteps/network_size exceed the LDS budget");
   const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
   const bool hw = (a.scheme & SMC_MATH_HW) != 0 && sizeof(Real) == 4;
   const bool allrows = a.all_rows != 0;
@@ -1627,17 +1579,6 @@ int32_t validate_common(const double* contracts, int64_t B, int32_t T, int64_t P
 using namespace smc;
 
 extern "C" {
-#if defined(SMC_EXPERIMENT_TRACE)
-// n < 0: zero the trace (before the launch to be traced), else copy its first n words to host
-__attribute__((visibility("default"))) int32_t smc_debug_trace(uint64_t* host, int64_t n) {
-  if (n < 0) {
-    static uint64_t zeros[1024 * kTraceStride];
-    return hipMemcpyToSymbol(HIP_SYMBOL(smc::g_trace), zeros, sizeof(zeros)) == hipSuccess ? 0 : 1;
-  }
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(smc::g_trace), static_cast<size_t>(n) * sizeof(uint64_t)) == hipSuccess
-             ? 0 : 1;
-}
-#endif
 #pragma GCC visibility push(default)
 
 int32_t smc_gbm_simulate(const double* contracts_dev, int64_t n_contracts, int32_t timesteps, int64_t n_paths,
@@ -1783,6 +1724,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   char* sync = static_cast<char*>(sync_dev);
   a.done = reinterpret_cast<uint32_t*>(sync);
   a.status = reinterpret_cast<uint32_t*>(sync + SMC_SYNC_STATUS_OFFSET);
+  a.launch_fail = reinterpret_cast<uint32_t*>(sync + SMC_SYNC_LAUNCH_FAIL_OFFSET);
   a.res_queue = reinterpret_cast<uint32_t*>(sync + 64);
   a.res_static_q = dynamic ? 0 : 3;
   a.spin_limit = exchange_spin_limit();

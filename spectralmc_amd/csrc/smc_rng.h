@@ -92,16 +92,6 @@ struct PathStream {
   //   2 alignbit + 1 sub + 4 transcendentals + 2 mul per pair.
   template <bool HW>
   __device__ __forceinline__ void normal_pair(float& z0, float& z1) {
-#if defined(SMC_EXPERIMENT_ZERO_NORMALS)  // tools/micro decomposition builds only
-    z0 = 0.0f;
-    z1 = 0.0f;
-    return;
-#elif defined(SMC_EXPERIMENT_NO_TRANSCENDENTALS)
-    const uint32_t ea = next(), eb = next();
-    z0 = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ea, 9)) - 1.5f;
-    z1 = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, eb, 9)) - 1.5f;
-    return;
-#endif
     const uint32_t a = next(), b = next();
     const float u1 = 2.0f - __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, a, 9));
     if constexpr (HW) {
@@ -126,22 +116,12 @@ struct PathStream {
     float r[4], c[4], sn[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-#if defined(SMC_EXPERIMENT_ZERO_NORMALS)  // tools/micro decomposition builds only
-      r[j] = 0.0f;
-      c[j] = sn[j] = 1.0f;
-#elif defined(SMC_EXPERIMENT_NO_TRANSCENDENTALS)
-      const uint32_t ea = next(), eb = next();
-      r[j] = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ea, 9)) - 1.5f;
-      c[j] = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, eb, 9)) - 1.5f;
-      sn[j] = c[j] * 0.5f;
-#else
       const uint32_t ua = next(), ub = next();
       const float u1 = 2.0f - __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ua, 9));
       r[j] = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u1));
       const float w = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ub, 9));
       c[j] = __builtin_amdgcn_cosf(w);
       sn[j] = __builtin_amdgcn_sinf(w);
-#endif
     }
     const f2 bb = {b, b}, aa = {a, a};
 #pragma unroll

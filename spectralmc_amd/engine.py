@@ -155,6 +155,11 @@ class TrainingEngine:
             self._sync_bytes = sync
         self._sync = self._syncs[0]
 
+    @property
+    def exchanges(self) -> bool:
+        """The step's path launch has workgroups that wait for each other (sliced resident kernel)."""
+        return self.kernel_name == "resident_kernel(sliced)"
+
     def check_status(self, stream: torch.cuda.Stream | None = None) -> None:
         """Raise SmcError(SMC_ERR_EXCHANGE_TIMEOUT) if a launch since the last check gave up waiting
         for a partner workgroup (its targets hold NaN); clears the sticky status word.  Waits for

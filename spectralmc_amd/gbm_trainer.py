@@ -26,6 +26,7 @@ from __future__ import annotations
 import asyncio
 import math
 import time
+import weakref
 import warnings
 from dataclasses import dataclass
 from typing import Callable, Iterable, Literal, Protocol, Sequence, runtime_checkable
@@ -280,7 +281,11 @@ class _StepProgram:
     # -- pieces -------------------------------------------------------------------------
     def mc(self, slot: int) -> None:
         out = self.slots[slot] if self.direct else None
-        if getattr(self.engine, "lanes", 1) > 1:  # slot k's step runs on lane k % lanes (steps take the lanes in turn)
+        lanes = getattr(self.engine, "lanes", 1)
+        if lanes > 1:
+            # slot k's step runs on lane k % lanes; steps take the lanes in turn because lanes divides
+            # SLOTS (GbmCVNNPricer.open_session rejects other values)
+            assert self.SLOTS % lanes == 0
             self.engine.enqueue_step(out, lane=slot)
         else:
             self.engine.enqueue_step(out)
@@ -423,6 +428,12 @@ class GbmCVNNPricer:
     #: best; "spread": evenly over the id range)
     network_cus: int = 32
     network_cu_pattern: str = "low"
+    #: launches whose workgroups wait for each other (the sliced resident kernel, C3; the resident
+    #: basket kernel, C5) need every workgroup of a group co-resident.  A collective that spins on a
+    #: few CUs while it waits for a slow peer (RCCL in data-parallel runs) can hold those CUs past the
+    #: exchange's poll budget, so such a launch is enqueued only after the previous step's network part
+    #: (and its all-reduce) has completed.  None: in data-parallel runs; True / False: always / never
+    exchange_after_network: bool | None = None
     #: network forward/backward/Adam on the fused HIP kernels (csrc/cvnn.hip) when the CVNN is a
     #: ComplexLinear + modReLU/zReLU chain; False (or other architectures): torch-ROCm modules
     fused_network: bool = True
@@ -562,6 +573,12 @@ class GbmCVNNPricer:
         """Set up a device training session (engine buffers, Adam, step program) for ``config``."""
         if isinstance(self._sampler_result, Failure):
             return Failure(SamplerInitFailed(error=self._sampler_result.error))
+        lanes = self.mc_lanes if self.overlap_mc else 1
+        if not isinstance(lanes, int) or lanes < 1 or _StepProgram.SLOTS % lanes:
+            # a lane's device cursor assumes it runs every lanes-th step; the step slots (whose graphs
+            # bind a lane) cycle mod SLOTS, so lanes must divide SLOTS
+            return Failure(InvalidTrainerConfig(
+                message=f"mc_lanes must divide {_StepProgram.SLOTS} (1, 2 or 4), got {lanes!r}"))
         adam_res = self._make_adam(config.learning_rate)
         if isinstance(adam_res, Failure):
             return adam_res
@@ -826,6 +843,13 @@ class TrainingSession:
         self._mc_pending = False             # the MC part of the next step is already enqueued
         self.mc_events: list[tuple[torch.cuda.Event, torch.cuda.Event]] | None = None
         self._closed = False
+        # exchanging path launches wait for the previous step's network part (pricer.exchange_after_network)
+        order = pricer.exchange_after_network
+        self._mc_after_nn = bool(getattr(self.engine, "exchanges", False) and
+                                 (order if order is not None else ctx is not None))
+        # a session that is never closed still destroys its masked streams (after a device sync: the
+        # streams may hold queued work when the session is collected)
+        self._finalizer = weakref.finalize(self, _finalize_streams, self._hip_streams, dev)
 
     def step(self, prefetch_next: bool = True) -> Result[int, TrainerError]:
         """Enqueue one training step.  With ``prefetch_next`` (and ``pricer.overlap_mc``) the MC
@@ -859,8 +883,9 @@ class TrainingSession:
             prog.handoff(slot)
             self._mc_done[slot].record(ms)
             self._mc_pending = False
-        if prefetch_next and self.sobol_skip + 2 * self.global_batch <= MAX_POINTS:
-            nxt = (self.steps + 1) % K
+        prefetch = prefetch_next and self.sobol_skip + 2 * self.global_batch <= MAX_POINTS
+        nxt = (self.steps + 1) % K
+        if prefetch and not self._mc_after_nn:
             with torch.cuda.stream(self._lane_stream(nxt)):
                 self._enqueue_mc(nxt)
             self._mc_pending = True
@@ -869,6 +894,13 @@ class TrainingSession:
             prog.run_nn(slot)
             self._nn_done[slot].record(self.stream)
             self._slot_used[slot] = True
+        if prefetch and self._mc_after_nn:
+            # an exchanging launch never shares the chip with this step's all-reduce
+            ns = self._lane_stream(nxt)
+            with torch.cuda.stream(ns):
+                ns.wait_event(self._nn_done[slot])
+                self._enqueue_mc(nxt)
+            self._mc_pending = True
         self.steps += 1
         self.sobol_skip += self.global_batch
         self.global_step += 1
@@ -897,6 +929,8 @@ class TrainingSession:
     def sync(self) -> None:
         """Wait for the enqueued steps; raises SmcError (SMC_ERR_EXCHANGE_TIMEOUT) if an exchanging
         path launch gave up on a partner workgroup since the last check (its targets hold NaN)."""
+        if self._closed:
+            raise RuntimeError("session is closed")
         self.stream.synchronize()
         for ms in self.mc_streams:
             ms.synchronize()
@@ -905,6 +939,8 @@ class TrainingSession:
             check(self.mc_stream)
 
     def read_metrics(self) -> tuple[float, float]:
+        if self._closed:
+            raise RuntimeError("session is closed")
         self.sync()
         return float(self.program.loss), float(self.program.grad_norm)
 
@@ -929,8 +965,15 @@ class TrainingSession:
             if check is not None:  # after the bookkeeping: the session is closed either way
                 check(torch.cuda.current_stream(dev))  # every stream of the session is idle by now
         finally:
-            _destroy_streams(self._hip_streams)
+            self._release_streams()
         return _BatchState(self.sobol_skip, self.global_step, loss, gn)
+
+    def _release_streams(self) -> None:
+        """Destroy the CU-masked streams and drop every reference to them (the torch wrappers)."""
+        self._finalizer.detach()
+        self.stream = self.mc_stream = None
+        self.mc_streams = []
+        _destroy_streams(self._hip_streams)
 
 
     def close_quietly(self) -> None:
@@ -941,7 +984,7 @@ class TrainingSession:
         self.stream.synchronize()
         for ms in self.mc_streams:
             ms.synchronize()
-        _destroy_streams(self._hip_streams)
+        self._release_streams()
         for p in self.params:
             if p.grad is not None:
                 p.grad = p.grad.clone()
@@ -985,6 +1028,12 @@ def _masked_stream(dev: torch.device, mask: list[int], owned: list[int]) -> torc
             raise RuntimeError("hipExtStreamCreateWithCUMask failed")
     owned.append(handle.value)
     return torch.cuda.ExternalStream(handle.value, device=dev)
+
+
+def _finalize_streams(owned: list[int], dev: torch.device) -> None:
+    if owned:
+        torch.cuda.synchronize(dev)
+        _destroy_streams(owned)
 
 
 def _destroy_streams(owned: list[int]) -> None:

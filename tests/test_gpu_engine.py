@@ -573,8 +573,8 @@ def test_sliced_train_step_bit_exact(oracle, golden, B, N, M, store, chunk) -> N
         # its exchanges wait for W arrivals per contract round from zero)
         words = sync.view(torch.int32).cpu().numpy()
         groups = -(-2 * torch.cuda.get_device_properties(0).multi_processor_count // W)  # sync-area capacity
-        # done counter, status word, contract queue and every group's two counter lines
-        assert words[0] == 0 and words[8] == 0 and words[16] == 0
+        # done counter, status word, launch failure flag, contract queue and every group's two counter lines
+        assert words[0] == 0 and words[8] == 0 and words[12] == 0 and words[16] == 0
         assert not words[32:32 + 64 * groups].any()
         contracts = c.cpu().numpy()
         got = t.cpu().numpy()
@@ -590,7 +590,9 @@ def test_exchange_timeout_sets_status_not_silent_nan(oracle, golden) -> None:
     """A sliced contract whose partner slice never arrives (test hook: slice W-1 of group 0 withholds
     its first arrival, 20,000-poll budget) ends the launch with NaN targets AND the sticky status word
     SMC_SYNC_EXCHANGE_TIMEOUT, which smc_sync_status reports (and clears) and TrainingEngine maps to
-    SmcError(SMC_ERR_EXCHANGE_TIMEOUT).  With the hook cleared the next step is bit-exact again."""
+    SmcError(SMC_ERR_EXCHANGE_TIMEOUT).  With the hook cleared the next step is bit-exact again, also
+    when it runs before anyone has read the status (the failure flag is per launch; only the status
+    word is sticky)."""
     from spectralmc_amd.engine import check_sync_status
 
     L = _L()
@@ -623,13 +625,18 @@ def test_exchange_timeout_sets_status_not_silent_nan(oracle, golden) -> None:
         _lib.check(L.smc_test_exchange_fault(0, 0))
     assert np.isnan(t[0].cpu().numpy()).all()  # group 0's first contract could not finish
     assert cur.tolist() == [B, B]                # the launch still completed and advanced the cursor
-    with pytest.raises(_lib.SmcError) as exc:
+    assert int(sync.view(torch.int32)[12]) == 0  # the launch's own failure flag is cleared at its end
+    wg, W = oracle.train_step_order(T, N, P)
+    # the next launch, status not yet read: waits normally, bit-exact
+    cur = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
+    c, t = step(cur)
+    kt, _ = oracle.kernel_targets(c.cpu().numpy(), T, N, M, seed=7, ordinal0=0, wg=wg, slices=W)
+    np.testing.assert_array_equal(t.cpu().numpy(), kt)
+    with pytest.raises(_lib.SmcError) as exc:  # the first launch's failure is still reported (sticky)
         check_sync_status(sync)
     assert exc.value.code == _lib.SMC_ERR_EXCHANGE_TIMEOUT
     assert _lib.sync_status(sync) == 0  # read-and-clear
     cur = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
     c, t = step(cur)
     check_sync_status(sync)
-    wg, W = oracle.train_step_order(T, N, P)
-    kt, _ = oracle.kernel_targets(c.cpu().numpy(), T, N, M, seed=7, ordinal0=0, wg=wg, slices=W)
     np.testing.assert_array_equal(t.cpu().numpy(), kt)

@@ -445,7 +445,8 @@ def test_batchnorm_residual_model_trains_on_torch_path(oracle) -> None:
     assert res.final_loss == pytest.approx(ref.loss, rel=1e-4)
 
 
-def test_mc_lanes_match_one_stream() -> None:
+@pytest.mark.parametrize("lanes", [2, 4])
+def test_mc_lanes_match_one_stream(lanes: int) -> None:
     """MC lanes (consecutive path launches on alternating streams, each with its own cursor, sync area
     and scratch; engine.py) give bit-identical training to the sequential one-stream program, eager
     and graph-replayed, on a shape the resident kernel takes (P = 4096, N | 4096)."""
@@ -463,9 +464,9 @@ def test_mc_lanes_match_one_stream() -> None:
     cfg = make_training_config(num_batches=9, batch_size=96)
     seq, m_s = pricer(False, 1)
     r_s = expect_success(seq.train(cfg))
-    lan, m_l = pricer(True, 2)
+    lan, m_l = pricer(True, lanes)
     sess = expect_success(lan.open_session(cfg))
-    assert sess.engine.lanes == 2 and len(sess.mc_streams) == 2
+    assert sess.engine.lanes == lanes and len(sess.mc_streams) == lanes
     for _ in range(9):
         expect_success(sess.step())
     st = sess.close()
@@ -474,6 +475,24 @@ def test_mc_lanes_match_one_stream() -> None:
     assert st.loss == r_s.final_loss and st.grad_norm == r_s.final_grad_norm
     for sync in sess.engine._syncs:  # every launch leaves its lane's counters zeroed
         assert int(sync.count_nonzero()) == 0
-    # lanes interleave the Sobol stream: lane k's cursor is k global batches past lane 0's
+    # lanes interleave the Sobol stream: after 9 steps + 1 prefetched (10 launches), lane k has run
+    # every lanes-th step and its cursor is the position of its next one
     cur = sess.engine.cursors.cpu().tolist()
-    assert cur[1][0] - cur[0][0] in (96, -96)
+    launched = [(10 - k + lanes - 1) // lanes for k in range(lanes)]
+    for k in range(lanes):
+        assert cur[k][0] == (k + lanes * launched[k]) * 96 and cur[k][1] == cur[k][0]
+    with pytest.raises(RuntimeError):
+        sess.read_metrics()  # closed sessions refuse to synchronise (streams released)
+
+
+def test_mc_lanes_must_divide_the_step_slots() -> None:
+    """A lane's cursor assumes it runs every lanes-th step, and the step slots cycle mod 4: lanes = 3
+    would draw other steps' contracts, so the session refuses it."""
+    sp = _sim()
+    model = make_test_cvnn(n_inputs=6, n_outputs=N, seed=5, dtype=torch.float32)
+    cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                               domain_bounds=make_domain_bounds())
+    p = expect_success(GbmCVNNPricer.create(cfg))
+    p.mc_lanes = 3
+    res = p.open_session(make_training_config(num_batches=2, batch_size=16))
+    assert isinstance(res, Failure) and "mc_lanes" in res.error.message
