@@ -327,17 +327,25 @@ static void normal_pair(mwc64x* g, int is_f64, double* z0, double* z1) {
   }
 }
 
-/* Normals of one group of 4 paths: z[t][j] for t < rows (f64 holder of dtype values). */
+/* Normals of one group of 4 paths: z[t][j] for t < rows (f64 holder of dtype values).  Step pairs
+ * (t, t + 1): one Box-Muller pair per path j; the last row of an odd count: two pairs, pair k -> paths
+ * 2k (z0) and 2k + 1 (z1) (smc_rng.h draw order, round 4). */
 static void group_normals(uint64_t seed, uint64_t ordinal, uint64_t group, int32_t rows, int is_f64, double* z) {
   mwc64x g;
   path_stream(seed, ordinal, group, &g);
-  for (int t = 0; t < rows; t += 2)
-    for (int j = 0; j < GROUP; ++j) {
-      double z0, z1;
-      normal_pair(&g, is_f64, &z0, &z1);
-      z[(int64_t)t * GROUP + j] = z0;
-      if (t + 1 < rows) z[(int64_t)(t + 1) * GROUP + j] = z1;
+  for (int t = 0; t < rows; t += 2) {
+    if (t + 1 < rows) {
+      for (int j = 0; j < GROUP; ++j) {
+        double z0, z1;
+        normal_pair(&g, is_f64, &z0, &z1);
+        z[(int64_t)t * GROUP + j] = z0;
+        z[(int64_t)(t + 1) * GROUP + j] = z1;
+      }
+    } else {
+      for (int j = 0; j < GROUP; j += 2)
+        normal_pair(&g, is_f64, &z[(int64_t)t * GROUP + j], &z[(int64_t)t * GROUP + j + 1]);
     }
+  }
 }
 
 /* normals[t][p] of contract ordinal `ordinal` (dtype 0: f32 out, 1: f64 out). */

@@ -246,13 +246,23 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   for (int i = 0; i < kRowBlock; ++i) {
     if (FULLBLOCK || i < nrows) {
       const int t = STRAIGHT ? i : t0 + i;
+      // step pairs draw one Box-Muller pair per path; the last step of an odd T (only in a partial
+      // block) two pairs for the 4 paths (smc_rng.h draw order)
+      const bool tail = !FULLBLOCK && t + 1 == T;
       if constexpr (kPacked) {
-        if ((i & 1) == 0) s.hw_log_increments4(step.b, step.a, zl, zh);
+        if ((i & 1) == 0) {
+          if (tail) s.hw_log_tail4(step.b, step.a, zl);
+          else s.hw_log_increments4(step.b, step.a, zl, zh);
+        }
         advance_packed(x, (i & 1) ? zh : zl);
       } else {
         if ((i & 1) == 0) {
+          if (tail) {
+            s.template normal_tail<HW>(zl);
+          } else {
 #pragma unroll
-          for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
+            for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
+          }
         }
 #pragma unroll
         for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], (i & 1) ? zh[j] : zl[j]);
@@ -305,8 +315,8 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
 }
 
 // The lane's 4 paths p0..p0+3 through all T rows in one rolled loop over step pairs (any T >= 1):
-// the stream, the draw order (one Box-Muller pair per path and step pair; the second normal of an
-// odd T's last pair is drawn and discarded) and the arithmetic are lane_paths'; x and the generator
+// the stream, the draw order (one Box-Muller pair per path and step pair; an odd T's last step two
+// pairs for the 4 paths) and the arithmetic are lane_paths'; x and the generator
 // stay in registers from row to row (no replay of earlier rows, no per-row branches).  STORE_ALL:
 // row t at row_base + t * pitch; else only the terminal row, at row_base.  The lane's 4 terminal
 // values go to x_out and their sum (f32 sum for f32 paths, then f64) is added to acc.
@@ -358,8 +368,9 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Rea
     if constexpr (STORE_ALL) store();
     row += rstride;
   }
-  if (T & 1) {
-    draw();
+  if (T & 1) {  // the last step of an odd T: two Box-Muller pairs for the 4 paths
+    if constexpr (kPacked) s.hw_log_tail4(step.b, step.a, zl);
+    else s.template normal_tail<HW>(zl);
     advance(zl);
     if constexpr (STORE_ALL) store();
   }
@@ -1238,8 +1249,12 @@ __global__ __launch_bounds__(256) void normals_kernel(uint64_t seed, uint64_t or
   Real z0[kPathsPerLane], z1[kPathsPerLane];
   for (int t = 0; t < rows; ++t) {
     if ((t & 1) == 0) {
+      if (t + 1 < rows) {
 #pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(z0[j], z1[j]);
+        for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(z0[j], z1[j]);
+      } else {
+        s.template normal_tail<HW>(z0);  // the last row of an odd count: two pairs for the 4 paths
+      }
     }
 #pragma unroll
     for (int j = 0; j < kPathsPerLane; ++j) {

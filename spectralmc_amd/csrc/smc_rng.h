@@ -17,8 +17,10 @@
 //                 f32: ln / sin / cos are the portable kernels of smc_math.h, so the normals
 //                 are bit-identical to the CPU restatement.
 //   draw order: for each step pair (t, t+1), t even: for j = 0..3 (path 4g + j): one Box-Muller
-//   pair (a, b) -> normals t and t+1 of that path.  Draws of paths >= P (ragged last group) are
-//   made and discarded, so the stream position never depends on P.
+//   pair (a, b) -> normals t and t+1 of that path.  The last step of an odd T (round 4): two pairs,
+//   pair k -> normal T-1 of paths 2k (z0) and 2k + 1 (z1), so no normal is drawn and discarded (at
+//   T = 1, the reference's lock-step shape, that halves the transcendentals).  Draws of paths >= P
+//   (ragged last group) are made and discarded, so the stream position never depends on P.
 //
 // Philox runs once per group (its round keys are wave-uniform, so the key schedule lives in
 // SGPRs) and is amortised over 4 paths x T steps; each further u32 is one v_mad_u64_u32 plus an
@@ -136,6 +138,24 @@ struct PathStream {
     }
   }
 
+  // HW log-Euler, last step of an odd T: the exponents y = a + b z of the lane's 4 paths from two
+  // Box-Muller pairs (paths 0, 1: pair 0's z0, z1; paths 2, 3: pair 1's), the arithmetic of
+  // hw_log_increments4.
+  __device__ __forceinline__ void hw_log_tail4(float b, float a, float (&y)[4]) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t ua = next(), ub = next();
+      const float u1 = 2.0f - __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ua, 9));
+      const float br = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u1)) * b;
+      const float w = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, ub, 9));
+      const f2 v = __builtin_elementwise_fma(f2{br, br}, f2{__builtin_amdgcn_cosf(w), __builtin_amdgcn_sinf(w)},
+                                             f2{a, a});
+      y[2 * k] = v.x;
+      y[2 * k + 1] = v.y;
+    }
+  }
+
   // Two N(0,1) draws, double precision: u1 = (a + 1) 2^-32 in (0, 1], angle = b 2^-32 revolutions;
   // ln u1 and (sin, cos) of the angle from the 32-bit integers (smc_math.h log_u32 / sincos2pi_u32,
   // restated by the CPU oracle: bit-identical normals), sqrt correctly rounded.
@@ -147,6 +167,14 @@ struct PathStream {
     math::sincos2pi_u32(b, s, c);
     z0 = r * c;
     z1 = r * s;
+  }
+
+  // The last step of an odd T: normals of the lane's 4 paths from two pairs (paths 2k, 2k + 1 take
+  // pair k's z0, z1).
+  template <bool HW, typename Real>
+  __device__ __forceinline__ void normal_tail(Real (&z)[4]) {
+    normal_pair<HW>(z[0], z[1]);
+    normal_pair<HW>(z[2], z[3]);
   }
 };
 

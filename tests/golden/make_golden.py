@@ -72,7 +72,8 @@ GBM_CASES = (
     ("c3shape", 16, 1024, 256, "float32", "log_euler", "normalize", 7, 0, slice(2, 3)),
     # resident-kernel shapes with T != 16 (rolled row loop): the reference's lock-step trainer shape
     # (tests/test_gbm_trainer.py:122-131: T = 1, N = 16, M = 4096), odd T with simple Euler, T > 16 RAW
-    ("lockstep", 1, 16, 4096, "float32", "log_euler", "normalize", 43, 0, slice(54, 56)),
+    ("lockstep", 1, 16, 4096, "float32", "log_euler", "raw", 43, 0, slice(54, 56)),
+    ("lockstepf64", 1, 16, 4096, "float64", "log_euler", "raw", 43, 0, slice(54, 56)),
     ("t5", 5, 64, 64, "float32", "simple_euler", "normalize", 11, 40, slice(56, 58)),
     ("t33", 33, 256, 16, "float32", "log_euler", "raw", 7, 2, slice(58, 60)),
 )

@@ -114,6 +114,53 @@ def test_lockstep_training_is_bit_exact(dtype) -> None:
     assert all(p.dtype == dtype for p in ma.parameters())
 
 
+def _lockstep_pricer(dtype: torch.dtype, seed: int = 43):
+    """The reference's lock-step trainer (tests/test_gbm_trainer.py:122-160): T = 1, N = 16, M = 4096,
+    LOG_EULER + RAW, mc_seed = seed, CVNN 6 -> 32 (modReLU) -> 16."""
+    from spectralmc.gbm import ForwardNormalization, PathScheme
+
+    prec = Precision.float32 if dtype == torch.float32 else Precision.float64
+    sp = make_simulation_params(timesteps=1, network_size=16, batches_per_mc_run=2 ** 12, threads_per_block=256,
+                                mc_seed=seed, buffer_size=1, dtype=prec)
+    bs = make_black_scholes_config(sim_params=sp, path_scheme=PathScheme.LOG_EULER,
+                                   normalization=ForwardNormalization.RAW)
+    model = make_test_cvnn(n_inputs=6, n_outputs=16, seed=seed, dtype=dtype)
+    cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=bs, domain_bounds=make_domain_bounds())
+    return expect_success(GbmCVNNPricer.create(cfg)), model
+
+
+@pytest.mark.parametrize("dtype", PRECISIONS)
+def test_reference_lockstep_contract(oracle, dtype) -> None:
+    """Reference tests/test_gbm_trainer.py:182-193 at its own shape: two pricers built alike train
+    batches (2, 3, 1) of 8 contracts in lock step, bit-identical after every call (f32: the resident
+    kernel's rolled row loop; f64: rows_kernel + cf_kernel); plus one step against the oracle
+    (reference-mode targets: RAW, T = 1, odd-T tail draw; torch-cpu _torch_step)."""
+    first, m1 = _lockstep_pricer(dtype)
+    second, m2 = _lockstep_pricer(dtype)
+    assert max_param_diff(m1, m2) == 0.0
+    for batches in (2, 3, 1):
+        cfg = make_training_config(num_batches=batches, batch_size=8, learning_rate=1.0e-2)
+        expect_success(first.train(cfg))
+        expect_success(second.train(cfg))
+        assert max_param_diff(m1, m2) == 0.0
+
+    one, m_one = _lockstep_pricer(dtype)
+    cpu_model = copy.deepcopy(m_one).cpu()
+    res = expect_success(one.train(make_training_config(num_batches=1, batch_size=8, learning_rate=1.0e-2)))
+    lo, hi = make_domain_bounds().arrays()
+    contracts = oracle.sobol_contracts(43, 0, 8, lo, hi)
+    sdt = "float32" if dtype == torch.float32 else "float64"
+    targets = oracle.training_targets(contracts, 1, 16, 4096, seed=43, ordinal0=0, normalize=False, dtype=sdt)
+    x = torch.tensor(contracts, dtype=dtype)
+    ref = oracle.torch_step(cpu_model, x, torch.zeros_like(x), torch.from_numpy(targets),
+                            torch.optim.Adam(cpu_model.parameters(), lr=1.0e-2))
+    tol = 1e-4 if dtype == torch.float32 else 1e-10
+    assert res.final_loss == pytest.approx(ref.loss, rel=tol)
+    for pg, pc in zip(m_one.parameters(), cpu_model.parameters(), strict=True):
+        a, b = pg.detach().cpu().double(), pc.detach().double()
+        assert float((a - b).norm() / max(float(b.norm()), 1e-12)) < tol
+
+
 @pytest.mark.parametrize("dtype", PRECISIONS)
 def test_snapshot_restore_continues_identically(dtype) -> None:
     """Reference tests/test_gbm_trainer.py:201-263 (both precisions)."""

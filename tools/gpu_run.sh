@@ -88,6 +88,9 @@ for step in "$@"; do
     testk:*)  # testk:<pytest -k expression with , for spaces>
       IFS=: read -r _ expr <<< "$step"
       run testk 600 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -rf -k "${expr//,/ }" ;;
+    ab:*)  # ab:<tag>:<kprof_step args with , for spaces>:<variant names with ,> (tools/micro/ab.sh)
+      IFS=: read -r _ tag args names <<< "$step"
+      run "ab_$tag" 900 bash tools/micro/ab.sh "$OUT/ab_$tag.txt" "${args//,/ }" ${names//,/ } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
