@@ -183,20 +183,20 @@ static void twiddle(int64_t j, int64_t N, double* s_out, double* c_out) {
 static inline uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
 static inline double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
 
-/* ln((a + 1) 2^-32): m = a + 1 = 2^e f exactly, f folded into [sqrt(1/2), sqrt(2)); table point
- * c = 1 + i/64 nearest f (i = rint((f - 1) 64), i = 0 at f = 1 so no cancellation near u = 1),
- * r = f INV - 1 in one fma, ln(1 + r) to r^8 (|r| <= 0.0078: truncation < 3e-19 of r), then
- * (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))) with ln 2 as a double plus its remainder. */
+/* ln((a + 1) 2^-32) as smc_math.h log_u32 (round 4): m = a + 1 = 2^e f exactly; mh = the top 20
+ * mantissa bits; f >= 1 + 0x6A09F 2^-20 is halved (e + 1); table entry idx = ((mh + 2^13) >> 14) + 32,
+ * halved ((mh + 2^14) >> 15) (c = 1 + (idx - 32)/64 nearest f, round half up on mh); r = f INV - 1 in
+ * one fma, ln(1 + r) to r^8, then (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))). */
 static double log_u32(uint32_t a) {
   const double m = (double)a + 1.0;
   const uint64_t bits = d2u(m);
-  int e = (int)(bits >> 52) - 1023;
-  uint64_t fb = (bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;
-  const int hi = fb > 0x3FF6A09E667F3BCDull;
-  if (hi) { fb -= 0x0010000000000000ull; e += 1; }
-  const double f = u2d(fb);
-  const int i = (int)rint((f - 1.0) * 64.0);
-  const double* t = kF64LogTab[i + 32];
+  const uint32_t hw = (uint32_t)(bits >> 32);
+  const uint32_t mh = hw & 0xFFFFFu;
+  const int half = mh >= 0x6A09Fu;
+  const int idx = half ? (int)((mh + (1u << 14)) >> 15) : (int)((mh + (1u << 13)) >> 14) + 32;
+  const int e = (int)(hw >> 20) - 1023 + (half ? 1 : 0);
+  const double f = u2d(((uint64_t)(mh | (half ? 0x3FE00000u : 0x3FF00000u)) << 32) | (bits & 0xFFFFFFFFull));
+  const double* t = kF64LogTab[idx];
   const double r = fma(f, t[0], -1.0);
   double q = -0.125;
   q = fma(q, r, 0.14285714285714285);
@@ -234,36 +234,39 @@ static void sincos_series(double x, double* s_out, double* c_out) {
   *c_out = fma(c, -u, 1.0);
 }
 
-/* (sin, cos)(2 pi b 2^-32): nearest table angle j = round(b / 2^24) (mod 256), rem = b - j 2^24 in
- * [-2^23, 2^23) exactly, x = 2 pi rem 2^-32 (|x| <= pi/256), sin x to x^7, cos x to x^6, then the
- * rotation by the table's (sin, cos)(2 pi j / 256). */
+/* (sin, cos)(2 pi b 2^-32) as smc_math.h (round 4): nearest of 64 table angles j = round(b / 2^26)
+ * (mod 64), rem = b - j 2^26 in [-2^25, 2^25) exactly, x = rem (2 pi 2^-32) (|x| <= pi/64), sin x to
+ * x^9, cos x to x^8, then the rotation by the table's (sin, cos)(2 pi j / 64). */
 static void sincos2pi_u32(uint32_t b, double* s_out, double* c_out) {
-  const uint32_t j = ((b + (1u << 23)) >> 24) & 255u;
-  const int32_t rem = (int32_t)(b - (j << 24));
-  const double x = (double)rem * 0x1p-32 * 6.283185307179586;
+  const uint32_t j = ((b + (1u << 25)) >> 26) & 63u;
+  const int32_t rem = (int32_t)(b - (j << 26));
+  const double x = (double)rem * 1.4629180792671596e-09;
   const double u = x * x;
-  double sp = -0.0001984126984126984;
+  double sp = 2.7557319223985893e-06;
+  sp = fma(sp, u, -0.0001984126984126984);
   sp = fma(sp, u, 0.008333333333333333);
   sp = fma(sp, u, -0.16666666666666666);
   const double sx = fma(sp * u, x, x);
-  double cp = -0.001388888888888889;
+  double cp = 2.48015873015873e-05;
+  cp = fma(cp, u, -0.001388888888888889);
   cp = fma(cp, u, 0.041666666666666664);
   cp = fma(cp, u, -0.5);
   const double cx = fma(cp, u, 1.0);
-  const double S = kF64SinCosTab[j][0], C = kF64SinCosTab[j][1];
+  const double S = kF64SinCos64Tab[j][0], C = kF64SinCos64Tab[j][1];
   *s_out = fma(S, cx, C * sx);
   *c_out = fma(C, cx, -(S * sx));
 }
 
 /* e^y as smc_math.h exp_f64 (the f64 device recursion; the oracle's reference mode keeps libm exp):
- * n = rint(y 64 / ln 2) = 64 m + j, r = y - n ln2/64 (Cody-Waite: ln2/64 with 17 trailing zero bits
- * plus its remainder, each a fused step; |r| <= 0.0055), e^r - 1 to r^6, 2^(j/64) from the table,
- * exact ldexp by m. */
+ * t = fma(y, 64 / ln 2, 1.5 2^52) rounds y 64 / ln 2 to the integer n = 64 m + j (t's low word),
+ * n = t - 1.5 2^52, r = y - n ln2/64 (Cody-Waite, two fused steps; |r| <= 0.0055), e^r - 1 to r^6,
+ * 2^(j/64) from the table, exact ldexp by m. */
 double oracle_exp_f64(double y) {
-  const double n = rint(y * 92.33248261689366);
-  const int ni = (int)n;
+  const double t = fma(y, 92.33248261689366, 6755399441055744.0);
+  const int ni = (int)(uint32_t)d2u(t);
+  const double n = t - 6755399441055744.0;
   const int j = ni & 63;
-  const int mm = (ni - j) / 64;
+  const int mm = ni >> 6;
   double r = fma(-n, 0.010830424696223417, y);
   r = fma(-n, 2.572804622327669e-14, r);
   double q = 0.001388888888888889;

@@ -221,8 +221,10 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   const bool store_all = STRAIGHT ? STRAIGHT_ALL : a.store == SMC_STORE_ALL;
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));  // the lane's group stream
-  // f32 HW log-Euler: the RNG hands back the step exponents directly (packed path pairs)
+  // f32 HW log-Euler: the RNG hands back the step exponents directly (packed path pairs); f64
+  // log-Euler: the exponents too (b folded into the Box-Muller radius), x *= exp_f64(y)
   constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
+  constexpr bool kY64 = LOG_EULER && sizeof(Real) == 8;
   Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
 #pragma unroll
   for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
@@ -231,6 +233,10 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
       s.hw_log_increments4(step.b, step.a, zl, zh);
       advance_packed(x, zl);
       advance_packed(x, zh);
+    } else if constexpr (kY64) {
+      s.f64_log_increments4(step.b, step.a, zl, zh);
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = x[j] * math::exp_f64(zl[j]) * math::exp_f64(zh[j]);
     } else {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
@@ -255,6 +261,13 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
           else s.hw_log_increments4(step.b, step.a, zl, zh);
         }
         advance_packed(x, (i & 1) ? zh : zl);
+      } else if constexpr (kY64) {
+        if ((i & 1) == 0) {
+          if (tail) s.f64_log_tail4(step.b, step.a, zl);
+          else s.f64_log_increments4(step.b, step.a, zl, zh);
+        }
+#pragma unroll
+        for (int j = 0; j < kPathsPerLane; ++j) x[j] = x[j] * math::exp_f64((i & 1) ? zh[j] : zl[j]);
       } else {
         if ((i & 1) == 0) {
           if (tail) {
@@ -328,6 +341,7 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Rea
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));
   constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
+  constexpr bool kY64 = LOG_EULER && sizeof(Real) == 8;  // exponents drawn directly (lane_paths)
   Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
 #pragma unroll
   for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
@@ -337,6 +351,8 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Rea
   auto draw = [&] {
     if constexpr (kPacked) {
       s.hw_log_increments4(step.b, step.a, zl, zh);
+    } else if constexpr (kY64) {
+      s.f64_log_increments4(step.b, step.a, zl, zh);
     } else {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
@@ -345,6 +361,9 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Rea
   auto advance = [&](const Real (&z)[kPathsPerLane]) {
     if constexpr (kPacked) {
       advance_packed(x, z);
+    } else if constexpr (kY64) {
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = x[j] * math::exp_f64(z[j]);
     } else {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], z[j]);
@@ -370,6 +389,7 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Rea
   }
   if (T & 1) {  // the last step of an odd T: two Box-Muller pairs for the 4 paths
     if constexpr (kPacked) s.hw_log_tail4(step.b, step.a, zl);
+    else if constexpr (kY64) s.f64_log_tail4(step.b, step.a, zl);
     else s.template normal_tail<HW>(zl);
     advance(zl);
     if constexpr (STORE_ALL) store();

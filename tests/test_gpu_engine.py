@@ -520,6 +520,49 @@ def test_rows_train_step_dynamic_queue_equals_targets(golden, B, T, N, M, dtype,
         assert not sync.view(torch.int32).any()
 
 
+def test_c2_f64_timed_call_matches_oracle(oracle, golden) -> None:
+    """The f64 C2 MC part exactly as the bench times it: smc_train_step at T = 16, N = M = 256
+    (P = 65,536: rows_kernel + the contract queue + cf_kernel), B = 2500 contracts (more than two rounds
+    of the persistent grid), two steps; every 80th contract against the oracle's reference-mode f64
+    targets (the reference's f64 recursion with libm exp on this build's f64 normals, numpy-order FFT)
+    at 1e-10 norm-relative (reference gbm.py:241-250 computes the recursion in f64)."""
+    L = _L()
+    B, T, N, M = 2500, 16, 256, 256
+    P = N * M
+    dtype = _lib.DTYPE_F64
+    pitch = int(L.smc_path_pitch(P, dtype))
+    assert L.smc_train_step_kernel(T, N, M, dtype, pitch) == b"rows_kernel+cf_kernel"
+    slots = 4 * torch.cuda.get_device_properties(0).multi_processor_count  # 4 workgroups per CU
+    assert B > 2 * slots
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
+    lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
+    hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
+    paths = torch.empty((B, T, pitch), dtype=torch.float64, device=DEV)
+    cur = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
+    nsync = int(L.smc_train_step_sync_bytes(T, N, M, dtype, pitch))
+    sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
+    for step in range(2):
+        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
+        t = torch.empty((B, N), dtype=torch.complex128, device=DEV)
+        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
+                                    _lib.ptr(c), None, B, T, N, M, 7, _lib.SCHEME_LOG_EULER | _lib.MATH_HW,
+                                    _lib.NORM_NORMALIZE, dtype, _lib.STORE_ALL, _lib.ptr(paths), pitch, B,
+                                    _lib.ptr(t), _lib.ptr(sync), nsync, None))
+        torch.cuda.synchronize()
+        assert cur.tolist() == [(step + 1) * B] * 2
+        assert not sync.view(torch.int32).any()
+        idx = np.arange(step, B, 80)
+        contracts = c.cpu().numpy()
+        np.testing.assert_array_equal(contracts, oracle.sobol_contracts(7, step * B, B, golden["bounds_lower"],
+                                                                        golden["bounds_upper"]))
+        got = t.cpu().numpy()[idx]
+        for k, b in enumerate(idx):  # one contract at a time: each keeps its own normal ordinal
+            want = oracle.training_targets(contracts[b:b + 1], T, N, M, seed=7, ordinal0=step * B + int(b),
+                                           dtype="float64")
+            assert _norm_rel(got[k:k + 1], want) < 1e-10, (step, b)
+
+
 SLICED_CASES = [  # (B, N, M, store, chunk): shapes with P > 65,536 (W = P / 65,536 slices)
     (None, 1024, 256, _lib.STORE_ALL, None),   # C3 per-contract shape, W = 4, > 1 contract per group
     (70, 1024, 256, _lib.STORE_ALL, 24),       # C3 shape in three chunk launches

@@ -91,6 +91,10 @@ for step in "$@"; do
     ab:*)  # ab:<tag>:<kprof_step args with , for spaces>:<variant names with ,> (tools/micro/ab.sh)
       IFS=: read -r _ tag args names <<< "$step"
       run "ab_$tag" 900 bash tools/micro/ab.sh "$OUT/ab_$tag.txt" "${args//,/ }" ${names//,/ } ;;
+    pmcv:*)  # pmcv:<variant|default>:<kprof_step args with ,>:<counters with ,> -> one PMC pass
+      IFS=: read -r _ var args ctrs <<< "$step"; tag="${var}_$(echo "$ctrs" | tr ',' '_' | cut -c1-40)"
+      if [ "$var" = default ]; then lib=$ROOT/spectralmc_amd/libspectralmc_hip.so; else lib=$ROOT/tools/micro/v/libsmc_$var.so; fi
+      cd /tmp && SMC_LIB_PATH=$lib run "pmcv_$tag" 120 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } -d "$OUT/pmcv_$tag" -o run --output-format csv -- python "$ROOT/tools/kprof_step.py" ${args//,/ }; cd "$ROOT" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
