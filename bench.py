@@ -54,11 +54,17 @@ CONFIGS = {
     # the lock-step trainer shape (tests/test_gbm_trainer.py:122-131, T = 1, N = 16, M = 4096) at C2's
     # batch, and C2 in float64 (Precision.float64: f64 paths, complex128 targets, f64 CVNN)
     "lockstep": (4096, 1, 16, 4096, [32, 32],
-                 "lock-step shape: 4096 contracts x 65536 paths (N=16 x M=4096), T=1, 3-layer CVNN 6->32->32->16 fp32"),
+                 "lock-step shape: 4096 contracts x 65536 paths (N=16 x M=4096), T=1, LOG_EULER + RAW, 3-layer CVNN "
+                 "6->32->32->16 fp32"),
+    # the reference's e2e shape (tests/test_e2e/test_full_stack_cvnn_pricer.py:40-51: T = 16, N = 128, M = 4)
+    # at C2's batch: P = 512, packed_kernel (8 contracts per workgroup)
+    "e2e": (4096, 16, 128, 4, [32],
+            "e2e shape: 4096 contracts x 512 paths (N=128 x M=4), T=16, 2-layer CVNN 6->32->128 fp32"),
     "c2f64": (4096, 16, 256, 256, [32, 32],
               "C2 in float64: 4096 contracts x 65536 paths (N=256 x M=256), T=16, 3-layer CVNN 6->32->32->256 fp64"),
 }
 SIM_DTYPE = {"c2f64": "float64"}  # default float32
+RAW_NORMALIZATION = {"lockstep"}  # ForwardNormalization.RAW (reference tests/test_gbm_trainer.py:138-142)
 BASKET_ASSETS = {"c5": 4}
 NETWORK_COMPUTE = {"c3": "bf16"}  # default "auto": f32 on the f32 MFMA kernels
 MFMA_PEAK_TFLOPS = {"mfma_bf16": 2516.6, "mfma_f32": 157.3, "valu": 157.3}  # MI355X_MICROARCH.md, dense
@@ -81,6 +87,8 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--lanes", type=int, default=2, choices=[1, 2, 4], help="MC lanes (pricer.mc_lanes): consecutive path launches "
                     "on alternating streams, each starting in the previous one's tail")
     ap.add_argument("--net-cus", type=int, default=32, help="CUs reserved for the network (pricer.network_cus)")
+    ap.add_argument("--net-cus-wide", type=int, default=64,
+                    help="CUs reserved for a wide (layered GEMM) network (pricer.network_cus_wide)")
     ap.add_argument("--net-cu-pattern", default="low", choices=["spread", "low"])
     ap.add_argument("--graphs", default="on", choices=["on", "off"], help="replay the step as hipGraphs")
     ap.add_argument("--kernel-iters", type=int, default=10)
@@ -105,7 +113,7 @@ def cpu_threads() -> int:
 
 
 def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: float, n_assets: int = 0,
-                 dtype: str = "float32") -> dict:
+                 dtype: str = "float32", normalize: bool = True) -> dict:
     """The reference CPU path (north_star: torch-cpu + numpy.fft; oracle/torch_cpu.py) timed on the
     host cores: MC for a time-boxed sample of the B contracts (extrapolated to B) + one full-size
     CVNN/Adam step on torch-cpu; plus C1 (BASELINE configs[0]) timed over 10 whole steps, and the
@@ -143,7 +151,8 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
                                  budget_s * 0.8, threads)
         path = "oracle C basket kernel-mode (f32)"
     else:
-        per_c, done, tg = sample(lambda c, o: cpu_path_targets(c, T, N, M, 7, o, dtype=dtype, normals="numpy"),
+        per_c, done, tg = sample(lambda c, o: cpu_path_targets(c, T, N, M, 7, o, dtype=dtype, normals="numpy",
+                                                               normalize=normalize),
                                  budget_s * 0.6, 2 * threads)
         path = ("torch-cpu paths (f64 recursion, numpy default_rng normals per contract) + numpy.fft "
                 "(oracle/torch_cpu.py)")
@@ -182,7 +191,8 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
     }
     if not n_assets:
         # second leg: the C/OpenMP oracle (f64 recursion, this build's normal streams)
-        per_c2, done2, _ = sample(lambda c, o: oracle.training_targets(c, T, N, M, seed=7, ordinal0=o, dtype=dtype),
+        per_c2, done2, _ = sample(lambda c, o: oracle.training_targets(c, T, N, M, seed=7, ordinal0=o, dtype=dtype,
+                                                                       normalize=normalize),
                                   budget_s * 0.2, threads)
         line["c_openmp_leg"] = {"value": B * N * M / (per_c2 * B + t_nn), "unit": "contracts*paths/s",
                                 "cores": threads, "kind": "port",
@@ -239,7 +249,11 @@ def main() -> None:
     n_inputs = 3 * n_assets + 4 if n_assets else 6
     model = make_test_cvnn(n_inputs=n_inputs, n_outputs=N, seed=123, dtype=torch.float64 if f64 else torch.float32,
                            device=dev, hidden_layers=len(widths), hidden_width=widths[0])
-    cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+    from spectralmc_amd.gbm import ForwardNormalization
+
+    norm = ForwardNormalization.RAW if args.config in RAW_NORMALIZATION else ForwardNormalization.NORMALIZE
+    cfg = make_gbm_cvnn_config(model, sim_params=sp,
+                               bs_config=make_black_scholes_config(sim_params=sp, normalization=norm),
                                domain_bounds=make_domain_bounds())
     pricer = expect_success(GbmCVNNPricer.create(cfg))
     pricer.store_paths = args.store == "all"
@@ -250,6 +264,7 @@ def main() -> None:
     pricer.high_priority_stream = args.priority
     pricer.mc_lanes = args.lanes
     pricer.network_cus = args.net_cus
+    pricer.network_cus_wide = args.net_cus_wide
     pricer.network_cu_pattern = args.net_cu_pattern
     if n_assets:
         from spectralmc_amd.basket import BasketConfig, use_basket_engine
@@ -458,7 +473,8 @@ def main() -> None:
         "final_loss": final.loss,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(B, T, N, M, widths, args.cpu_seconds, n_assets, "float64" if f64 else "float32")
+        cb = cpu_baseline(B, T, N, M, widths, args.cpu_seconds, n_assets, "float64" if f64 else "float32",
+                          normalize=args.config not in RAW_NORMALIZATION)
         line["cpu_baseline"] = cb
         line["speedup_vs_cpu"] = value / cb["value"]
     if rank == 0:

@@ -183,24 +183,22 @@ static void twiddle(int64_t j, int64_t N, double* s_out, double* c_out) {
 static inline uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
 static inline double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
 
-/* ln((a + 1) 2^-32) as smc_math.h log_u32 (round 4): m = a + 1 = 2^e f exactly; mh = the top 20
- * mantissa bits; f >= 1 + 0x6A09F 2^-20 is halved (e + 1); table entry idx = ((mh + 2^13) >> 14) + 32,
- * halved ((mh + 2^14) >> 15) (c = 1 + (idx - 32)/64 nearest f, round half up on mh); r = f INV - 1 in
- * one fma, ln(1 + r) to r^8, then (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))). */
+/* ln((a + 1/2) 2^-32) as smc_math.h log_u32 (round 4): m = a + 1/2 = 2^e f exactly; mh = the top 20
+ * mantissa bits; f >= 1 + 0x6A09F 2^-20 is halved (e + 1); table entry idx = ((mh + 2^11) >> 12) + 128,
+ * halved (mh + 2^12) >> 13 (c = 1 + (idx - 128)/256 nearest f, round half up on mh); r = f INV - 1 in
+ * one fma, ln(1 + r) to r^6, then (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))). */
 static double log_u32(uint32_t a) {
-  const double m = (double)a + 1.0;
+  const double m = (double)a + 0.5;
   const uint64_t bits = d2u(m);
   const uint32_t hw = (uint32_t)(bits >> 32);
   const uint32_t mh = hw & 0xFFFFFu;
   const int half = mh >= 0x6A09Fu;
-  const int idx = half ? (int)((mh + (1u << 14)) >> 15) : (int)((mh + (1u << 13)) >> 14) + 32;
+  const int idx = half ? (int)((mh + (1u << 12)) >> 13) : (int)((mh + (1u << 11)) >> 12) + 128;
   const int e = (int)(hw >> 20) - 1023 + (half ? 1 : 0);
   const double f = u2d(((uint64_t)(mh | (half ? 0x3FE00000u : 0x3FF00000u)) << 32) | (bits & 0xFFFFFFFFull));
   const double* t = kF64LogTab[idx];
   const double r = fma(f, t[0], -1.0);
-  double q = -0.125;
-  q = fma(q, r, 0.14285714285714285);
-  q = fma(q, r, -0.16666666666666666);
+  double q = -0.16666666666666666;
   q = fma(q, r, 0.2);
   q = fma(q, r, -0.25);
   q = fma(q, r, 0.3333333333333333);
@@ -210,73 +208,56 @@ static double log_u32(uint32_t a) {
   return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, t[1] + (t[2] + p)));
 }
 
-static void sincos_series(double x, double* s_out, double* c_out) {
-  const double u = x * x;
-  double s = 2.8114572543455206e-15;
-  s = fma(s, -u, 7.647163731819816e-13);
-  s = fma(s, -u, 1.6059043836821613e-10);
-  s = fma(s, -u, 2.505210838544172e-08);
-  s = fma(s, -u, 2.7557319223985893e-06);
-  s = fma(s, -u, 0.0001984126984126984);
-  s = fma(s, -u, 0.008333333333333333);
-  s = fma(s, -u, 0.16666666666666666);
-  s = fma(s, -u, 1.0);
-  *s_out = s * x;
-  double c = 1.5619206968586225e-16;
-  c = fma(c, -u, 4.779477332387385e-14);
-  c = fma(c, -u, 1.1470745597729725e-11);
-  c = fma(c, -u, 2.08767569878681e-09);
-  c = fma(c, -u, 2.755731922398589e-07);
-  c = fma(c, -u, 2.48015873015873e-05);
-  c = fma(c, -u, 0.001388888888888889);
-  c = fma(c, -u, 0.041666666666666664);
-  c = fma(c, -u, 0.5);
-  *c_out = fma(c, -u, 1.0);
-}
-
-/* (sin, cos)(2 pi b 2^-32) as smc_math.h (round 4): nearest of 64 table angles j = round(b / 2^26)
- * (mod 64), rem = b - j 2^26 in [-2^25, 2^25) exactly, x = rem (2 pi 2^-32) (|x| <= pi/64), sin x to
- * x^9, cos x to x^8, then the rotation by the table's (sin, cos)(2 pi j / 64). */
+/* (sin, cos)(2 pi b 2^-32) as smc_math.h (round 4): nearest of 1024 table angles j = round(b / 2^22)
+ * (mod 1024), rem = b - j 2^22 in [-2^21, 2^21) exactly, x = rem (2 pi 2^-32) (|x| <= pi/1024), sin x to
+ * x^5, cos x to x^4, then the rotation by the table's (sin, cos)(2 pi j / 1024). */
 static void sincos2pi_u32(uint32_t b, double* s_out, double* c_out) {
-  const uint32_t j = ((b + (1u << 25)) >> 26) & 63u;
-  const int32_t rem = (int32_t)(b - (j << 26));
+  const uint32_t j = ((b + (1u << 21)) >> 22) & 1023u;
+  const int32_t rem = (int32_t)(b - (j << 22));
   const double x = (double)rem * 1.4629180792671596e-09;
   const double u = x * x;
-  double sp = 2.7557319223985893e-06;
-  sp = fma(sp, u, -0.0001984126984126984);
-  sp = fma(sp, u, 0.008333333333333333);
-  sp = fma(sp, u, -0.16666666666666666);
+  const double sp = fma(u, 0.008333333333333333, -0.16666666666666666);
   const double sx = fma(sp * u, x, x);
-  double cp = 2.48015873015873e-05;
-  cp = fma(cp, u, -0.001388888888888889);
-  cp = fma(cp, u, 0.041666666666666664);
-  cp = fma(cp, u, -0.5);
+  const double cp = fma(u, 0.041666666666666664, -0.5);
   const double cx = fma(cp, u, 1.0);
-  const double S = kF64SinCos64Tab[j][0], C = kF64SinCos64Tab[j][1];
+  const double S = kF64SinCosTab[j][0], C = kF64SinCosTab[j][1];
   *s_out = fma(S, cx, C * sx);
   *c_out = fma(C, cx, -(S * sx));
 }
 
-/* e^y as smc_math.h exp_f64 (the f64 device recursion; the oracle's reference mode keeps libm exp):
- * t = fma(y, 64 / ln 2, 1.5 2^52) rounds y 64 / ln 2 to the integer n = 64 m + j (t's low word),
- * n = t - 1.5 2^52, r = y - n ln2/64 (Cody-Waite, two fused steps; |r| <= 0.0055), e^r - 1 to r^6,
- * 2^(j/64) from the table, exact ldexp by m. */
-double oracle_exp_f64(double y) {
+/* The split of e^y as smc_math.h exp_split: t = fma(y, 64 / ln 2, 1.5 2^52) rounds y 64 / ln 2 to the
+ * integer n = 64 m + j (t's low word), n = t - 1.5 2^52, r = y - n ln2/64 (Cody-Waite, two fused steps),
+ * e^r - 1 to r^5; e^y = 2^m T (1 + em1), T = 2^(j/64) from the table. */
+static void exp_split(double y, double* T, double* em1, int* m) {
   const double t = fma(y, 92.33248261689366, 6755399441055744.0);
   const int ni = (int)(uint32_t)d2u(t);
   const double n = t - 6755399441055744.0;
-  const int j = ni & 63;
-  const int mm = ni >> 6;
   double r = fma(-n, 0.010830424696223417, y);
   r = fma(-n, 2.572804622327669e-14, r);
-  double q = 0.001388888888888889;
-  q = fma(q, r, 0.008333333333333333);
+  double q = 0.008333333333333333;
   q = fma(q, r, 0.041666666666666664);
   q = fma(q, r, 0.16666666666666666);
   q = fma(q, r, 0.5);
-  const double em1 = fma(q, r * r, r);
-  const double T = kF64Exp2Tab[j];
-  return ldexp(fma(T, em1, T), mm);
+  *T = kF64Exp2Tab[ni & 63];
+  *em1 = fma(q, r * r, r);
+  *m = ni >> 6;
+}
+
+/* e^y as smc_math.h exp_f64 (the oracle's reference mode keeps libm exp) */
+double oracle_exp_f64(double y) {
+  double T, em1;
+  int m;
+  exp_split(y, &T, &em1, &m);
+  return ldexp(fma(T, em1, T), m);
+}
+
+/* x e^y as smc_math.h mul_exp_f64, the f64 device log-Euler step: (x T) (1 + em1) scaled by 2^m */
+double oracle_mul_exp_f64(double x, double y) {
+  double T, em1;
+  int m;
+  exp_split(y, &T, &em1, &m);
+  const double xt = x * T;
+  return ldexp(fma(xt, em1, xt), m);
 }
 double oracle_log_u32(uint32_t a) { return log_u32(a); }
 void oracle_sincos2pi_u32(uint32_t b, double* s, double* c) { sincos2pi_u32(b, s, c); }
@@ -313,7 +294,7 @@ void oracle_stream_u32(uint64_t seed, uint64_t ordinal, uint64_t group, int64_t 
 static void normal_pair(mwc64x* g, int is_f64, double* z0, double* z1) {
   const uint32_t a = mwc_next(g), b = mwc_next(g);
   if (is_f64) {
-    /* u1 = (a + 1) 2^-32, angle b 2^-32 revolutions: smc_math.h log_u32 / sincos2pi_u32 */
+    /* u1 = (a + 1/2) 2^-32, angle b 2^-32 revolutions: smc_math.h log_u32 / sincos2pi_u32 */
     const double r = sqrt(-2.0 * log_u32(a));
     double sn, cs;
     sincos2pi_u32(b, &sn, &cs);
@@ -633,7 +614,35 @@ void oracle_kernel_cf(const double* contracts, int64_t B, int32_t N, int32_t M, 
       }
       for (int n = 0; n < N; ++n) {
         double col = 0.0;
-        for (int g = 0; g < G; ++g) col += part[g * N + n];
+        if (lanes == 1024 && W == 1 && N % 4 == 0 && N <= 1024 && G * N == 4096) {
+          /* resident_kernel's column_sums_tree (gbm.hip, round 4): R = 1024 / N partials, partial k adds
+           * groups k, k + R, k + 2R, k + 3R in order from 0.0; N < 64: the 64 / N partials of wave w
+           * (k = w 64/N + j) by a butterfly over j (offsets 32/N, ..., 1: lane offsets 32, ..., N), then the
+           * 16 wave sums in order; N >= 64: the R partials in k order */
+          const int R = 1024 / N;
+          double pk[1024];
+          for (int k = 0; k < R; ++k) {
+            double p = 0.0;
+            for (int u = 0; u < 4; ++u) p += part[(k + u * R) * N + n];
+            pk[k] = p;
+          }
+          if (N < 64) {
+            const int per = 64 / N;
+            for (int w = 0; w < 16; ++w) {
+              double v[64], nv[64];
+              for (int j = 0; j < per; ++j) v[j] = pk[w * per + j];
+              for (int off = per / 2; off >= 1; off >>= 1) {
+                for (int j = 0; j < per; ++j) nv[j] = v[j] + v[j ^ off];
+                memcpy(v, nv, sizeof(double) * (size_t)per);
+              }
+              col += v[0];
+            }
+          } else {
+            for (int k = 0; k < R; ++k) col += pk[k];
+          }
+        } else {
+          for (int g = 0; g < G; ++g) col += part[g * N + n];
+        }
         avg[n] += col; /* slices in order from 0.0 */
       }
     }

@@ -111,7 +111,7 @@ def stream_u32(seed: int, ordinal: int, group: int, n: int) -> np.ndarray:
 
 
 def log_u32(a: int) -> float:
-    """ln((a + 1) 2^-32): the f64 Box-Muller radius' log (csrc/smc_math.h log_u32)."""
+    """ln((a + 1/2) 2^-32): the f64 Box-Muller radius' log (csrc/smc_math.h log_u32)."""
     return float(lib().oracle_log_u32(a))
 
 
@@ -262,13 +262,18 @@ def kernel_cf(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndar
 
 def engine_wg(timesteps: int, network_size: int, n_paths: int, with_rowsum: bool = False,
               sliced: bool = False) -> int:
-    """Lanes of the engine workgroup smc_train_targets uses for an f32 training launch: 1024 for
+    """Lanes whose reduction order an f32 training launch of smc_train_targets follows: 1024 for
     resident_kernel (1 <= T <= 65,536, 4096 | P <= 65,536, N | 4096, 4 <= N <= 1024, no row sums, no
-    workspace), 512 otherwise (gbm.hip resident_ok)."""
+    workspace; gbm.hip resident_ok), P / 4 for packed_kernel (256 <= P <= 2048, P | 4096, 4 | N, N | P:
+    one chunk of P / 4 lanes per contract; gbm.hip packed_ok), 512 otherwise."""
     N, P = network_size, n_paths
-    ok = (1 <= timesteps <= 65536 and not with_rowsum and not sliced and P % 4096 == 0 and P // 4096 <= 16
-          and 4 <= N <= 1024 and 4096 % N == 0)
-    return 1024 if ok else 512
+    if with_rowsum or sliced or not 1 <= timesteps <= 65536:
+        return 512
+    if P % 4096 == 0 and P // 4096 <= 16 and 4 <= N <= 1024 and 4096 % N == 0:
+        return 1024
+    if 256 <= P <= 2048 and 4096 % P == 0 and N >= 4 and N % 4 == 0 and P % N == 0:
+        return P // 4
+    return 512
 
 
 def train_step_order(timesteps: int, network_size: int, n_paths: int) -> tuple[int, int]:

@@ -41,8 +41,9 @@ def numpy_seed_stream(mc_seed: int, skip: int, count: int) -> list[int]:
 
 def cpu_path_targets(contracts: np.ndarray, timesteps: int, network_size: int, batches: int, seed: int,
                      ordinal0: int = 0, dtype: str = "float32", normals: str = "build",
-                     workers: int | None = None) -> np.ndarray:
-    """CF targets (B, N) of B contracts on the torch-cpu + numpy.fft path (log-Euler, NORMALIZE).
+                     workers: int | None = None, normalize: bool = True) -> np.ndarray:
+    """CF targets (B, N) of B contracts on the torch-cpu + numpy.fft path (log-Euler; NORMALIZE, or RAW
+    with normalize=False).
 
     normals "build": this build's stream for each contract ordinal (oracle.normals), so the
     result is comparable with the GPU and the reference fixtures; "numpy": the reference
@@ -90,7 +91,8 @@ def cpu_path_targets(contracts: np.ndarray, timesteps: int, network_size: int, b
             fwd = np_sim(X0) * np.exp(np_sim(r - d) * times)
             df = np.exp(np_sim(-r) * times)
             terminal = paths[-1].numpy()
-            s_T = terminal * (fwd[-1] / terminal.mean())  # sims *= F / cp.mean(sims)  (terminal row)
+            # sims *= F / cp.mean(sims) (terminal row; RAW keeps the simulated values)
+            s_T = terminal * (fwd[-1] / terminal.mean()) if normalize else terminal
             put = (df[-1] * np.maximum(np_sim(K) - s_T, np_sim(0))).astype(np_sim)
             out[b] = np.fft.fft(put.reshape(M, N), axis=1).mean(axis=0)
     return out

@@ -178,7 +178,7 @@ struct Stepper {
     if constexpr (LOG_EULER) {
       if constexpr (sizeof(Real) == 4 && HW) return x * __builtin_amdgcn_exp2f(fmaf(b, z, a));
       else if constexpr (sizeof(Real) == 4) return x * math::exp2_any(fmaf(b, z, a));
-      else return x * math::exp_f64(fma(b, z, a));
+      else return math::mul_exp_f64(x, fma(b, z, a));
     }
     if constexpr (sizeof(Real) == 4) return fabsf(fmaf(x, fmaf(b, z, a), x));
     else return fabs(fma(x, fma(b, z, a), x));
@@ -213,13 +213,14 @@ template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS, bool MASKED, boo
 __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                            uint64_t ordinal, int64_t chunk, int nvalid, int t0, int nrows,
                                            Real* contract_base, double (&acc)[ALLROWS ? kRowBlock : 1],
-                                           Real* x_out = nullptr) {
+                                           Real* x_out = nullptr, int lid = -1) {
   using V4 = typename Vec4T<Real>::type;
   const int T = a.T;
   const int64_t P = a.P;
   const int64_t pitch = a.pitch ? a.pitch : P;
   const bool store_all = STRAIGHT ? STRAIGHT_ALL : a.store == SMC_STORE_ALL;
-  const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
+  const int lane_id = lid < 0 ? static_cast<int>(threadIdx.x) : lid;  // the lane's 4-path slot in the chunk
+  const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(lane_id);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));  // the lane's group stream
   // f32 HW log-Euler: the RNG hands back the step exponents directly (packed path pairs); f64
   // log-Euler: the exponents too (b folded into the Box-Muller radius), x *= exp_f64(y)
@@ -236,7 +237,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
     } else if constexpr (kY64) {
       s.f64_log_increments4(step.b, step.a, zl, zh);
 #pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) x[j] = x[j] * math::exp_f64(zl[j]) * math::exp_f64(zh[j]);
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp_f64(math::mul_exp_f64(x[j], zl[j]), zh[j]);
     } else {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
@@ -245,7 +246,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
     }
   }
   // wave-uniform row base (SGPR pair) + 32-bit per-lane byte offset
-  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(Real)) * threadIdx.x;
+  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(Real)) * static_cast<uint32_t>(lane_id);
   Real* chunk_base = contract_base + chunk;
   const __amdgpu_buffer_rsrc_t contract_rsrc = row_rsrc(contract_base);
 #pragma unroll
@@ -267,7 +268,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
           else s.f64_log_increments4(step.b, step.a, zl, zh);
         }
 #pragma unroll
-        for (int j = 0; j < kPathsPerLane; ++j) x[j] = x[j] * math::exp_f64((i & 1) ? zh[j] : zl[j]);
+        for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp_f64(x[j], (i & 1) ? zh[j] : zl[j]);
       } else {
         if ((i & 1) == 0) {
           if (tail) {
@@ -336,16 +337,17 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                           uint64_t ordinal, int64_t chunk, Real* contract_base, int T, int64_t pitch,
-                                          double& acc, Real (&x_out)[kPathsPerLane]) {
+                                          double& acc, Real (&x_out)[kPathsPerLane], int lid = -1) {
   using V4 = typename Vec4T<Real>::type;
-  const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(threadIdx.x);
+  const int lane_id = lid < 0 ? static_cast<int>(threadIdx.x) : lid;  // the lane's 4-path slot in the chunk
+  const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(lane_id);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));
   constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
   constexpr bool kY64 = LOG_EULER && sizeof(Real) == 8;  // exponents drawn directly (lane_paths)
   Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
 #pragma unroll
   for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
-  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(Real)) * threadIdx.x;
+  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(Real)) * static_cast<uint32_t>(lane_id);
   const char* row = reinterpret_cast<const char*>(contract_base + chunk);
   const int64_t rstride = STORE_ALL ? pitch * static_cast<int64_t>(sizeof(Real)) : 0;
   auto draw = [&] {
@@ -363,7 +365,7 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Rea
       advance_packed(x, z);
     } else if constexpr (kY64) {
 #pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) x[j] = x[j] * math::exp_f64(z[j]);
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp_f64(x[j], z[j]);
     } else {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], z[j]);
@@ -892,8 +894,44 @@ size_t resident_lds_bytes(int N) {
          (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 9 + 6 * kResPreDraw) * sizeof(double);
 }
 
-template <bool LOG_EULER, bool HW, bool STORE_ALL, bool T16>
+// Column sums of the whole-contract CF phase (W = 1, round 4): part[G][N] (G = 4096 / N) as a tree
+// instead of N threads adding G terms each: thread (k, n) = (tid / N, tid mod N) adds groups k, k + R,
+// k + 2R, k + 3R (R = 1024 / N) in order from 0.0 (consecutive lanes read consecutive columns: no LDS
+// bank conflicts); for N < 64 the 64 / N partials a wave holds of a column are added by a butterfly (lane
+// offsets 32, 16, ..., N) and the 16 wave sums in wave order, else the R partials in k order.  Then
+// avg[n] = sum / M.  The red scratch may alias part (read before the barrier inside).  Oracle:
+// kernel_cf(wg=1024, slices=1).
+__device__ __forceinline__ void column_sums_tree(const double* part, double* red, double* avg, int N, int M) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int R = kResThreads / N;
+  const int n = tid % N, k = tid / N;
+  double p = 0.0;
+  if (tid < N * R) {  // N <= 1024 (resident_ok): R >= 1
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p += part[(k + u * R) * N + n];
+  }
+  for (int off = 32; off >= N; off >>= 1) p += __shfl_xor(p, off, 64);
+  lds_barrier();  // every read of part is done (red may alias it)
+  if (N < 64) {
+    if (lane < N) red[wave * N + n] = p;
+  } else if (tid < N * R) {
+    red[k * N + n] = p;
+  }
+  lds_barrier();
+  const int terms = N < 64 ? kResWaves : R;
+  for (int c = tid; c < N; c += kResThreads) {
+    double t = 0.0;
+    for (int w = 0; w < terms; ++w) t += red[w * N + c];
+    avg[c] = t / static_cast<double>(M);
+  }
+}
+
+// ONTHEFLY (RAW normalisation, whole contracts, rolled rows: the reference's lock-step shape): the scale
+// is 1, so each chunk's payoffs go into the column sums as the chunk finishes (same chunk order, same
+// bits) and no terminal value is parked in LDS or in the register shift register.
+template <bool LOG_EULER, bool HW, bool STORE_ALL, bool T16, bool ONTHEFLY = false>
 __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
+  static_assert(!(ONTHEFLY && T16), "the on-the-fly CF phase is instantiated for the rolled row loop only");
   typedef float v4f __attribute__((ext_vector_type(4)));
   extern __shared__ double lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1000,6 +1038,8 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     // register array would put it in scratch memory); chunk ch ends in slot ch - nch + kResRegChunks
     float term[kResRegChunks][kPathsPerLane];
     double acc[1] = {0.0};
+    double colsum[kPathsPerLane] = {0.0, 0.0, 0.0, 0.0};
+    const Payoff<float> pay_raw(a, c, 1.0);  // ONTHEFLY: RAW, the terminal sum is not needed
     for (int ch = 0; ch < nch; ++ch) {
       float xt[kPathsPerLane];
       if constexpr (T16)  // the straight-line 16-row block (the benchmark shape)
@@ -1009,7 +1049,10 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       else
         lane_rows<float, LOG_EULER, HW, STORE_ALL>(a, step, x0, static_cast<uint64_t>(ord0 + b),
                                             p0 + static_cast<int64_t>(ch) * kResChunk, base, T, pitch, acc[0], xt);
-      if (ch < kResLdsChunks) {
+      if constexpr (ONTHEFLY) {
+#pragma unroll
+        for (int j = 0; j < kPathsPerLane; ++j) colsum[j] += static_cast<double>(pay_raw(xt[j]));
+      } else if (ch < kResLdsChunks) {
         term_lds[ch * kResThreads + tid] = v4f{xt[0], xt[1], xt[2], xt[3]};
       } else {
 #pragma unroll
@@ -1067,8 +1110,9 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       tot = row[6];
     }
     const Payoff<float> pay(a, c, tot);
-    double colsum[kPathsPerLane] = {0.0, 0.0, 0.0, 0.0};
-    {
+    if constexpr (!ONTHEFLY) {
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) colsum[j] = 0.0;  // (the zeros before the loop are dead here)
       v4f v[kResLdsChunks];  // every slot read (unused ones too), so the 8 reads are in flight together
 #pragma unroll
       for (int ch = 0; ch < kResLdsChunks; ++ch) v[ch] = term_lds[ch * kResThreads + tid];
@@ -1081,7 +1125,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < kResRegChunks; ++i) {
+    for (int i = 0; i < kResRegChunks && !ONTHEFLY; ++i) {
       if (i >= kResRegChunks - (nch - kResLdsChunks)) {  // chunk kResLdsChunks + i - (...), ascending
 #pragma unroll
         for (int j = 0; j < kPathsPerLane; ++j) colsum[j] += static_cast<double>(pay(term[i][j]));
@@ -1092,10 +1136,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     for (int j = 0; j < kPathsPerLane; ++j) part[g * N + 4 * q + j] = colsum[j];
     lds_barrier();
     if (W == 1) {
-      for (int n = tid; n < N; n += kResThreads) {
-        const double t = group_sum(part, n, G, N);
-        avg[n] = t / static_cast<double>(M);
-      }
+      column_sums_tree(part, part, avg, N, M);
     } else {
       // column-sum exchange: the slice's G group sums per column, published by wave 0; the last
       // slice to arrive adds the W column sums in slice order and runs the FFT
@@ -1140,6 +1181,125 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       *a.done = 0u;
     }
   }
+}
+
+// ---- packed_kernel: several whole contracts per workgroup (small P) ------------------------------
+// For 256 <= P <= 2048 (P | 4096) a contract's paths are P/4 lanes = P/256 whole waves, so a 1024-thread
+// workgroup runs K = 4096 / P contracts side by side instead of one contract on a quarter of a
+// 512-thread workgroup plus a CF re-read kernel (the reference's e2e shape, P = 512:
+// tests/test_e2e/test_full_stack_cvnn_pricer.py:40-51).  Persistent: workgroup w runs the contract
+// groups w, w + gridDim.x, ... (contracts K g ... K g + K - 1).  Per contract, resident_kernel's orders
+// with one chunk of P / 4 lanes (oracle kernel mode, wg = P / 4): lane -> f32 4-path sum -> f64, wave
+// butterfly, the contract's waves in order; item (q, g) = (lane mod N/4, 4 lane / N) is batch row m = g,
+// column sums over m ascending from 0.0, the M-mean, then the K FFTs side by side (fft_rows).  The
+// terminal values stay in registers; every barrier is LDS-only.  With a.sobol (smc_train_step) the
+// workgroup draws its contracts' Sobol rows and the last workgroup advances the cursor.
+constexpr int kPackMinP = 256, kPackMaxP = 2048;
+
+size_t packed_lds_bytes(int64_t P, int N) {
+  const int64_t K = kResChunk / P;
+  const int64_t part = K * P > 2 * K * N ? K * P : 2 * K * N;  // payoff sums [K][M][N]; FFT re / im [K][N] each
+  return static_cast<size_t>(part + K * N + 2 * N + kResWaves + 7 * K) * sizeof(double);
+}
+
+template <bool LOG_EULER, bool HW, bool STORE_ALL, bool T16>
+__global__ __launch_bounds__(kResThreads) void packed_kernel(EngineArgs a) {
+  extern __shared__ double lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = a.N, M = a.M;
+  const int64_t P = a.P;
+  const int64_t pitch = a.pitch ? a.pitch : P;
+  const int lpc = static_cast<int>(P / kPathsPerLane);  // lanes per contract (a multiple of 64)
+  const int K = kResThreads / lpc;                      // contracts per group
+  const int wpc = lpc / 64;                             // waves per contract
+  const int k = tid / lpc, l = tid - k * lpc;           // this lane's contract slot, its lane in the contract
+  const int cols = N / 4;
+  const int q = l % cols, g = l / cols;                 // item (q, g): columns 4q .. 4q + 3 of batch row g
+  const int64_t partn = K * P > 2 * K * N ? K * P : 2 * static_cast<int64_t>(K) * N;
+  double* part = lds;                                   // [K][M][N]; FFT re / im [K][N] after the M-mean
+  double* avg = part + partn;                           // [K][N]
+  double* cs = avg + K * N;                             // [N]
+  double* sn = cs + N;                                  // [N]
+  double* wsum = sn + N;                                // [kResWaves]
+  double* rows = wsum + kResWaves;                      // [K][7]: the drawn Sobol row, then the terminal sum
+  for (int j = tid; j < N; j += kResThreads) math::twiddle(j, N, sn[j], cs[j]);
+  const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
+  const int64_t sob0 = a.sobol ? a.cursor[0] + a.sobol_index0 : 0;
+  const int64_t ngroups = (a.B + K - 1) / K;
+  for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int64_t b0 = grp * K;
+    const int kv = a.B - b0 < K ? static_cast<int>(a.B - b0) : K;  // contracts of this group
+    if (tid < 6 * kv) {  // the group's contract rows (sobol_sampler.py:222-246, or the caller's)
+      const int kk = tid / 6, d = tid - 6 * kk;
+      double v;
+      if (a.sobol) {
+        v = sobol_coord(a.sobol, a.sobol_dim, d, static_cast<uint64_t>(sob0 + b0 + kk), a.lower, a.upper);
+        a.contracts_out[(b0 + kk) * 6 + d] = v;
+        if (a.cvnn_out) a.cvnn_out[(b0 + kk) * 6 + d] = static_cast<float>(v);
+      } else {
+        v = a.contracts[(b0 + kk) * 6 + d];
+      }
+      rows[kk * 7 + d] = v;
+    }
+    lds_barrier();
+    const bool active = k < kv;
+    const double* r = rows + (active ? k : 0) * 7;
+    const Contract c{r[0], r[1], r[2], r[3], r[4], r[5]};
+    const int T = T16 ? kRowBlock : a.T;
+    float xt[kPathsPerLane] = {0.0f, 0.0f, 0.0f, 0.0f};
+    double acc[1] = {0.0};
+    if (active) {
+      const Stepper<float, LOG_EULER, HW> step(c, T);
+      const float x0 = static_cast<float>(c.X0);
+      const int64_t b = b0 + k;
+      float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * T * pitch : b * pitch);
+      if constexpr (T16)
+        lane_paths<float, LOG_EULER, HW, false, false, true, true, STORE_ALL>(
+            a, step, x0, static_cast<uint64_t>(ord0 + b), 0, kPathsPerLane, 0, kRowBlock, base, acc, xt, l);
+      else
+        lane_rows<float, LOG_EULER, HW, STORE_ALL>(a, step, x0, static_cast<uint64_t>(ord0 + b), 0, base, T, pitch,
+                                                   acc[0], xt, l);
+    }
+    const double w = wave_sum(acc[0]);  // a wave holds lanes of one contract only
+    if (lane == 0) wsum[wave] = w;
+    lds_barrier();
+    if (tid < K) {  // the contract's waves in order
+      double tot = 0.0;
+      for (int v = 0; v < wpc; ++v) tot += wsum[tid * wpc + v];
+      rows[tid * 7 + 6] = tot;
+    }
+    lds_barrier();
+    if (active) {
+      const Payoff<float> pay(a, c, r[6]);
+      double* pk = part + static_cast<int64_t>(k) * P;
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) pk[g * N + 4 * q + j] = 0.0 + static_cast<double>(pay(xt[j]));
+    }
+    lds_barrier();
+    for (int e = tid; e < kv * N; e += kResThreads) {  // column sums over the M batch rows in order
+      const int kk = e / N, n = e - kk * N;
+      avg[e] = group_sum(part + static_cast<int64_t>(kk) * P, n, M, N) / static_cast<double>(M);
+    }
+    lds_barrier();
+    fft_rows<float, kResThreads, true>(avg, cs, sn, N, K, kv, part, part + static_cast<int64_t>(K) * N,
+                                       static_cast<float2*>(a.targets) + b0 * N);
+    lds_barrier();  // part / avg / rows are rewritten by the next group
+  }
+  if (a.done && tid == 0) {
+    // every workgroup read the cursor before it arrives here: the last one advances it
+    __threadfence();
+    if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
+      a.cursor[0] += a.advance;
+      a.cursor[1] += a.advance;
+      *a.done = 0u;
+    }
+  }
+}
+
+bool packed_ok(const EngineArgs& a, bool f32) {
+  return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.res_slices <= 1 && a.T >= 1 &&
+         a.T <= kResMaxT && a.P >= kPackMinP && a.P <= kPackMaxP && kResChunk % a.P == 0 && a.N >= 4 &&
+         a.N % 4 == 0 && a.P % a.N == 0 && (a.pitch == 0 || (a.pitch % 4 == 0 && a.pitch >= a.P));
 }
 
 bool resident_ok(const EngineArgs& a, bool f32) {
@@ -1456,8 +1616,10 @@ int32_t launch_rows_k(const EngineArgs& a, hipStream_t stream) {
 
 template <bool LOG_EULER, bool HW, bool STORE_ALL>
 int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
-  auto kernel = a.T == kRowBlock ? resident_kernel<LOG_EULER, HW, STORE_ALL, true>
-                                 : resident_kernel<LOG_EULER, HW, STORE_ALL, false>;
+  const int W = a.res_slices > 1 ? a.res_slices : 1;
+  auto kernel = a.T == kRowBlock                 ? resident_kernel<LOG_EULER, HW, STORE_ALL, true>
+                : (!a.normalize && W == 1) ? resident_kernel<LOG_EULER, HW, STORE_ALL, false, true>
+                                           : resident_kernel<LOG_EULER, HW, STORE_ALL, false>;
   const size_t lds = resident_lds_bytes(a.N);
   if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1465,7 +1627,6 @@ int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
     (void)hipGetLastError();
     return fail(SMC_ERR_HIP, "resident_kernel: cannot raise the dynamic LDS limit");
   }
-  const int W = a.res_slices > 1 ? a.res_slices : 1;
   unsigned grid = 0;
   if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kResThreads, lds, a.B * W, &grid, stream))
     return st;
@@ -1480,6 +1641,27 @@ int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
   }
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(kResThreads), lds, stream, a);
   return check_launch("resident_kernel");
+}
+
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
+int32_t launch_packed_k(const EngineArgs& a, hipStream_t stream) {
+  auto kernel = a.T == kRowBlock ? packed_kernel<LOG_EULER, HW, STORE_ALL, true>
+                                 : packed_kernel<LOG_EULER, HW, STORE_ALL, false>;
+  const size_t lds = packed_lds_bytes(a.P, a.N);
+  if (lds > kMaxLds) return fail(SMC_ERR_INVALID_SHAPE, "packed_kernel: network_size exceeds the LDS budget");
+  if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "packed_kernel: cannot raise the dynamic LDS limit");
+  }
+  const int64_t K = kResChunk / a.P;
+  unsigned grid = 0;
+  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kResThreads, lds, (a.B + K - 1) / K, &grid,
+                                 stream))
+    return st;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kResThreads), lds, stream, a);
+  return check_launch("packed_kernel");
 }
 
 // Training-shape kernel choice: 3 = resident_kernel where it applies (P <= 65,536), else the
@@ -1507,6 +1689,22 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
       SMC_RES(false, false, true)
       SMC_RES(false, false, false)
 #undef SMC_RES
+    }
+    if (SMC_TRAIN_MODE == 3 && packed_ok(a, true)) {  // small P: several contracts per workgroup
+      const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+      const bool hw = (a.scheme & SMC_MATH_HW) != 0;
+      const bool sa = a.store == SMC_STORE_ALL;
+#define SMC_PACK(LE, HWM, SA) \
+  if (log_euler == LE && hw == HWM && sa == SA) return launch_packed_k<LE, HWM, SA>(a, stream);
+      SMC_PACK(true, true, true)
+      SMC_PACK(true, true, false)
+      SMC_PACK(true, false, true)
+      SMC_PACK(true, false, false)
+      SMC_PACK(false, true, true)
+      SMC_PACK(false, true, false)
+      SMC_PACK(false, false, true)
+      SMC_PACK(false, false, false)
+#undef SMC_PACK
     }
     // the split pair: the straight-line T = 16 paths_kernel, or (ragged chunks) simulate_contract;
     // other whole-chunk shapes take rows_kernel below
@@ -1778,7 +1976,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   }
   const bool fused = SMC_TRAIN_MODE == 3 && dtype == SMC_DTYPE_F32 && n_contracts > 0 && chunk_contracts > 0 &&
                      valid_scheme(scheme) && (store_mode == SMC_STORE_ALL || store_mode == SMC_STORE_TERMINAL) &&
-                     paths_dev && targets_dev && resident_ok(a, true);
+                     paths_dev && targets_dev && (resident_ok(a, true) || packed_ok(a, true));
   if (fused) {
     // one resident launch per chunk of contracts; each draws its own contracts, the last advances
     // the cursor (the earlier ones read it unchanged)
@@ -1877,6 +2075,7 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.store = SMC_STORE_ALL;
   const bool f32 = (dtype & 0xff) == SMC_DTYPE_F32;
   if (SMC_TRAIN_MODE == 3 && resident_ok(a, f32)) return "resident_kernel";
+  if (SMC_TRAIN_MODE == 3 && packed_ok(a, f32)) return "packed_kernel";
   if (SMC_TRAIN_MODE >= 2 && split_ok(a, f32) && a.T == kRowBlock && a.P % kChunk == 0) return "paths_kernel+cf_kernel";
   if (SMC_TRAIN_MODE >= 2 && rows_ok(a, f32)) return "rows_kernel+cf_kernel";
   if (SMC_TRAIN_MODE >= 2 && split_ok(a, f32)) return "paths_kernel+cf_kernel";

@@ -100,9 +100,11 @@ __device__ __forceinline__ void lds_barrier() {  // LDS visibility only: no vmcn
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// K rows at once (avg, xr, xi: [K][N]; out: [kv][N], rows k < kv written): the per-row arithmetic and
+// order of one row, the (row, index) pairs spread over the NT threads (packed_kernel's contracts).
 template <typename Real, int NT, bool LDS_ONLY = false>
-__device__ void fft_row(const double* avg, const double* cs, const double* sn, int N, double* xr, double* xi,
-                        typename Complex2<Real>::type* out) {
+__device__ void fft_rows(const double* avg, const double* cs, const double* sn, int N, int K, int kv, double* xr,
+                         double* xi, typename Complex2<Real>::type* out) {
   using C2 = typename Complex2<Real>::type;
   const int tid = threadIdx.x;
   const int logN = 31 - __builtin_clz(static_cast<unsigned>(N));
@@ -110,10 +112,11 @@ __device__ void fft_row(const double* avg, const double* cs, const double* sn, i
     if constexpr (LDS_ONLY) lds_barrier();
     else __syncthreads();
   };
-  for (int n = tid; n < N; n += NT) {
+  for (int e = tid; e < K * N; e += NT) {
+    const int k = e >> logN, n = e & (N - 1);
     const int r = static_cast<int>(__builtin_bitreverse32(static_cast<unsigned>(n)) >> (32 - logN));
-    xr[r] = avg[n];
-    xi[r] = 0.0;
+    xr[k * N + r] = avg[e];
+    xi[k * N + r] = 0.0;
   }
   barrier();
   // one radix-2 butterfly on registers, the operations of the stage loop in the same order
@@ -130,11 +133,14 @@ __device__ void fft_row(const double* avg, const double* cs, const double* sn, i
   int s = 1;
   for (; s + 1 <= logN; s += 2) {
     const int h = 1 << (s - 1), shift = logN - s;
-    for (int qd = tid; qd < N / 4; qd += NT) {
+    for (int e = tid; e < K * (N / 4); e += NT) {
+      const int qd = e & (N / 4 - 1);
+      double* yr = xr + (e >> (logN - 2)) * N;
+      double* yi = xi + (e >> (logN - 2)) * N;
       const int pos = qd & (h - 1);
       const int i0 = ((qd >> (s - 1)) << (s + 1)) + pos;
-      double r0 = xr[i0], m0 = xi[i0], r1 = xr[i0 + h], m1 = xi[i0 + h];
-      double r2 = xr[i0 + 2 * h], m2 = xi[i0 + 2 * h], r3 = xr[i0 + 3 * h], m3 = xi[i0 + 3 * h];
+      double r0 = yr[i0], m0 = yi[i0], r1 = yr[i0 + h], m1 = yi[i0 + h];
+      double r2 = yr[i0 + 2 * h], m2 = yi[i0 + 2 * h], r3 = yr[i0 + 3 * h], m3 = yi[i0 + 3 * h];
       const double w1r = cs[pos << shift], w1i = -sn[pos << shift];
       bfly(r0, m0, r1, m1, w1r, w1i);  // stage s: (i0, i0 + h), (i0 + 2h, i0 + 3h)
       bfly(r2, m2, r3, m3, w1r, w1i);
@@ -142,41 +148,56 @@ __device__ void fft_row(const double* avg, const double* cs, const double* sn, i
       const double w3r = cs[(pos + h) << (shift - 1)], w3i = -sn[(pos + h) << (shift - 1)];
       bfly(r0, m0, r2, m2, w2r, w2i);  // stage s + 1: (i0, i0 + 2h), (i0 + h, i0 + 3h)
       bfly(r1, m1, r3, m3, w3r, w3i);
-      xr[i0] = r0;
-      xi[i0] = m0;
-      xr[i0 + h] = r1;
-      xi[i0 + h] = m1;
-      xr[i0 + 2 * h] = r2;
-      xi[i0 + 2 * h] = m2;
-      xr[i0 + 3 * h] = r3;
-      xi[i0 + 3 * h] = m3;
+      yr[i0] = r0;
+      yi[i0] = m0;
+      yr[i0 + h] = r1;
+      yi[i0 + h] = m1;
+      yr[i0 + 2 * h] = r2;
+      yi[i0 + 2 * h] = m2;
+      yr[i0 + 3 * h] = r3;
+      yi[i0 + 3 * h] = m3;
     }
     barrier();
   }
   if (s == logN) {  // an odd number of stages: the last one alone
     const int h = 1 << (s - 1), shift = logN - s;  // twiddle index t = (j mod h) << shift
-    for (int j = tid; j < N / 2; j += NT) {
+    for (int e = tid; e < K * (N / 2); e += NT) {
+      const int j = e & (N / 2 - 1);
+      double* yr = xr + (e >> (logN - 1)) * N;
+      double* yi = xi + (e >> (logN - 1)) * N;
       const int pos = j & (h - 1);
       const int i0 = ((j >> (s - 1)) << s) + pos, i1 = i0 + h;
-      double br = xr[i0], bi = xi[i0], ar = xr[i1], ai = xi[i1];
+      double br = yr[i0], bi = yi[i0], ar = yr[i1], ai = yi[i1];
       bfly(br, bi, ar, ai, cs[pos << shift], -sn[pos << shift]);
-      xr[i1] = ar;
-      xi[i1] = ai;
-      xr[i0] = br;
-      xi[i0] = bi;
+      yr[i1] = ar;
+      yi[i1] = ai;
+      yr[i0] = br;
+      yi[i0] = bi;
     }
     barrier();
   }
-  for (int k = tid; k <= N / 2; k += NT) {
+  const int nb = N / 2 + 1;
+  for (int e = tid; e < kv * nb; e += NT) {
+    const int k = e / nb, kk = e - k * nb;
+    const double* yr = xr + k * N;
+    const double* yi = xi + k * N;
+    C2* o = out + static_cast<int64_t>(k) * N;
     C2 v;
-    v.x = static_cast<Real>(xr[k]);
-    v.y = static_cast<Real>(xi[k]);
-    out[k] = v;
-    if (k != 0 && 2 * k != N) {
-      v.y = static_cast<Real>(-xi[k]);
-      out[N - k] = v;
+    v.x = static_cast<Real>(yr[kk]);
+    v.y = static_cast<Real>(yi[kk]);
+    o[kk] = v;
+    if (kk != 0 && 2 * kk != N) {
+      v.y = static_cast<Real>(-yi[kk]);
+      o[N - kk] = v;
     }
   }
+}
+
+// One row: in-place radix-2 DIT FFT of avg[0..N) (N a power of two) -> out (fft_rows with K = 1).
+template <typename Real, int NT, bool LDS_ONLY = false>
+__device__ void fft_row(const double* avg, const double* cs, const double* sn, int N, double* xr, double* xi,
+                        typename Complex2<Real>::type* out) {
+  fft_rows<Real, NT, LDS_ONLY>(avg, cs, sn, N, 1, 1, xr, xi, out);
 }
 
 }  // namespace

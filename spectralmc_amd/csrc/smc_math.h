@@ -152,27 +152,22 @@ __device__ __forceinline__ void twiddle(int64_t j, int64_t N, double& s_out, dou
 }
 
 // ---- f64 path engine: the Box-Muller transcendentals of 32-bit uniforms and exp ------------
-// Fixed IEEE-754 sequences (fma, +, -, *, exact ldexp and integer bit manipulation) over tables
-// (smc_f64_tables.h: generated in 60-digit decimal arithmetic, rounded to double), restated op for op
-// by oracle/gbm_oracle.c, so f64 normals are bit-identical on the CPU.  Accuracy against libm
+// Fixed IEEE-754 sequences (fma, +, -, *, exact scaling and integer bit manipulation) over tables
+// (smc_f64_tables.h: generated in 60-digit decimal arithmetic, rounded to double), restated op for op by
+// oracle/gbm_oracle.c, so f64 normals are bit-identical on the CPU.  Accuracy against libm
 // (tests/test_oracle.py): ln within 1 ulp, (sin, cos) within 2^-53 absolute, exp within 1 ulp.
-// Round 4: table indices and the exp split from integer bits (the magic-number rint, the mantissa's top
-// bits) instead of f64 rint/convert chains, a 64-angle sin/cos table with one more series term, and
-// the tables replicated in LDS so that a wave's random lookups do not collide on LDS banks: copy
-// (lane mod C) of entry e sits at [e][copy], so the 16 lanes of a ds_read_b128 group (the 32 of a
-// ds_read_b64 group) read distinct 16-B (8-B) slots when C = 16 (32); SMC_F64_COPIES sets C.  The
-// kernels that run this math copy the tables into LDS first (f64_tables_load): a global load on the
-// path loop would wait for the wave's outstanding path stores (one vmcnt counter).
-#ifndef SMC_F64_COPIES
-#define SMC_F64_COPIES 4
-#endif
-constexpr int kF64C = SMC_F64_COPIES;                   // copies of the 16-B entries (log, sin/cos)
-constexpr int kF64C8 = 2 * kF64C < 32 ? 2 * kF64C : 32;  // copies of the 8-B entries (ln lo, exp)
+// The f64 path kernel is VALU-issue-bound (PMC, round 4: the VALU busy ~95 % of the launch at ~4 cycles
+// per f64 instruction; LDS bank conflicts of the random table reads do not limit it), so round 4 trades
+// table size for polynomial terms: ln from a 256-point table (degree 6), sin / cos from a 1024-angle
+// table (to x^5 / x^4), exp to degree 5, table indices and the exp split from integer bits, the
+// Box-Muller uniform (a + 1/2) 2^-32 (never 0 or 1: no special case in the radius), and the exp's 2^m
+// applied to the path value as an exponent-field add.  The kernels that run this math copy the tables
+// into LDS first (f64_tables_load): a global load on the path loop would wait for the wave's outstanding
+// path stores (one vmcnt counter).
 struct alignas(16) F64Tables {
-  double2 log[64][kF64C];   // (INV, -ln(INV) hi) at c = 1 + i/64, i = -32..31 (entry i + 32)
-  double2 sc[64][kF64C];    // (sin, cos)(2 pi j / 64)
-  double loglo[64][kF64C8]; // -ln(INV) lo
-  double ex[64][kF64C8];    // 2^(j / 64)
+  double2 sc[1024];     // (sin, cos)(2 pi j / 1024)
+  double log[256][3];   // INV, -ln(INV) hi, lo at c = 1 + i/256, i = -128..127 (entry i + 128)
+  double ex[64];        // 2^(j / 64)
 };
 
 __device__ __forceinline__ F64Tables& f64_lds() {
@@ -183,55 +178,43 @@ __device__ __forceinline__ F64Tables& f64_lds() {
 // Every thread of the workgroup, before the workgroup's first f64 path math.
 __device__ inline void f64_tables_load() {
   F64Tables& t = f64_lds();
-  for (int k = threadIdx.x; k < 64 * kF64C; k += blockDim.x) {
-    const int e = k / kF64C, c = k % kF64C;
-    t.log[e][c] = double2{kF64LogTab[e][0], kF64LogTab[e][1]};
-    t.sc[e][c] = double2{kF64SinCos64Tab[e][0], kF64SinCos64Tab[e][1]};
-  }
-  for (int k = threadIdx.x; k < 64 * kF64C8; k += blockDim.x) {
-    const int e = k / kF64C8, c = k % kF64C8;
-    t.loglo[e][c] = kF64LogTab[e][2];
-    t.ex[e][c] = kF64Exp2Tab[e];
-  }
+  for (int k = threadIdx.x; k < 1024; k += blockDim.x) t.sc[k] = double2{kF64SinCosTab[k][0], kF64SinCosTab[k][1]};
+  for (int k = threadIdx.x; k < 256 * 3; k += blockDim.x) (&t.log[0][0])[k] = (&kF64LogTab[0][0])[k];
+  for (int k = threadIdx.x; k < 64; k += blockDim.x) t.ex[k] = kF64Exp2Tab[k];
   __syncthreads();
 }
 
-__device__ __forceinline__ int f64_copy16() { return static_cast<int>(threadIdx.x) & (kF64C - 1); }
-__device__ __forceinline__ int f64_copy8() { return static_cast<int>(threadIdx.x) & (kF64C8 - 1); }
-
-// ln((a + 1) 2^-32): m = a + 1 = 2^e f exactly (a double with <= 32 significant bits); with mh the top 20
-// mantissa bits, f >= 1 + 0x6A09F 2^-20 (just above sqrt 2) is halved (e + 1), so f is in [0.7071,
-// 1.4143); the table point c = 1 + i/64 nearest f is read off mh (round half up: i = (mh + 2^13) >> 14,
-// halved f: ((mh + 2^14) >> 15) - 32; i = 0 at f = 1, so no cancellation near u = 1); r = f INV - 1 in
-// one fma, ln(1 + r) to r^8 (|r| <= 0.0079), then (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))).
+// ln((a + 1/2) 2^-32): m = a + 1/2 = 2^e f exactly (<= 33 significant bits); with mh the top 20 mantissa
+// bits, f >= 1 + 0x6A09F 2^-20 (just above sqrt 2) is halved (e + 1), so f is in [0.7071, 1.4143); the
+// table point c = 1 + i/256 nearest f is read off mh (round half up: i = (mh + 2^11) >> 12, halved f:
+// ((mh + 2^12) >> 13) - 128; i = 0 at f = 1, so no cancellation near u = 1); r = f INV - 1 in one fma
+// (|r| <= 0.0028), ln(1 + r) to r^6, then (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))).
 __device__ __forceinline__ double log_u32(uint32_t a) {
-  const double m = static_cast<double>(a) + 1.0;  // exact: a + 1 <= 2^32
+  const double m = static_cast<double>(a) + 0.5;  // exact
   const uint64_t bits = __double_as_longlong(m);
   const uint32_t hw = static_cast<uint32_t>(bits >> 32);
   const uint32_t mh = hw & 0xFFFFFu;
   const uint32_t h = mh >= 0x6A09Fu ? 1u : 0u;  // halve f (branch-free: shifts and adds by h)
-  const int idx = static_cast<int>(((mh + (0x2000u << h)) >> (14u + h)) + 32u - 32u * h);
+  const int idx = static_cast<int>(((mh + (0x800u << h)) >> (12u + h)) + 128u - 128u * h);
   const int e = static_cast<int>((hw >> 20) + h) - 1023;
   const double f = __longlong_as_double(static_cast<long long>(
       (static_cast<uint64_t>(mh | (0x3FF00000u - (h << 20))) << 32) | (bits & 0xFFFFFFFFull)));
-  const double2 t = f64_lds().log[idx][f64_copy16()];
-  const double lo = f64_lds().loglo[idx][f64_copy8()];
-  const double r = fma(f, t.x, -1.0);
-  double q = -0.125;
-  q = fma(q, r, 0.14285714285714285);
-  q = fma(q, r, -0.16666666666666666);
+  const double* t = f64_lds().log[idx];
+  const double r = fma(f, t[0], -1.0);
+  double q = -0.16666666666666666;
   q = fma(q, r, 0.2);
   q = fma(q, r, -0.25);
   q = fma(q, r, 0.3333333333333333);
   q = fma(q, r, -0.5);
   const double p = fma(q, r * r, r);
   const double k = static_cast<double>(e - 32);
-  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, t.y + (lo + p)));
+  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, t[1] + (t[2] + p)));
 }
 
-// sqrt(x) for the Box-Muller radius x = -2 ln u in [0, 44.4]: the correctly rounded f64 sqrt sequence
-// (rsq seed, one Goldschmidt and two Newton-Raphson corrections) without the denormal / huge-argument
-// scaling that this range never needs, so the result is the IEEE sqrt the oracle takes.
+// sqrt(x) for the Box-Muller radius x = -2 ln u in [1.1e-10, 46.1] (u never 0 or 1): the correctly
+// rounded f64 sqrt sequence (rsq seed, one Goldschmidt and two Newton-Raphson corrections) without the
+// denormal / huge-argument scaling and the zero case this range never needs, so the result is the IEEE
+// sqrt the oracle takes.
 __device__ __forceinline__ double sqrt_radius(double x) {
   const double y = __builtin_amdgcn_rsq(x);
   double g = x * y, h = 0.5 * y;
@@ -241,53 +224,66 @@ __device__ __forceinline__ double sqrt_radius(double x) {
   double d = fma(-g, g, x);
   g = fma(d, h, g);
   d = fma(-g, g, x);
-  g = fma(d, h, g);
-  return x == 0.0 ? 0.0 : g;
+  return fma(d, h, g);
 }
 
-// (sin, cos)(2 pi b 2^-32): nearest table angle j = round(b / 2^26) (mod 64), rem = b - j 2^26 in
-// [-2^25, 2^25) exactly, x = rem (2 pi 2^-32) (|x| <= pi/64), sin x to x^9, cos x to x^8, then the
-// rotation by the table's (sin, cos)(2 pi j / 64).
+// (sin, cos)(2 pi b 2^-32): nearest of 1024 table angles j = round(b / 2^22) (mod 1024), rem = b - j 2^22
+// in [-2^21, 2^21) exactly, x = rem (2 pi 2^-32) (|x| <= pi/1024), sin x to x^5, cos x to x^4, then the
+// rotation by the table's (sin, cos)(2 pi j / 1024).
 __device__ __forceinline__ void sincos2pi_u32(uint32_t b, double& s_out, double& c_out) {
-  const uint32_t j = ((b + (1u << 25)) >> 26) & 63u;
-  const int32_t rem = static_cast<int32_t>(b - (j << 26));
+  const uint32_t j = ((b + (1u << 21)) >> 22) & 1023u;
+  const int32_t rem = static_cast<int32_t>(b - (j << 22));
   const double x = static_cast<double>(rem) * 1.4629180792671596e-09;  // 2 pi 2^-32 (exact scaling of 2 pi)
   const double u = x * x;
-  double sp = 2.7557319223985893e-06;
-  sp = fma(sp, u, -0.0001984126984126984);
-  sp = fma(sp, u, 0.008333333333333333);
-  sp = fma(sp, u, -0.16666666666666666);
+  const double sp = fma(u, 0.008333333333333333, -0.16666666666666666);
   const double sx = fma(sp * u, x, x);
-  double cp = 2.48015873015873e-05;
-  cp = fma(cp, u, -0.001388888888888889);
-  cp = fma(cp, u, 0.041666666666666664);
-  cp = fma(cp, u, -0.5);
+  const double cp = fma(u, 0.041666666666666664, -0.5);
   const double cx = fma(cp, u, 1.0);
-  const double2 sc = f64_lds().sc[j][f64_copy16()];
+  const double2 sc = f64_lds().sc[j];
   s_out = fma(sc.x, cx, sc.y * sx);
   c_out = fma(sc.y, cx, -(sc.x * sx));
 }
 
-// e^y: t = fma(y, 64 / ln 2, 1.5 2^52) rounds y 64 / ln 2 to the integer n = 64 m + j held in t's low
-// word (|n| < 2^31), n = t - 1.5 2^52 exactly; r = y - n ln2/64 (Cody-Waite: ln2/64 with 17 trailing zero
-// bits plus its remainder, each a fused step; |r| <= 0.0055), e^r - 1 to r^6, 2^(j/64) from the table,
-// exact ldexp by m.  No overflow handling: the path recursion's exponents stay within |y| < 700.
-__device__ __forceinline__ double exp_f64(double y) {
+// The split of e^y: t = fma(y, 64 / ln 2, 1.5 2^52) rounds y 64 / ln 2 to the integer n = 64 m + j held
+// in t's low word (|n| < 2^31), n = t - 1.5 2^52 exactly; r = y - n ln2/64 (Cody-Waite: ln2/64 with 17
+// trailing zero bits plus its remainder, each a fused step; |r| <= 0.0055), e^r - 1 to r^5; e^y =
+// 2^m T (1 + em1) with T = 2^(j/64) from the table.
+struct ExpSplit {
+  double T, em1;
+  int m;
+};
+__device__ __forceinline__ ExpSplit exp_split(double y) {
   const double t = fma(y, 92.33248261689366, 6755399441055744.0);
   const int ni = static_cast<int>(static_cast<uint32_t>(__double_as_longlong(t)));
   const double n = t - 6755399441055744.0;
-  const int j = ni & 63;
-  const int mm = ni >> 6;
   double r = fma(-n, 0.010830424696223417, y);
   r = fma(-n, 2.572804622327669e-14, r);
-  double q = 0.001388888888888889;
-  q = fma(q, r, 0.008333333333333333);
+  double q = 0.008333333333333333;
   q = fma(q, r, 0.041666666666666664);
   q = fma(q, r, 0.16666666666666666);
   q = fma(q, r, 0.5);
-  const double em1 = fma(q, r * r, r);
-  const double T = f64_lds().ex[j][f64_copy8()];
-  return ldexp(fma(T, em1, T), mm);
+  return ExpSplit{f64_lds().ex[ni & 63], fma(q, r * r, r), ni >> 6};
+}
+
+// 2^m x for a normal x and a normal result (no overflow / underflow on the path recursion, |y| < 700):
+// an add to the exponent field, equal to ldexp there.
+__device__ __forceinline__ double scale_exp2(double x, int m) {
+  const uint64_t bits = __double_as_longlong(x);
+  const uint32_t hi = static_cast<uint32_t>(bits >> 32) + (static_cast<uint32_t>(m) << 20);
+  return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | (bits & 0xFFFFFFFFull)));
+}
+
+// e^y (the f64 recursion of simple paths and the tests): T (1 + em1) scaled by 2^m.
+__device__ __forceinline__ double exp_f64(double y) {
+  const ExpSplit e = exp_split(y);
+  return scale_exp2(fma(e.T, e.em1, e.T), e.m);
+}
+
+// x e^y as the f64 log-Euler step: (x T) (1 + em1) scaled by 2^m.
+__device__ __forceinline__ double mul_exp_f64(double x, double y) {
+  const ExpSplit e = exp_split(y);
+  const double xt = x * e.T;
+  return scale_exp2(fma(xt, e.em1, xt), e.m);
 }
 
 }  // namespace math

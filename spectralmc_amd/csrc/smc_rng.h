@@ -12,7 +12,7 @@
 //                 (x, c) <- A x + c (mod 2^64 split into (x, c)), output x ^ c, A = 4294883355
 //   normals     = Box-Muller on consecutive u32 pairs (a, b):
 //                   u1 = 2 - 1.m(a >> 9) in (0, 1],  angle = (b >> 9) 2^-23 revolutions       (f32)
-//                   u1 = (a + 1) * 2^-32,                   u2 = b * 2^-32      (f64: smc_math.h)
+//                   u1 = (a + 1/2) * 2^-32,                 u2 = b * 2^-32      (f64: smc_math.h)
 //                   z0 = sqrt(-2 ln u1) cos(2 pi u2),  z1 = sqrt(-2 ln u1) sin(2 pi u2)
 //                 f32: ln / sin / cos are the portable kernels of smc_math.h, so the normals
 //                 are bit-identical to the CPU restatement.
@@ -156,7 +156,7 @@ struct PathStream {
     }
   }
 
-  // Two N(0,1) draws, double precision: u1 = (a + 1) 2^-32 in (0, 1], angle = b 2^-32 revolutions;
+  // Two N(0,1) draws, double precision: u1 = (a + 1/2) 2^-32 in (0, 1), angle = b 2^-32 revolutions;
   // ln u1 and (sin, cos) of the angle from the 32-bit integers (smc_math.h log_u32 / sincos2pi_u32,
   // restated by the CPU oracle: bit-identical normals), sqrt correctly rounded (sqrt_radius).
   template <bool HW>

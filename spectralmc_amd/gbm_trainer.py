@@ -427,6 +427,9 @@ class GbmCVNNPricer:
     #: the rest; 0: none) and their choice of CU ids ("low": the lowest logical ids, which measured
     #: best; "spread": evenly over the id range)
     network_cus: int = 32
+    #: the same for a wide fused network (a layer input of >= 256 real features: the layered MFMA GEMMs,
+    #: C2/H=256 ~0.26 ms of whole-chip work): more CUs, so the network still hides under the path kernel
+    network_cus_wide: int = 64
     network_cu_pattern: str = "low"
     #: launches whose workgroups wait for each other (the sliced resident kernel, C3; the resident
     #: basket kernel, C5) need every workgroup of a group co-resident.  A collective that spins on a
@@ -813,14 +816,15 @@ class TrainingSession:
             fused = self.program.fused
             narrow = fused is not None and max(t.in_features for t in fused.table) < 128
             cus = torch.cuda.get_device_properties(dev).multi_processor_count
-            if (pricer.network_cus > 0 and narrow and getattr(self.engine, "kernel_name", "") == "resident_kernel"
-                    and cus >= 4 * pricer.network_cus):
+            net_cus = pricer.network_cus if narrow else (pricer.network_cus_wide if fused is not None else 0)
+            if (net_cus > 0 and getattr(self.engine, "kernel_name", "") == "resident_kernel" and cus >= 2 * net_cus):
                 # the network on its own CUs beside the path kernels (CU-masked HIP streams); the path
                 # kernel sizes its persistent grid to its stream's CUs (gbm.hip resident_grid).  Only for
-                # the whole-contract resident launch (C2, the lock-step shape) and a narrow fused network
-                # (fb_kernel path: ~70 us of whole-chip work at C2); a wide one (C2/H=256: 0.27 ms) on 32
-                # CUs would outlast the path kernel (3.39 vs 3.30 ms/step)
-                net_mask, mc_mask = _cu_masks(dev, pricer.network_cus, pricer.network_cu_pattern)
+                # the whole-contract resident launch (C2, the lock-step shape) and a fused network: a
+                # narrow one (fb_kernel path, ~70 us of whole-chip work at C2) on network_cus, a wide one
+                # (C2/H=256: 0.26 ms) on network_cus_wide (on 32 CUs it outlasted the path kernel: 3.39
+                # vs 3.30 ms/step)
+                net_mask, mc_mask = _cu_masks(dev, net_cus, pricer.network_cu_pattern)
                 self.stream = _masked_stream(dev, net_mask, self._hip_streams)
                 self.mc_streams = [_masked_stream(dev, mc_mask, self._hip_streams) for _ in range(lanes)]
             else:

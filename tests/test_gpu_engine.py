@@ -563,6 +563,64 @@ def test_c2_f64_timed_call_matches_oracle(oracle, golden) -> None:
             assert _norm_rel(got[k:k + 1], want) < 1e-10, (step, b)
 
 
+PACKED_CASES = [  # (B, T, N, M, normalize, store): P < 4096 -> packed_kernel, K = 4096 / P contracts per workgroup
+    (4096, 16, 128, 4, 1, _lib.STORE_ALL),       # the reference's e2e shape (P = 512, K = 8) at a full batch
+    (1001, 16, 64, 4, 1, _lib.STORE_ALL),        # P = 256 (K = 16, one wave per contract), ragged last group
+    (300, 5, 256, 8, 0, _lib.STORE_TERMINAL),    # P = 2048 (K = 2), odd T (rolled rows), RAW, terminal rows
+    (77, 1, 16, 64, 1, _lib.STORE_ALL),          # T = 1, N = 16, P = 1024
+]
+
+
+@pytest.mark.parametrize("B,T,N,M,normalize,store", PACKED_CASES)
+def test_packed_train_step_matches_oracle(oracle, golden, B, T, N, M, normalize, store) -> None:
+    """Small P: smc_train_step runs K = 4096 / P whole contracts per 1024-thread
+    workgroup (packed_kernel, Sobol draw and cursor advance fused).  Portable math bit-exact with the
+    kernel-mode oracle in the packed order (one chunk of P / 4 lanes per contract: oracle.engine_wg);
+    hw math within 1e-5 of the reference mode; contracts equal the Sobol draw; the sync area is left
+    zeroed."""
+    L = _L()
+    P = N * M
+    pitch = int(L.smc_path_pitch(P, 0))
+    assert L.smc_train_step_kernel(T, N, M, 0, pitch) == b"packed_kernel"
+    assert oracle.engine_wg(T, N, P) == P // 4
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
+    lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
+    hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
+    shape = (B, T, pitch) if store == _lib.STORE_ALL else (B, pitch)
+    paths = torch.empty(shape, dtype=torch.float32, device=DEV)
+    nsync = int(L.smc_train_step_sync_bytes(T, N, M, 0, pitch))
+    sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
+    norm = _lib.NORM_NORMALIZE if normalize else _lib.NORM_RAW
+    for math in (0, _lib.MATH_HW):
+        cur = torch.tensor([40, 9], dtype=torch.int64, device=DEV)
+        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
+        f = torch.empty((B, 6), dtype=torch.float32, device=DEV)
+        t = torch.full((B, N), float("nan"), dtype=torch.complex64, device=DEV)
+        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
+                                    _lib.ptr(c), _lib.ptr(f), B, T, N, M, 7, _lib.SCHEME_LOG_EULER | math, norm,
+                                    _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, B, _lib.ptr(t), _lib.ptr(sync),
+                                    nsync, None))
+        torch.cuda.synchronize()
+        assert cur.tolist() == [40 + B, 9 + B]
+        assert not sync.view(torch.int32).any()
+        contracts = c.cpu().numpy()
+        np.testing.assert_array_equal(contracts, oracle.sobol_contracts(7, 40, B, golden["bounds_lower"],
+                                                                        golden["bounds_upper"]))
+        np.testing.assert_array_equal(f.cpu().numpy(), contracts.astype(np.float32))
+        got = t.cpu().numpy()
+        if math == 0:
+            kt, _ = oracle.kernel_targets(contracts, T, N, M, seed=7, ordinal0=9, normalize=bool(normalize),
+                                          wg=P // 4)
+            np.testing.assert_array_equal(got, kt)
+            if store == _lib.STORE_ALL:  # the stored rows are the kernel-mode paths
+                kp, _, _ = oracle.kernel_paths(contracts[:3], T, P, 7, ordinal0=9, want_paths=True, wg=P // 4)
+                np.testing.assert_array_equal(paths[:3, :, :P].cpu().numpy(), kp)
+        else:
+            want = oracle.training_targets(contracts[:24], T, N, M, seed=7, ordinal0=9, normalize=bool(normalize))
+            assert _norm_rel(got[:24], want) < 1e-5
+
+
 SLICED_CASES = [  # (B, N, M, store, chunk): shapes with P > 65,536 (W = P / 65,536 slices)
     (None, 1024, 256, _lib.STORE_ALL, None),   # C3 per-contract shape, W = 4, > 1 contract per group
     (70, 1024, 256, _lib.STORE_ALL, 24),       # C3 shape in three chunk launches
