@@ -470,12 +470,12 @@ __device__ void simulate_contract(const EngineArgs& a, const Contract& c, uint64
 // ---- phases 2+3: normalised put payoff, mean over M batches, real-input DFT ------------
 // Reference scalar semantics: gbm.py:429-431 evaluate times/forwards/df in the sim dtype;
 // the put is df * max(K - x * scale, 0) with x * scale rounded to the sim dtype (gbm.py:437, 473).
+// The contract's payoff constants that do not need the terminal sum (forward F_T, discount df_T,
+// strike), taken before a contract's simulation so the f64 contract row need not stay live across it.
 template <typename Real>
-struct Payoff {
-  Real s, K, df;
-  Payoff() = default;
-  __device__ Payoff(const EngineArgs& a, const Contract& c, double terminal_sum) {
-    Real F;
+struct PayoffPre {
+  Real F, df, K;
+  __device__ explicit PayoffPre(const Contract& c) {
     const Real Tm = static_cast<Real>(c.T);
     if constexpr (sizeof(Real) == 4) {
       F = static_cast<float>(c.X0) * math::exp_any(static_cast<float>(c.r - c.d) * Tm);
@@ -484,8 +484,20 @@ struct Payoff {
       F = c.X0 * exp((c.r - c.d) * Tm);
       df = exp(-c.r * Tm);
     }
-    s = a.normalize ? F / static_cast<Real>(terminal_sum / static_cast<double>(a.P)) : Real(1);
     K = static_cast<Real>(c.K);
+  }
+};
+
+template <typename Real>
+struct Payoff {
+  Real s, K, df;
+  Payoff() = default;
+  __device__ Payoff(const EngineArgs& a, const Contract& c, double terminal_sum)
+      : Payoff(a, PayoffPre<Real>(c), terminal_sum) {}
+  __device__ Payoff(const EngineArgs& a, const PayoffPre<Real>& pre, double terminal_sum) {
+    df = pre.df;
+    s = a.normalize ? pre.F / static_cast<Real>(terminal_sum / static_cast<double>(a.P)) : Real(1);
+    K = pre.K;
     // a failed exchange hands over a NaN terminal sum: keep the targets NaN (df * max(K - NaN, 0)
     // would be 0, a plausible value) so a caller that skips smc_sync_status still sees it
     if (terminal_sum != terminal_sum) df = static_cast<Real>(__builtin_nan(""));
@@ -1039,7 +1051,8 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     float term[kResRegChunks][kPathsPerLane];
     double acc[1] = {0.0};
     double colsum[kPathsPerLane] = {0.0, 0.0, 0.0, 0.0};
-    const Payoff<float> pay_raw(a, c, 1.0);  // ONTHEFLY: RAW, the terminal sum is not needed
+    const PayoffPre<float> pre(c);                // all the payoff needs of c after the chunk loop
+    const Payoff<float> pay_raw(a, pre, 1.0);  // ONTHEFLY: RAW, the terminal sum is not needed
     for (int ch = 0; ch < nch; ++ch) {
       float xt[kPathsPerLane];
       if constexpr (T16)  // the straight-line 16-row block (the benchmark shape)
@@ -1109,7 +1122,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       lds_barrier();
       tot = row[6];
     }
-    const Payoff<float> pay(a, c, tot);
+    const Payoff<float> pay(a, pre, tot);
     if constexpr (!ONTHEFLY) {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) colsum[j] = 0.0;  // (the zeros before the loop are dead here)

@@ -92,7 +92,7 @@ for step in "$@"; do
       IFS=: read -r _ tag args names <<< "$step"
       run "ab_$tag" 900 bash tools/micro/ab.sh "$OUT/ab_$tag.txt" "${args//,/ }" ${names//,/ } ;;
     pmcv:*)  # pmcv:<variant|default>:<kprof_step args with ,>:<counters with ,> -> one PMC pass
-      IFS=: read -r _ var args ctrs <<< "$step"; tag="${var}_$(echo "$ctrs" | tr ',' '_' | cut -c1-40)"
+      IFS=: read -r _ var args ctrs <<< "$step"; tag="${var}_$(echo "$ctrs" | tr ',' '_' | cut -c1-40)_$(echo "$args" | md5sum | cut -c1-6)"
       if [ "$var" = default ]; then lib=$ROOT/spectralmc_amd/libspectralmc_hip.so; else lib=$ROOT/tools/micro/v/libsmc_$var.so; fi
       cd /tmp && SMC_LIB_PATH=$lib run "pmcv_$tag" 120 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } -d "$OUT/pmcv_$tag" -o run --output-format csv -- python "$ROOT/tools/kprof_step.py" ${args//,/ }; cd "$ROOT" ;;
     *) echo "unknown step $step"; exit 2 ;;
