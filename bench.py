@@ -381,7 +381,7 @@ def main() -> None:
                    "note": "small complex GEMMs (K = 12..512) plus the targets read, timed alone; " + (
                        "in the step it runs after the path kernel on the same stream (rows_kernel holds every "
                        "CU slot for its whole duration; gbm_trainer.py)"
-                       if session.engine.kernel_name == "rows_kernel+cf_kernel" or not pricer.overlap_mc else
+                       if session.engine.kernel_name.startswith("rows_") or not pricer.overlap_mc else
                        "in the step it is enqueued on its own stream and its workgroups take the CUs the path "
                        "kernels leave (32 CU-masked CUs at C2; else the tails)")}
 

@@ -807,7 +807,7 @@ class TrainingSession:
         # duration (persistent, 8 waves per SIMD, contracts from a queue): a concurrent network part
         # gets no tail to run in and only stretches it (C2 in f64: 10.55 ms/step overlapped, 10.35
         # sequential), so those shapes run the step on one stream
-        overlap = pricer.overlap_mc and getattr(self.engine, "kernel_name", "") != "rows_kernel+cf_kernel"
+        overlap = pricer.overlap_mc and not getattr(self.engine, "kernel_name", "").startswith("rows_")
         if overlap:
             # the network part is a few short launches: a high-priority queue lets its workgroups
             # take CU slots as the long MC kernel frees them instead of queueing behind it
