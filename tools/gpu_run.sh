@@ -95,6 +95,10 @@ for step in "$@"; do
       IFS=: read -r _ var args ctrs <<< "$step"; tag="${var}_$(echo "$ctrs" | tr ',' '_' | cut -c1-40)_$(echo "$args" | md5sum | cut -c1-6)"
       if [ "$var" = default ]; then lib=$ROOT/spectralmc_amd/libspectralmc_hip.so; else lib=$ROOT/tools/micro/v/libsmc_$var.so; fi
       cd /tmp && SMC_LIB_PATH=$lib run "pmcv_$tag" 120 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } -d "$OUT/pmcv_$tag" -o run --output-format csv -- python "$ROOT/tools/kprof_step.py" ${args//,/ }; cd "$ROOT" ;;
+    testlib:*)  # testlib:<variant|default>:<pytest -k expression with , for spaces> (GPU tests on a variant library)
+      IFS=: read -r _ var expr <<< "$step"
+      if [ "$var" = default ]; then lib=$ROOT/spectralmc_amd/libspectralmc_hip.so; else lib=$ROOT/tools/micro/v/libsmc_$var.so; fi
+      SMC_LIB_PATH=$lib run "testlib_$var" 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider -rf -k "${expr//,/ }" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
