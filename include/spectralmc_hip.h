@@ -185,14 +185,17 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
 int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
                                   int32_t dtype, int64_t path_pitch);
 /* Name of the kernel smc_train_step launches for this shape ("resident_kernel",
- * "resident_kernel(sliced)", or smc_train_targets_kernel's name).  Static string. */
+ * "resident_kernel(sliced)", or smc_train_targets_kernel's name).  Static string.  dtype may carry
+ * SMC_QUERY_RAW: the shape's targets use RAW normalisation (one-wave-per-contract shapes). */
+#define SMC_QUERY_RAW 0x100
 const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
                                   int32_t dtype, int64_t path_pitch);
 /* Workspace bytes smc_train_targets needs for sliced contracts (0: P too small to slice). */
 int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, int64_t n_paths,
                                    int32_t all_rows);
-/* Name of the kernel smc_train_targets launches for this shape ("contract_kernel" or
- * "queue_kernel"; sliced = a workspace is passed).  Static string. */
+/* Name of the kernel smc_train_targets launches for this shape ("wave_kernel", "resident_kernel",
+ * "packed_kernel", the split pairs, "contract_kernel" or "queue_kernel"; sliced = a workspace is
+ * passed; dtype | SMC_QUERY_RAW as for smc_train_step_kernel).  Static string. */
 const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, int64_t n_paths,
                                      int32_t dtype, int64_t path_pitch, int32_t sliced);
 /* Recommended row pitch (elements) for a path scratch buffer of n_paths columns: the row

@@ -261,14 +261,17 @@ def kernel_cf(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndar
 
 
 def engine_wg(timesteps: int, network_size: int, n_paths: int, with_rowsum: bool = False,
-              sliced: bool = False) -> int:
+              sliced: bool = False, normalize: bool = True) -> int:
     """Lanes whose reduction order an f32 training launch of smc_train_targets follows: 1024 for
     resident_kernel (1 <= T <= 65,536, 4096 | P <= 65,536, N | 4096, 4 <= N <= 1024, no row sums, no
     workspace; gbm.hip resident_ok), P / 4 for packed_kernel (256 <= P <= 2048, P | 4096, 4 | N, N | P:
-    one chunk of P / 4 lanes per contract; gbm.hip packed_ok), 512 otherwise."""
+    one chunk of P / 4 lanes per contract; gbm.hip packed_ok), 64 for wave_kernel (RAW, T <= 2, 256 | P,
+    4 | N, N | 256: one wave per contract; gbm.hip wave_ok), 512 otherwise."""
     N, P = network_size, n_paths
     if with_rowsum or sliced or not 1 <= timesteps <= 65536:
         return 512
+    if not normalize and timesteps <= 2 and P % 256 == 0 and N >= 4 and N % 4 == 0 and 256 % N == 0:
+        return 64
     if P % 4096 == 0 and P // 4096 <= 16 and 4 <= N <= 1024 and 4096 % N == 0:
         return 1024
     if 256 <= P <= 2048 and 4096 % P == 0 and N >= 4 and N % 4 == 0 and P % N == 0:
@@ -276,7 +279,7 @@ def engine_wg(timesteps: int, network_size: int, n_paths: int, with_rowsum: bool
     return 512
 
 
-def train_step_order(timesteps: int, network_size: int, n_paths: int) -> tuple[int, int]:
+def train_step_order(timesteps: int, network_size: int, n_paths: int, normalize: bool = True) -> tuple[int, int]:
     """(wg, slices) of the f32 resident launch smc_train_step makes for this shape (gbm.hip
     resident_slices / resident_ok: W = the fewest power-of-two slices of <= 65,536 paths, W <= 8),
     or (engine_wg(...), 1) where it falls back to the separate draw + smc_train_targets calls."""
@@ -284,9 +287,11 @@ def train_step_order(timesteps: int, network_size: int, n_paths: int) -> tuple[i
     W = 1
     while W < 8 and P > W * 65536:
         W *= 2
+    if engine_wg(timesteps, N, P, normalize=normalize) == 64:
+        return 64, 1
     ok = (1 <= timesteps <= 65536 and P % (W * 4096) == 0 and P // (W * 4096) <= 16 and 4 <= N <= 1024
           and 4096 % N == 0)
-    return (1024, W) if ok else (engine_wg(timesteps, N, P), 1)
+    return (1024, W) if ok else (engine_wg(timesteps, N, P, normalize=normalize), 1)
 
 
 def kernel_targets(contracts: np.ndarray, timesteps: int, network_size: int, batches: int, seed: int,

@@ -33,6 +33,7 @@ NORM_RAW = 0
 NORM_NORMALIZE = 1
 DTYPE_F32 = 0
 DTYPE_F64 = 1
+QUERY_RAW = 0x100  # smc_train_step_kernel / smc_train_targets_kernel: the targets use RAW normalisation
 STORE_TERMINAL = 1
 MATH_HW = 0x100
 TRAIN_DYNAMIC = 0x200

@@ -1344,6 +1344,106 @@ __global__ __launch_bounds__(kResThreads) void packed_kernel(EngineArgs a) {
   }
 }
 
+// ---- wave_kernel: one wave per contract (RAW normalisation, T <= 2) -------------------------------
+// RAW targets need no terminal sum, so a contract's payoffs can be added up as its paths finish, and a
+// whole contract fits one wave: its 64 lanes walk the contract in 256-path chunks (4 paths per lane),
+// add each chunk's payoffs to the lane's four column sums, and after the last chunk the wave alone takes
+// the M-mean and the FFT from its own LDS -- no workgroup barrier per contract.  At the reference's
+// lock-step shape (T = 1, N = 16, M = 4096, RAW: tests/test_gbm_trainer.py:122-142) the 1024-thread
+// resident kernel's per-contract barriers and serial CF phase cost as much as the paths themselves
+// (profiles/r04/ab_lockstep_decomposition.txt).  Orders (oracle kernel mode, wg = 64): item (q, g) =
+// (lane mod N/4, 4 lane / N) adds batch rows m = g, g + 256/N, ... ascending from 0.0 (chunk order), the
+// column sums add g in order from 0.0, the M-mean, then the FFT of fft_row.  Persistent: wave w of the
+// grid runs contracts w, w + (all waves), ...; with a.sobol (smc_train_step) each wave draws its
+// contract's Sobol row and the last workgroup advances the cursor.
+constexpr int kWaveThreads = 256;
+constexpr int kWaveChunk = 64 * kPathsPerLane;  // 256 paths per chunk
+constexpr int kWaveMaxT = 2;
+
+size_t wave_lds_bytes(int N) {
+  const size_t per_wave = kWaveChunk + 3 * static_cast<size_t>(N) + 8;  // part [G][N], avg, re, im, row
+  return (static_cast<size_t>(kWaveThreads / 64) * per_wave + 2 * static_cast<size_t>(N)) * sizeof(double);
+}
+
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
+__global__ __launch_bounds__(kWaveThreads) void wave_kernel(EngineArgs a) {
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int N = a.N, M = a.M, T = a.T;
+  const int64_t P = a.P;
+  const int64_t pitch = a.pitch ? a.pitch : P;
+  const int cols = N / 4, G = kWaveChunk / N;  // column quads, batch rows per chunk
+  const int q = lane % cols, g = lane / cols;
+  const int per_wave = kWaveChunk + 3 * N + 8;
+  double* part = lds + wave * per_wave;  // [G][N]
+  double* avg = part + kWaveChunk;       // [N]
+  double* re = avg + N;                  // [N]
+  double* im = re + N;                   // [N]
+  double* row = im + N;                  // [6] the drawn Sobol row
+  double* cs = lds + (kWaveThreads / 64) * per_wave;
+  double* sn = cs + N;
+  for (int j = threadIdx.x; j < N; j += kWaveThreads) math::twiddle(j, N, sn[j], cs[j]);
+  __syncthreads();
+  const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
+  const int64_t sob0 = a.sobol ? a.cursor[0] + a.sobol_index0 : 0;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * (kWaveThreads / 64);
+  for (int64_t b = static_cast<int64_t>(blockIdx.x) * (kWaveThreads / 64) + wave; b < a.B; b += nw) {
+    Contract c;
+    if (a.sobol) {  // sobol_sampler.py:222-246, one lane per dimension
+      if (lane < 6) {
+        const double v = sobol_coord(a.sobol, a.sobol_dim, lane, static_cast<uint64_t>(sob0 + b), a.lower, a.upper);
+        row[lane] = v;
+        a.contracts_out[b * 6 + lane] = v;
+        if (a.cvnn_out) a.cvnn_out[b * 6 + lane] = static_cast<float>(v);
+      }
+      wave_lds_sync();
+      c = Contract{row[0], row[1], row[2], row[3], row[4], row[5]};
+    } else {
+      c = load_contract(a.contracts + b * 6);
+    }
+    const Stepper<float, LOG_EULER, HW> step(c, T);
+    const float x0 = static_cast<float>(c.X0);
+    const Payoff<float> pay(a, PayoffPre<float>(c), 1.0);  // RAW: scale 1
+    float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * T * pitch : b * pitch);
+    double colsum[kPathsPerLane] = {0.0, 0.0, 0.0, 0.0};
+    double acc = 0.0;  // (the terminal sum: not needed for RAW targets)
+    for (int64_t chunk = 0; chunk < P; chunk += kWaveChunk) {
+      float xt[kPathsPerLane];
+      lane_rows<float, LOG_EULER, HW, STORE_ALL>(a, step, x0, static_cast<uint64_t>(ord0 + b), chunk, base, T, pitch,
+                                                 acc, xt, lane);
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) colsum[j] += static_cast<double>(pay(xt[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < kPathsPerLane; ++j) part[g * N + 4 * q + j] = colsum[j];
+    wave_lds_sync();
+    for (int n = lane; n < N; n += 64) {
+      double t = 0.0;
+      for (int gg = 0; gg < G; ++gg) t += part[gg * N + n];
+      avg[n] = t / static_cast<double>(M);
+    }
+    wave_lds_sync();
+    fft_rows<float, 64, true, true>(avg, cs, sn, N, 1, 1, re, im, static_cast<float2*>(a.targets) + b * N);
+    wave_lds_sync();  // part / avg / re / im are rewritten by the wave's next contract
+  }
+  __syncthreads();  // every wave of the workgroup is done with its contracts
+  if (a.done && threadIdx.x == 0) {
+    // every workgroup read the cursor before it arrives here: the last one advances it
+    __threadfence();
+    if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
+      a.cursor[0] += a.advance;
+      a.cursor[1] += a.advance;
+      *a.done = 0u;
+    }
+  }
+}
+
+bool wave_ok(const EngineArgs& a, bool f32) {
+  return f32 && a.simulate && a.targets && !a.normalize && !a.all_rows && a.slices <= 1 && a.res_slices <= 1 &&
+         a.T >= 1 && a.T <= kWaveMaxT && a.P % kWaveChunk == 0 && a.N >= 4 && a.N % 4 == 0 &&
+         kWaveChunk % a.N == 0 && (a.pitch == 0 || (a.pitch % 4 == 0 && a.pitch >= a.P));
+}
+
 bool packed_ok(const EngineArgs& a, bool f32) {
   return f32 && a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.res_slices <= 1 && a.T >= 1 &&
          a.T <= kResMaxT && a.P >= kPackMinP && a.P <= kPackMaxP && kResChunk % a.P == 0 && a.N >= 4 &&
@@ -1709,6 +1809,25 @@ int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
 }
 
 template <bool LOG_EULER, bool HW, bool STORE_ALL>
+int32_t launch_wave_k(const EngineArgs& a, hipStream_t stream) {
+  auto kernel = wave_kernel<LOG_EULER, HW, STORE_ALL>;
+  const size_t lds = wave_lds_bytes(a.N);
+  if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             static_cast<int>(lds)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "wave_kernel: cannot raise the dynamic LDS limit");
+  }
+  unsigned grid = 0;
+  const int64_t wpg = kWaveThreads / 64;
+  if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kWaveThreads, lds, (a.B + wpg - 1) / wpg, &grid,
+                                 stream))
+    return st;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWaveThreads), lds, stream, a);
+  return check_launch("wave_kernel");
+}
+
+template <bool LOG_EULER, bool HW, bool STORE_ALL>
 int32_t launch_packed_k(const EngineArgs& a, hipStream_t stream) {
   auto kernel = a.T == kRowBlock ? packed_kernel<LOG_EULER, HW, STORE_ALL, true>
                                  : packed_kernel<LOG_EULER, HW, STORE_ALL, false>;
@@ -1739,6 +1858,22 @@ template <typename Real>
 int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   if (a.B == 0) return SMC_OK;
   if constexpr (sizeof(Real) == 4) {
+    if (SMC_TRAIN_MODE == 3 && wave_ok(a, true)) {  // RAW, T <= 2: one wave per contract
+      const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+      const bool hw = (a.scheme & SMC_MATH_HW) != 0;
+      const bool sa = a.store == SMC_STORE_ALL;
+#define SMC_WAVE(LE, HWM, SA) \
+  if (log_euler == LE && hw == HWM && sa == SA) return launch_wave_k<LE, HWM, SA>(a, stream);
+      SMC_WAVE(true, true, true)
+      SMC_WAVE(true, true, false)
+      SMC_WAVE(true, false, true)
+      SMC_WAVE(true, false, false)
+      SMC_WAVE(false, true, true)
+      SMC_WAVE(false, true, false)
+      SMC_WAVE(false, false, true)
+      SMC_WAVE(false, false, false)
+#undef SMC_WAVE
+    }
     if (SMC_TRAIN_MODE == 3 && resident_ok(a, true)) {
       const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
       const bool hw = (a.scheme & SMC_MATH_HW) != 0;
@@ -2041,7 +2176,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
   }
   const bool fused = SMC_TRAIN_MODE == 3 && dtype == SMC_DTYPE_F32 && n_contracts > 0 && chunk_contracts > 0 &&
                      valid_scheme(scheme) && (store_mode == SMC_STORE_ALL || store_mode == SMC_STORE_TERMINAL) &&
-                     paths_dev && targets_dev && (resident_ok(a, true) || packed_ok(a, true));
+                     paths_dev && targets_dev && (wave_ok(a, true) || resident_ok(a, true) || packed_ok(a, true));
   if (fused) {
     // one resident launch per chunk of contracts; each draws its own contracts, the last advances
     // the cursor (the earlier ones read it unchanged)
@@ -2117,6 +2252,8 @@ const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32
   a.res_cnt = reinterpret_cast<uint32_t*>(&a);
   a.res_xsum = a.res_xcol = reinterpret_cast<double*>(&a);
   a.done = reinterpret_cast<uint32_t*>(&a);
+  a.normalize = (dtype & SMC_QUERY_RAW) ? 0 : 1;
+  if (SMC_TRAIN_MODE == 3 && wave_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "wave_kernel";
   if (SMC_TRAIN_MODE == 3 && resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))
     return a.res_slices > 1 ? "resident_kernel(sliced)" : "resident_kernel";
   return smc_train_targets_kernel(timesteps, network_size, a.P, dtype, path_pitch, 0);
@@ -2139,6 +2276,8 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.slices = slices_for(n_paths, sliced != 0);
   a.store = SMC_STORE_ALL;
   const bool f32 = (dtype & 0xff) == SMC_DTYPE_F32;
+  a.normalize = (dtype & SMC_QUERY_RAW) ? 0 : 1;
+  if (SMC_TRAIN_MODE == 3 && wave_ok(a, f32)) return "wave_kernel";
   if (SMC_TRAIN_MODE == 3 && resident_ok(a, f32)) return "resident_kernel";
   if (SMC_TRAIN_MODE == 3 && packed_ok(a, f32)) return "packed_kernel";
   if (SMC_TRAIN_MODE >= 2 && split_ok(a, f32) && a.T == kRowBlock && a.P % kChunk == 0) return "paths_kernel+cf_kernel";

@@ -100,16 +100,26 @@ __device__ __forceinline__ void lds_barrier() {  // LDS visibility only: no vmcn
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// One wave's LDS hand-off (no workgroup barrier): its own LDS writes complete and visible to its lanes.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
 // K rows at once (avg, xr, xi: [K][N]; out: [kv][N], rows k < kv written): the per-row arithmetic and
 // order of one row, the (row, index) pairs spread over the NT threads (packed_kernel's contracts).
-template <typename Real, int NT, bool LDS_ONLY = false>
+// WAVE: one wave runs it alone (NT = 64, lane index, wave-local LDS hand-offs, no s_barrier).
+template <typename Real, int NT, bool LDS_ONLY = false, bool WAVE = false>
 __device__ void fft_rows(const double* avg, const double* cs, const double* sn, int N, int K, int kv, double* xr,
                          double* xi, typename Complex2<Real>::type* out) {
   using C2 = typename Complex2<Real>::type;
-  const int tid = threadIdx.x;
+  static_assert(!WAVE || NT == 64, "a wave-local FFT runs on the 64 lanes of one wave");
+  const int tid = WAVE ? static_cast<int>(threadIdx.x & 63) : static_cast<int>(threadIdx.x);
   const int logN = 31 - __builtin_clz(static_cast<unsigned>(N));
   auto barrier = [] {
-    if constexpr (LDS_ONLY) lds_barrier();
+    if constexpr (WAVE) wave_lds_sync();
+    else if constexpr (LDS_ONLY) lds_barrier();
     else __syncthreads();
   };
   for (int e = tid; e < K * N; e += NT) {

@@ -46,6 +46,11 @@ def path_buffer_budget(device: torch.device) -> int:
     return torch.cuda.get_device_properties(device).total_memory // 2
 
 
+# persistent launches whose workgroups never wait for each other (whole contracts per workgroup or per
+# wave): MC lanes and the CU-masked network streams apply to them
+WHOLE_CONTRACT_KERNELS = ("resident_kernel", "wave_kernel", "packed_kernel")
+
+
 @dataclass(frozen=True)
 class StepBuffers:
     contracts: torch.Tensor   # (B, 6) f64, BlackScholes.Inputs field order
@@ -121,12 +126,12 @@ class TrainingEngine:
         # zero-filled once; every step leaves its counters zeroed
         self._uses_train_step = self._f32_in and self.dim == 6 and self._workspace is None
         # the path/CF kernel the step runs for this shape (bench labels, rocprof cross-check)
+        query = self._dtype_code | (_lib.QUERY_RAW if self._norm == _lib.NORM_RAW else 0)
         if self._uses_train_step:
-            self.kernel_name = _lib.lib().smc_train_step_kernel(self.T, self.N, self.M, self._dtype_code,
-                                                                self.pitch).decode()
+            self.kernel_name = _lib.lib().smc_train_step_kernel(self.T, self.N, self.M, query, self.pitch).decode()
         else:
             self.kernel_name = _lib.lib().smc_train_targets_kernel(
-                self.T, self.N, self.P, self._dtype_code, self.pitch, 1 if ws else 0).decode()
+                self.T, self.N, self.P, query, self.pitch, 1 if ws else 0).decode()
         # MC lanes: consecutive steps alternate over `lanes` sets of {cursor, sync area, path scratch}, so
         # a caller may run step s + 1's launch on another stream while step s's is still in its tail
         # (the next launch's workgroups take the CUs the last contracts free).
@@ -134,7 +139,7 @@ class TrainingEngine:
         # lanes * global_batch.  Only for one whole-contract resident launch per step (no exchange
         # between workgroups, which needs every workgroup of a group co-resident) within the budget.
         self.lanes = 1
-        if (lanes > 1 and self._uses_train_step and self.kernel_name == "resident_kernel" and self.chunk >= B
+        if (lanes > 1 and self._uses_train_step and self.kernel_name in WHOLE_CONTRACT_KERNELS and self.chunk >= B
                 and lanes * per_contract * self.chunk <= budget):
             self.lanes = lanes
         self._next_lane = 0
@@ -238,4 +243,5 @@ def check_sync_status(sync: torch.Tensor | None, stream: torch.cuda.Stream | Non
                             "targets hold NaN (were all workgroups of a group co-resident?)")
 
 
-__all__ = ["TrainingEngine", "StepBuffers", "DEFAULT_PATH_BUFFER_BYTES", "check_sync_status", "path_buffer_budget"]
+__all__ = ["TrainingEngine", "StepBuffers", "DEFAULT_PATH_BUFFER_BYTES", "WHOLE_CONTRACT_KERNELS", "check_sync_status",
+           "path_buffer_budget"]

@@ -36,7 +36,7 @@ import torch
 from pydantic import BaseModel, ConfigDict, PositiveInt, ValidationError
 
 from . import _lib
-from .engine import StepBuffers, TrainingEngine
+from .engine import WHOLE_CONTRACT_KERNELS, StepBuffers, TrainingEngine
 from .errors.gbm import EngineFailure, NormalsUnavailable
 from .errors.sampler import SamplerValidationFailed, SequenceExhausted
 from .errors.trainer import (
@@ -817,7 +817,8 @@ class TrainingSession:
             narrow = fused is not None and max(t.in_features for t in fused.table) < 128
             cus = torch.cuda.get_device_properties(dev).multi_processor_count
             net_cus = pricer.network_cus if narrow else (pricer.network_cus_wide if fused is not None else 0)
-            if (net_cus > 0 and getattr(self.engine, "kernel_name", "") == "resident_kernel" and cus >= 2 * net_cus):
+            if (net_cus > 0 and getattr(self.engine, "kernel_name", "") in WHOLE_CONTRACT_KERNELS
+                    and cus >= 2 * net_cus):
                 # the network on its own CUs beside the path kernels (CU-masked HIP streams); the path
                 # kernel sizes its persistent grid to its stream's CUs (gbm.hip resident_grid).  Only for
                 # the whole-contract resident launch (C2, the lock-step shape) and a fused network: a

@@ -179,7 +179,12 @@ def test_train_targets_kernel_choice() -> None:
     assert L.smc_train_targets_kernel(16, 256, 65536, 0, 66560, 1) == b"queue_kernel"
     rows = b"rows_kernel+cf_kernel"
     assert L.smc_train_targets_kernel(17, 256, 65536, 0, 0, 0) == b"resident_kernel"        # any T
-    assert L.smc_train_targets_kernel(1, 16, 65536, 0, 66560, 0) == b"resident_kernel"      # lock-step shape
+    assert L.smc_train_targets_kernel(1, 16, 65536, 0, 66560, 0) == b"resident_kernel"      # lock-step, NORMALIZE
+    raw = _lib.QUERY_RAW
+    assert L.smc_train_targets_kernel(1, 16, 65536, raw, 66560, 0) == b"wave_kernel"        # lock-step, RAW
+    assert L.smc_train_step_kernel(1, 16, 4096, raw, 66560) == b"wave_kernel"
+    assert L.smc_train_targets_kernel(3, 16, 65536, raw, 66560, 0) == b"resident_kernel"    # RAW, T > 2
+    assert L.smc_train_targets_kernel(16, 128, 512, 0, 1024, 0) == b"packed_kernel"         # e2e shape, P = 512
     assert L.smc_train_targets_kernel(17, 2048, 65536, 0, 66560, 0) == rows                 # N > 1024, T != 16
     assert L.smc_train_targets_kernel(17, 2048, 65536, 0, 0, 0) == b"contract_kernel"       # no padding
     assert L.smc_train_targets_kernel(16, 256, 65536, 1, 66048, 0) == b"rows_fused_kernel"  # f64 (CF fused)

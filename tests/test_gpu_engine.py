@@ -286,7 +286,7 @@ def test_multi_round_launches_match_oracle(oracle, golden, B, T, N, M, scheme, n
     c = _contracts(oracle, golden, B, seed=7, skip=3)
     got, _, _ = _run_targets(c, T, N, M, scheme, normalize, "float32", store, ordinal0=9, with_rowsum=False)
     kt, _ = oracle.kernel_targets(c, T, N, M, seed=7, ordinal0=9, scheme=scheme, normalize=bool(normalize),
-                                  wg=oracle.engine_wg(T, N, N * M))
+                                  wg=oracle.engine_wg(T, N, N * M, normalize=bool(normalize)))
     np.testing.assert_array_equal(got, kt)
     # padded pitch and chunked launches: same bits
     pitch = int(_L().smc_path_pitch(N * M, 0))
@@ -620,6 +620,66 @@ def test_packed_train_step_matches_oracle(oracle, golden, B, T, N, M, normalize,
         else:
             want = oracle.training_targets(contracts[:24], T, N, M, seed=7, ordinal0=9, normalize=bool(normalize))
             assert _norm_rel(got[:24], want) < 1e-5
+
+
+WAVE_CASES = [  # (B, T, N, M, store): RAW, T <= 2 -> wave_kernel, one wave per contract
+    (4096, 1, 16, 4096, _lib.STORE_ALL),      # the reference's lock-step shape at C2's batch (bench "lockstep")
+    (333, 2, 64, 64, _lib.STORE_ALL),          # T = 2, more contracts than one per wave? (no: < 4096 waves)
+    (5000, 1, 256, 16, _lib.STORE_TERMINAL),   # more contracts than resident waves: two rounds; N = 256
+]
+
+
+@pytest.mark.parametrize("B,T,N,M,store", WAVE_CASES)
+def test_wave_train_step_matches_oracle(oracle, golden, B, T, N, M, store) -> None:
+    """RAW targets at T <= 2 (the reference's lock-step trainer shape, tests/test_gbm_trainer.py:122-142):
+    smc_train_step runs one wave per contract (wave_kernel: payoffs added as the chunks finish, the
+    M-mean and FFT by the wave alone).  Portable math bit-exact with the kernel-mode oracle in the wave's
+    order (wg = 64); hw math within 1e-5 of the reference mode; contracts equal the Sobol draw; the
+    stored terminal rows equal the kernel-mode paths; the sync area is left zeroed."""
+    L = _L()
+    P = N * M
+    pitch = int(L.smc_path_pitch(P, 0))
+    assert L.smc_train_step_kernel(T, N, M, _lib.QUERY_RAW, pitch) == b"wave_kernel"
+    assert L.smc_train_step_kernel(T, N, M, 0, pitch) != b"wave_kernel"  # NORMALIZE needs the terminal sum first
+    assert oracle.train_step_order(T, N, P, normalize=False) == (64, 1)
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
+    lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
+    hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
+    shape = (B, T, pitch) if store == _lib.STORE_ALL else (B, pitch)
+    paths = torch.empty(shape, dtype=torch.float32, device=DEV)
+    nsync = int(L.smc_train_step_sync_bytes(T, N, M, 0, pitch))
+    sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
+    for math in (0, _lib.MATH_HW):
+        cur = torch.tensor([17, 3], dtype=torch.int64, device=DEV)
+        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
+        f = torch.empty((B, 6), dtype=torch.float32, device=DEV)
+        t = torch.full((B, N), float("nan"), dtype=torch.complex64, device=DEV)
+        _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
+                                    _lib.ptr(c), _lib.ptr(f), B, T, N, M, 43, _lib.SCHEME_LOG_EULER | math,
+                                    _lib.NORM_RAW, _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, B, _lib.ptr(t),
+                                    _lib.ptr(sync), nsync, None))
+        torch.cuda.synchronize()
+        assert cur.tolist() == [17 + B, 3 + B]
+        assert not sync.view(torch.int32).any()
+        contracts = c.cpu().numpy()
+        np.testing.assert_array_equal(contracts, oracle.sobol_contracts(7, 17, B, golden["bounds_lower"],
+                                                                        golden["bounds_upper"]))
+        got = t.cpu().numpy()
+        if math == 0:
+            sub = np.arange(0, B, 7)  # every 7th contract (its own normal ordinal): the oracle loops per contract
+            for b in sub[:64]:
+                kt, _ = oracle.kernel_targets(contracts[b:b + 1], T, N, M, seed=43, ordinal0=3 + int(b),
+                                              normalize=False, wg=64)
+                np.testing.assert_array_equal(got[b:b + 1], kt)
+            kp, _, _ = oracle.kernel_paths(contracts[:2], T, P, 43, ordinal0=3, want_paths=True, wg=64)
+            if store == _lib.STORE_ALL:
+                np.testing.assert_array_equal(paths[:2, :, :P].cpu().numpy(), kp)
+            else:
+                np.testing.assert_array_equal(paths[:2, :P].cpu().numpy(), kp[:, -1])
+        else:
+            want = oracle.training_targets(contracts[:16], T, N, M, seed=43, ordinal0=3, normalize=False)
+            assert _norm_rel(got[:16], want) < 1e-5
 
 
 SLICED_CASES = [  # (B, N, M, store, chunk): shapes with P > 65,536 (W = P / 65,536 slices)

@@ -72,7 +72,7 @@ def test_portable_math_targets_bit_exact_and_match_reference(oracle, gbm_golden,
     if m["dtype"] == "float32":
         kt, _ = oracle.kernel_targets(contracts, m["T"], m["N"], m["M"], seed=m["seed"], ordinal0=m["ordinal0"],
                                       scheme=m["scheme"], normalize=m["normalize"],
-                                      wg=oracle.engine_wg(m["T"], m["N"], m["N"] * m["M"]))
+                                      wg=oracle.engine_wg(m["T"], m["N"], m["N"] * m["M"], normalize=m["normalize"]))
         np.testing.assert_array_equal(got, kt)
         assert per_contract_rel(got, want).max() < 5e-6
     else:
