@@ -131,6 +131,7 @@ struct MArgs {
   int32_t segs;      // batch segments of the weight gradients
   int32_t zs, gs;    // LDS row strides (Op elements) of the activation and output-gradient buffers
   int32_t pre_global;  // pre-activations in the f32 workspace [bp][2 no] instead of LDS [R][2 no]
+  int32_t lgemm_mb;  // lgemm_kernel launches: feature blocks of the launch (set per launch)
   int32_t layered;   // wide layers: one MFMA GEMM launch per layer and direction (lgemm_kernel) instead of fb_kernel
   int32_t lpb;       // loss partials per batch block of `rows` rows (1; layered: feature blocks of the last layer)
   int64_t n_params;
@@ -669,6 +670,9 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
 #ifndef SMC_LGEMM_M
 #define SMC_LGEMM_M 64
 #endif
+#ifndef SMC_LGEMM_XCD
+#define SMC_LGEMM_XCD 1
+#endif
 constexpr int kLM = SMC_LGEMM_M, kLN = 64, kLK = SMC_LGEMM_K, kLLd = kLK + 4;  // tile (features x batch rows), K stage, LDS stride
 constexpr int kLThreads = 256;  // 4 waves x (kLM / 4 features x 64 rows); kLM = 64: 512 workgroups at H = 256 (263 vs 269 us per step with 128)
 constexpr int kLTM = kLM / 4 / 16, kLTN = kLN / 16;           // 16 x 16 tiles per wave
@@ -729,7 +733,21 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   const float* P = a.params;
   // C[m][n] = sum_k A[m][k] B[n][k]: fwd / last A = Wc [wout][kx], B = Z_l [bp][kx];
   // bwd A = Wc^T [win][wout], B = dU_l [bp][wout]
-  const int mb = blockIdx.x, nb = blockIdx.y;
+  // XCD-aware tile order: the 1-D grid's consecutive workgroups go round-robin to the 8 XCDs, so
+  // workgroup w runs on XCD w % 8; each XCD takes a contiguous eighth of the batch blocks with every
+  // feature block, and reads only its eighth of the row operand (B) and the whole weight matrix (A)
+  // into its own L2, instead of every XCD streaming all of B past one feature block
+  const int MB = static_cast<int>(a.lgemm_mb);
+  const int NB = static_cast<int>(gridDim.x) / MB;
+  int mb, nb;
+  if (SMC_LGEMM_XCD && NB % 8 == 0) {
+    const int xcd = static_cast<int>(blockIdx.x) & 7, local = static_cast<int>(blockIdx.x) >> 3;
+    nb = xcd * (NB >> 3) + local / MB;
+    mb = local % MB;
+  } else {
+    mb = static_cast<int>(blockIdx.x) % MB;
+    nb = static_cast<int>(blockIdx.x) / MB;
+  }
   const int64_t kbeg = 0;
   const MLayer& ly = a.layer[l];
   const bool bwd = MODE == kLBwd;
@@ -770,6 +788,27 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
       *reinterpret_cast<f32x4*>(&sb[buf][r * kLLd + 4 * q]) = rb[v];
     }
   };
+  // the layer whose output (or output gradient) this launch writes
+  const MLayer& lo = MODE == kLBwd ? a.layer[l - 1] : ly;
+  const int N = lo.no;
+  // epilogue phase B: thread -> features 4q .. 4q + 3 (2 complex outputs) of rows rb0, rb0 + 16, ...
+  const int q = tid % (kLM / 4), rb0 = tid / (kLM / 4);
+  const int f0 = m0 + 4 * q;
+  // the row loop's global inputs (targets / pre-activations), loaded before the K loop so that their
+  // latency hides behind it: two waves per SIMD cannot hide a load latency per row of the epilogue
+  constexpr int kRows = kLN / (kLThreads / (kLM / 4));  // rows per thread (4)
+  float2 in[kRows][2];
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const int64_t b = n0 + rb0 + k * (kLThreads / (kLM / 4));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int jj = (f0 >> 1) + h;
+      in[k][h] = float2{0.0f, 0.0f};
+      if (MODE == kLLast && jj < N && b < a.batch) in[k][h] = *reinterpret_cast<const float2*>(a.targets + (b * N + jj) * 2);
+      if (MODE == kLBwd && jj < N && lo.pre >= 0) in[k][h] = *reinterpret_cast<const float2*>(a.fws + lo.pre + b * (2 * N) + 2 * jj);
+    }
+  }
   f32x4 acc[kLTM][kLTN];
 #pragma unroll
   for (int i = 0; i < kLTM; ++i)
@@ -821,36 +860,16 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
       *reinterpret_cast<f32x4*>(&tile[(j * 16 + c) * TLD + (wave * kLTM + i) * 16 + 4 * g]) = acc[i][j];
   __syncthreads();
   const int64_t bp = a.bp;
-  const int64_t blk = blockIdx.y;  // batch block of kLN rows (= a.rows)
+  const int64_t blk = nb;  // batch block of kLN rows (= a.rows)
   // the layer whose output (or output gradient) this launch writes, and its row-major / ^T buffers
-  const MLayer& lo = MODE == kLBwd ? a.layer[l - 1] : ly;
   const MLayer& nx = MODE == kLFwd ? a.layer[l + 1] : ly;
   const int64_t rm_off = MODE == kLFwd ? nx.zr : lo.dr;
   const int64_t tr_off = MODE == kLFwd ? nx.zt : lo.gt;
   const int rm_ld = MODE == kLFwd ? nx.kx : lo.wout;  // row-major row length
   const int nvalid = MODE == kLFwd ? ly.wout : lo.wout;  // features this launch writes
-  const int N = lo.no;
   const float scale = 2.0f / static_cast<float>(static_cast<double>(a.batch) * ly.no);
-  // phase B: thread -> features 4q .. 4q + 3 (2 complex outputs) of rows rb, rb + 8, ..., in order
-  const int q = tid % (kLM / 4), rb0 = tid / (kLM / 4);
-  const int f0 = m0 + 4 * q;
   double loss = 0.0;
   float dcs[2] = {0.0f, 0.0f};
-  // the row loop's global inputs (targets / pre-activations) loaded ahead of its stores: one wave per
-  // SIMD cannot hide a load latency per row
-  constexpr int kRows = kLN / (kLThreads / (kLM / 4));  // rows per thread (8)
-  float2 in[kRows][2];
-#pragma unroll
-  for (int k = 0; k < kRows; ++k) {
-    const int64_t b = n0 + rb0 + k * (kLThreads / (kLM / 4));
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int jj = (f0 >> 1) + h;
-      in[k][h] = float2{0.0f, 0.0f};
-      if (MODE == kLLast && jj < N && b < a.batch) in[k][h] = *reinterpret_cast<const float2*>(a.targets + (b * N + jj) * 2);
-      if (MODE == kLBwd && jj < N && lo.pre >= 0) in[k][h] = *reinterpret_cast<const float2*>(a.fws + lo.pre + b * (2 * N) + 2 * jj);
-    }
-  }
 #pragma unroll
   for (int k = 0; k < kRows; ++k) {
     const int rr = rb0 + k * (kLThreads / (kLM / 4));
@@ -912,7 +931,7 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
     if (MODE == kLLast && tid == 0) {
       double t = 0.0;
       for (int w = 0; w < kLThreads / 64; ++w) t += red[w];
-      a.lossp[blk * a.lpb + blockIdx.x] = t;
+      a.lossp[blk * a.lpb + mb] = t;
     }
   } else {
     __syncthreads();
@@ -927,7 +946,7 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   }
   if constexpr (MODE == kLFwd) {
     // columns [wout, kx_{l+1}) of Z_{l+1} (the ones column when 2 no is a multiple of 16)
-    if (blockIdx.x == gridDim.x - 1) {
+    if (mb == MB - 1) {
       for (int e = tid; e < (nx.kx - ly.wout) * kLN; e += kLThreads) {
         const int k = ly.wout + e / kLN;
         const int64_t b = n0 + e % kLN;
@@ -1109,15 +1128,18 @@ int32_t launch_layered(const Plan& p, hipStream_t s) {
   if (int32_t rc = check_launch("cvnn lpack_kernel")) return rc;
   const unsigned by = static_cast<unsigned>(a.bp / kLN);
   const int L = a.n_layers;
+  MArgs g = a;  // lgemm_mb: the launch's feature blocks (1-D grid of lgemm_mb x by workgroups)
   for (int l = 0; l < L; ++l) {
-    const dim3 grid(static_cast<unsigned>((a.layer[l].wout + kLM - 1) / kLM), by);
-    if (l + 1 < L) hipLaunchKernelGGL(lgemm_kernel<kLFwd>, grid, dim3(kLThreads), 0, s, a, l);
-    else hipLaunchKernelGGL(lgemm_kernel<kLLast>, grid, dim3(kLThreads), 0, s, a, l);
+    g.lgemm_mb = (a.layer[l].wout + kLM - 1) / kLM;
+    const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * by);
+    if (l + 1 < L) hipLaunchKernelGGL(lgemm_kernel<kLFwd>, grid, dim3(kLThreads), 0, s, g, l);
+    else hipLaunchKernelGGL(lgemm_kernel<kLLast>, grid, dim3(kLThreads), 0, s, g, l);
     if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
   }
   for (int l = L - 1; l >= 1; --l) {
-    const dim3 grid(static_cast<unsigned>((a.layer[l].win + kLM - 1) / kLM), by);
-    hipLaunchKernelGGL(lgemm_kernel<kLBwd>, grid, dim3(kLThreads), 0, s, a, l);
+    g.lgemm_mb = (a.layer[l].win + kLM - 1) / kLM;
+    const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * by);
+    hipLaunchKernelGGL(lgemm_kernel<kLBwd>, grid, dim3(kLThreads), 0, s, g, l);
     if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
   }
   // weight gradients from the ^T copies, as after fb_kernel (its 64 x 64 blocks measured faster here

@@ -37,6 +37,9 @@ namespace {
 
 // rows_kernel occupancy: 8 waves per SIMD (<= 64 VGPRs) = 4 workgroups per CU, so C2's 4096 contracts
 // are exactly 4 rounds of 1024 persistent workgroups (at 69 VGPRs: 3 per CU, 5.33 rounds)
+#ifndef SMC_ROWS_WAVES_F64
+#define SMC_ROWS_WAVES_F64 6
+#endif
 #ifndef SMC_ROWS_WAVES
 #define SMC_ROWS_WAVES 8
 #endif
@@ -600,7 +603,7 @@ __host__ __device__ inline int cf_part_doubles(int N) {
 
 template <typename Real>
 __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int64_t b,
-                                    double terminal_sum, double* lds, int part_doubles = -1) {
+                                    double terminal_sum, double* lds) {
   using C2 = typename Complex2<Real>::type;
   const int tid = threadIdx.x;
   const int T = a.T, N = a.N, M = a.M;
@@ -618,8 +621,8 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
   const int cols = quad ? N / 4 : N;
   const int G = cols <= kThreads ? kThreads / cols : 1;
   const int items = cols * G;
-  double* part = lds;                                            // [cf_part_doubles(N)] (or part_doubles)
-  double* avg = part + (part_doubles >= 0 ? part_doubles : cf_part_doubles(N));  // [N]
+  double* part = lds;                                            // [cf_part_doubles(N)]
+  double* avg = part + cf_part_doubles(N);                       // [N]
   double* cs = avg + N;                                          // [N]
   double* sn = cs + N;                                           // [N]
 
@@ -801,18 +804,14 @@ __global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
 // contract by blockIdx.x and every later one from the counter, so a workgroup that starts late (a
 // concurrent network kernel held its slot) takes fewer contracts instead of finishing last; the
 // last workgroup out resets the counters.  Which workgroup runs a contract changes no result.
-// FUSED_CF (round 4, the f64 shapes): the workgroup takes the contract's CF phase itself right after the
-// simulation (its stores drained, the terminal row re-read from L2 / HBM by cf_targets_contract, the
-// split pair's cf_kernel order: bit-identical targets) instead of a second launch that re-reads every
-// terminal row afterwards; the f64 kernel is VALU-bound, so the re-read overlaps the other workgroups'
-// simulation.
-__host__ __device__ constexpr int rows_cf_part_doubles(int N) {  // f64: no column quads, items <= max(512, N)
-  return (2 * N > kThreads ? 2 * N : kThreads);
-}
-
-template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL, bool FUSED_CF>
-__device__ __forceinline__ void rows_body(const EngineArgs& a) {
-  static_assert(!FUSED_CF || sizeof(Real) == 8, "the fused CF phase is sized for f64 rows (no column quads)");
+// f64 rows run at 6 waves per SIMD (SMC_ROWS_WAVES_F64; round 4 A/B on MI355X, C2-f64: 9.01 ms at 6 vs
+// 9.20-9.28 ms at 8 waves, and 9.49-9.53 ms with the CF phase fused into this kernel, which then re-read
+// the terminal row while its own path math waited): the f64 path math is VALU-bound and the larger
+// register budget removes its spills.
+template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof(Real) == 8 ? SMC_ROWS_WAVES_F64
+                                                                                              : SMC_ROWS_WAVES)))
+void rows_kernel(EngineArgs a) {
   extern __shared__ double lds[];
   if constexpr (sizeof(Real) == 8) math::f64_tables_load();
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
@@ -836,20 +835,11 @@ __device__ __forceinline__ void rows_body(const EngineArgs& a) {
     const double w = wave_sum(acc);
     double* ws = lds + parity * kWaves;
     if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = w;
-    if constexpr (FUSED_CF) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's path stores (the terminal row)
-      __syncthreads();
-      double tot = 0.0;  // every thread adds the waves in order (the split pair's order)
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      double tot = 0.0;
       for (int k = 0; k < kWaves; ++k) tot += ws[k];
-      const Contract cc = load_contract(a.contracts + b * 6);  // reloaded: not kept live across the paths
-      cf_targets_contract<Real>(a, cc, b, tot, lds + 2 * kWaves, rows_cf_part_doubles(a.N));
-    } else {
-      lds_barrier();
-      if (threadIdx.x == 0) {
-        double tot = 0.0;
-        for (int k = 0; k < kWaves; ++k) tot += ws[k];
-        *pad_sum<Real>(a, b) = tot;
-      }
+      *pad_sum<Real>(a, b) = tot;
     }
     if (dyn) {
       // next_b is rewritten only after the next contract's lds_barrier: every thread has read it
@@ -869,23 +859,6 @@ __device__ __forceinline__ void rows_body(const EngineArgs& a) {
       __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-}
-
-template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SMC_ROWS_WAVES)))
-void rows_kernel(EngineArgs a) {
-  rows_body<Real, LOG_EULER, HW, STORE_ALL, false>(a);
-}
-
-// The fused f64 kernel: the CF phase needs more registers than the 64 of 8 waves per SIMD (it spilled in
-// the path loop), so it runs at SMC_ROWS_FUSED_WAVES
-#ifndef SMC_ROWS_FUSED_WAVES
-#define SMC_ROWS_FUSED_WAVES 6
-#endif
-template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SMC_ROWS_FUSED_WAVES)))
-void rows_fused_kernel(EngineArgs a) {
-  rows_body<Real, LOG_EULER, HW, STORE_ALL, true>(a);
 }
 
 // ---- resident_kernel: the terminal row never leaves the chip -----------------------------------
@@ -1744,23 +1717,6 @@ int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
 
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 int32_t launch_rows_k(const EngineArgs& a, hipStream_t stream) {
-  if constexpr (sizeof(Real) == 8) {  // one launch: the CF phase fused (rows_kernel FUSED_CF)
-    auto k = rows_fused_kernel<Real, LOG_EULER, HW, STORE_ALL>;
-    const size_t lds = (2 * kWaves + static_cast<size_t>(rows_cf_part_doubles(a.N)) + 3 * static_cast<size_t>(a.N)) *
-                       sizeof(double);
-    if (lds + sizeof(math::F64Tables) > kMaxLds)
-      return fail(SMC_ERR_INVALID_SHAPE, "engine: network_size exceeds the LDS budget");
-    if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               static_cast<int>(lds)) != hipSuccess) {
-      (void)hipGetLastError();
-      return fail(SMC_ERR_HIP, "rows_kernel: cannot raise the dynamic LDS limit");
-    }
-    unsigned grid = 0;
-    if (int32_t st = resident_grid(reinterpret_cast<const void*>(k), kThreads, lds, a.B, &grid)) return st;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), lds, stream, a);
-    return check_launch("rows_fused_kernel");
-  }
   const size_t lds1 = 2 * kWaves * sizeof(double), lds2 = lds_bytes(a.T, a.N, true);
   auto k1 = rows_kernel<Real, LOG_EULER, HW, STORE_ALL>;
   auto k2 = cf_kernel<Real>;
@@ -2281,7 +2237,7 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   if (SMC_TRAIN_MODE == 3 && resident_ok(a, f32)) return "resident_kernel";
   if (SMC_TRAIN_MODE == 3 && packed_ok(a, f32)) return "packed_kernel";
   if (SMC_TRAIN_MODE >= 2 && split_ok(a, f32) && a.T == kRowBlock && a.P % kChunk == 0) return "paths_kernel+cf_kernel";
-  if (SMC_TRAIN_MODE >= 2 && rows_ok(a, f32)) return f32 ? "rows_kernel+cf_kernel" : "rows_fused_kernel";  // f64: the CF phase fused
+  if (SMC_TRAIN_MODE >= 2 && rows_ok(a, f32)) return "rows_kernel+cf_kernel";
   if (SMC_TRAIN_MODE >= 2 && split_ok(a, f32)) return "paths_kernel+cf_kernel";
   return a.slices > 1 ? "queue_kernel" : "contract_kernel";
 }

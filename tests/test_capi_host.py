@@ -187,7 +187,7 @@ def test_train_targets_kernel_choice() -> None:
     assert L.smc_train_targets_kernel(16, 128, 512, 0, 1024, 0) == b"packed_kernel"         # e2e shape, P = 512
     assert L.smc_train_targets_kernel(17, 2048, 65536, 0, 66560, 0) == rows                 # N > 1024, T != 16
     assert L.smc_train_targets_kernel(17, 2048, 65536, 0, 0, 0) == b"contract_kernel"       # no padding
-    assert L.smc_train_targets_kernel(16, 256, 65536, 1, 66048, 0) == b"rows_fused_kernel"  # f64 (CF fused)
+    assert L.smc_train_targets_kernel(16, 256, 65536, 1, 66048, 0) == b"rows_kernel+cf_kernel"  # f64
     assert L.smc_train_targets_kernel(16, 256, 65536, 1, 0, 0) == b"contract_kernel"        # f64, no padding
     assert L.smc_train_targets_kernel(16, 6, 6144, 0, 6144, 0) == b"contract_kernel"        # pitch == P
     assert L.smc_train_targets_kernel(16, 6, 6144, 0, 7168, 0) == split                     # N not | 4096

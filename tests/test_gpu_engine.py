@@ -252,8 +252,7 @@ def test_rows_kernel_matches_oracle_and_contract_kernel(oracle, golden, B, T, N,
     P = N * M
     dcode = 0 if dtype == "float32" else 1
     pitch = int(_L().smc_path_pitch(P, dcode))
-    assert _L().smc_train_targets_kernel(T, N, P, dcode, pitch, 0) == (b"rows_kernel+cf_kernel" if dcode == 0
-                                                                        else b"rows_fused_kernel")
+    assert _L().smc_train_targets_kernel(T, N, P, dcode, pitch, 0) == b"rows_kernel+cf_kernel"
     flags = _lib.MATH_HW if hw else 0
     got, _, paths = _run_targets(c, T, N, M, scheme, normalize, dtype, store, ordinal0=9, with_rowsum=False,
                                  flags=flags, pitch=pitch)
@@ -474,7 +473,7 @@ def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store, ch
 ROWS_STEP_CASES = [  # (B, T, N, M, dtype, store, chunk): smc_train_step shapes on rows_kernel + cf_kernel
     (None, 16, 64, 64, _lib.DTYPE_F64, _lib.STORE_ALL, None),      # f64, > 4 contracts per workgroup slot
     (2500, 5, 32, 64, _lib.DTYPE_F64, _lib.STORE_TERMINAL, 900),   # f64, three chunk launches, odd T
-    (None, 3, 64, 32, _lib.DTYPE_F32, _lib.STORE_ALL, None),       # f32, P = 2048 (not a resident shape)
+    (None, 3, 64, 96, _lib.DTYPE_F32, _lib.STORE_ALL, None),       # f32, P = 6144 (neither resident nor packed)
 ]
 
 
@@ -490,7 +489,7 @@ def test_rows_train_step_dynamic_queue_equals_targets(golden, B, T, N, M, dtype,
     P = N * M
     f64 = dtype == _lib.DTYPE_F64
     pitch = int(L.smc_path_pitch(P, dtype))
-    assert L.smc_train_step_kernel(T, N, M, dtype, pitch) == (b"rows_fused_kernel" if f64 else b"rows_kernel+cf_kernel")
+    assert L.smc_train_step_kernel(T, N, M, dtype, pitch) == b"rows_kernel+cf_kernel"
     eng = SobolEngine(6, 7, 0)
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
@@ -532,7 +531,7 @@ def test_c2_f64_timed_call_matches_oracle(oracle, golden) -> None:
     P = N * M
     dtype = _lib.DTYPE_F64
     pitch = int(L.smc_path_pitch(P, dtype))
-    assert L.smc_train_step_kernel(T, N, M, dtype, pitch) == b"rows_fused_kernel"  # the CF phase fused (f64)
+    assert L.smc_train_step_kernel(T, N, M, dtype, pitch) == b"rows_kernel+cf_kernel"
     slots = 4 * torch.cuda.get_device_properties(0).multi_processor_count  # 4 workgroups per CU
     assert B > 2 * slots
     eng = SobolEngine(6, 7, 0)

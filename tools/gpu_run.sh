@@ -91,6 +91,12 @@ for step in "$@"; do
     ab:*)  # ab:<tag>:<kprof_step args with , for spaces>:<variant names with ,> (tools/micro/ab.sh)
       IFS=: read -r _ tag args names <<< "$step"
       run "ab_$tag" 900 bash tools/micro/ab.sh "$OUT/ab_$tag.txt" "${args//,/ }" ${names//,/ } ;;
+    py:*)  # py:<tag>:<script and args with , for spaces> (a python tool under its own limit)
+      IFS=: read -r _ tag args <<< "$step"
+      run "py_$tag" 300 python -u ${args//,/ } ;;
+    abnet:*)  # abnet:<tag>:<kprof_net args with , for spaces>:<variant names with ,> (isolated network step)
+      IFS=: read -r _ tag args names <<< "$step"
+      AB_SCRIPT=tools/kprof_net.py run "abnet_$tag" 900 bash tools/micro/ab.sh "$OUT/abnet_$tag.txt" "${args//,/ }" ${names//,/ } ;;
     pmcv:*)  # pmcv:<variant|default>:<kprof_step args with ,>:<counters with ,> -> one PMC pass
       IFS=: read -r _ var args ctrs <<< "$step"; tag="${var}_$(echo "$ctrs" | tr ',' '_' | cut -c1-40)_$(echo "$args" | md5sum | cut -c1-6)"
       if [ "$var" = default ]; then lib=$ROOT/spectralmc_amd/libspectralmc_hip.so; else lib=$ROOT/tools/micro/v/libsmc_$var.so; fi

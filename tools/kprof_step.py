@@ -34,7 +34,8 @@ def main() -> None:
     ap.add_argument("--lanes", type=int, default=1, help="launches alternate over this many streams, each with "
                     "its own cursor, sync area and path scratch (consecutive launches may overlap)")
     ap.add_argument("--dynamic", action="store_true", help="SMC_TRAIN_DYNAMIC: every contract from the queue")
-    ap.add_argument("--trace", default="", help="save per-workgroup timestamps (SMC_EXPERIMENT_TRACE builds)")
+    ap.add_argument("--norm", default="", choices=["", "raw", "normalize"],
+                    help="targets normalisation (default: RAW for the lock-step shape, else NORMALIZE)")
     a = ap.parse_args()
     B, T, N, M = SHAPES[a.config]
     B = a.B or B
@@ -66,24 +67,20 @@ def main() -> None:
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(lanes - 1)]
     scheme = _lib.SCHEME_LOG_EULER | (_lib.MATH_HW if a.math == "hw" else 0) | (_lib.TRAIN_DYNAMIC if a.dynamic else 0)
     n_launched = [0]
+    raw = a.norm == "raw" or (a.norm == "" and a.config == "lockstep")
+    norm = _lib.NORM_RAW if raw else _lib.NORM_NORMALIZE
 
     def step():
         k = n_launched[0] % lanes
         n_launched[0] += 1
         _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur[k]), 0, lanes * B,
                                     _lib.ptr(c), None if f64 else _lib.ptr(f), B, T, N, M, 7, scheme,
-                                    _lib.NORM_NORMALIZE, dcode, store, _lib.ptr(pathss[k]), pitch, chunk, _lib.ptr(t),
+                                    norm, dcode, store, _lib.ptr(pathss[k]), pitch, chunk, _lib.ptr(t),
                                     _lib.ptr(syncs[k]), nsync, _lib.stream_handle(streams[k])))
 
     for _ in range(lanes):
         step()
     torch.cuda.synchronize()
-    if a.trace:  # the trace keeps the last launch only: zero it before the timed launches
-        import ctypes
-        fn = getattr(L, "smc_debug_trace")
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
-        assert fn(None, -1) == 0
-        a.iters = 1
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for s_ in streams[1:]:
@@ -95,16 +92,9 @@ def main() -> None:
     e1.record()
     torch.cuda.synchronize()
     assert all(_lib.sync_status(sy) == 0 for sy in syncs)
-    if a.trace:  # gbm.hip g_trace: [workgroup][40] s_memrealtime stamps of the last launch
-        import ctypes
-        buf = np.zeros((1024, 40), dtype=np.uint64)
-        fn = getattr(L, "smc_debug_trace")
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
-        assert fn(buf.ctypes.data, buf.size) == 0
-        np.save(a.trace, buf)
-    name = L.smc_train_step_kernel(T, N, M, dcode, pitch).decode()
+    name = L.smc_train_step_kernel(T, N, M, dcode | (_lib.QUERY_RAW if raw else 0), pitch).decode()
     ms = e0.elapsed_time(e1) / a.iters
-    print(f"{a.config} pitch={pitch} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
+    print(f"{a.config} {'raw' if raw else 'normalize'} pitch={pitch} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
           f"({launches} launch(es) of {chunk}), checksum {float(t.abs().double().mean()):.6g}")
 
 
