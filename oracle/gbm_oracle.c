@@ -178,34 +178,31 @@ static void twiddle(int64_t j, int64_t N, double* s_out, double* c_out) {
   *c_out = ((q + 1) & 2) ? -cb : cb;
 }
 
-/* ---- f64 normals: op-for-op restatement of smc_math.h log_u32 / sincos2pi_u32 ---------- */
+/* ---- f64 normals: op-for-op restatement of smc_math.h m2log_u32 / sincos2pi_u32 --------- */
 #include "f64_tables.h"
 static inline uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
 static inline double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
 
-/* ln((a + 1/2) 2^-32) as smc_math.h log_u32 (round 4): m = a + 1/2 = 2^e f exactly; mh = the top 20
- * mantissa bits; f >= 1 + 0x6A09F 2^-20 is halved (e + 1); table entry idx = ((mh + 2^11) >> 12) + 128,
- * halved (mh + 2^12) >> 13 (c = 1 + (idx - 128)/256 nearest f, round half up on mh); r = f INV - 1 in
- * one fma, ln(1 + r) to r^6, then (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))). */
-static double log_u32(uint32_t a) {
+/* -2 ln((a + 1/2) 2^-32) as smc_math.h m2log_u32 (round 4, v3): m = a + 1/2 = 2^e f exactly; table point
+ * c = 1 + i/1024, i = (mh + 2^9) >> 10 from the top 20 mantissa bits mh; r' = -2 (f INV - 1) in one fma;
+ * r' + r'^2 Q(r') (Q: D5 = 1/80, D4 = 1/32, D3 = 1/12, D2 = 1/4, Horner); then
+ * (k (-2 LN2_HI) + (-2 T_HI)) + ((k (-2 LN2_LO) + (-2 T_LO)) + that), k = e - 32. */
+static double m2log_u32(uint32_t a) {
   const double m = (double)a + 0.5;
   const uint64_t bits = d2u(m);
   const uint32_t hw = (uint32_t)(bits >> 32);
   const uint32_t mh = hw & 0xFFFFFu;
-  const int half = mh >= 0x6A09Fu;
-  const int idx = half ? (int)((mh + (1u << 12)) >> 13) : (int)((mh + (1u << 11)) >> 12) + 128;
-  const int e = (int)(hw >> 20) - 1023 + (half ? 1 : 0);
-  const double f = u2d(((uint64_t)(mh | (half ? 0x3FE00000u : 0x3FF00000u)) << 32) | (bits & 0xFFFFFFFFull));
+  const uint32_t idx = (mh + 0x200u) >> 10;
+  const double f = u2d(((uint64_t)(mh | 0x3FF00000u) << 32) | (bits & 0xFFFFFFFFull));
+  const double k = (double)((int)(hw >> 20) - 1055);
   const double* t = kF64LogTab[idx];
-  const double r = fma(f, t[0], -1.0);
-  double q = -0.16666666666666666;
-  q = fma(q, r, 0.2);
-  q = fma(q, r, -0.25);
-  q = fma(q, r, 0.3333333333333333);
-  q = fma(q, r, -0.5);
+  const double r = fma(f, t[0], 2.0);
+  double q = 0.0125;
+  q = fma(q, r, 0.03125);
+  q = fma(q, r, 0.08333333333333333);
+  q = fma(q, r, 0.25);
   const double p = fma(q, r * r, r);
-  const double k = (double)(e - 32);
-  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, t[1] + (t[2] + p)));
+  return fma(k, kF64M2Ln2Hi, t[1]) + (fma(k, kF64M2Ln2Lo, t[2]) + p);
 }
 
 /* (sin, cos)(2 pi b 2^-32) as smc_math.h (round 4): nearest of 1024 table angles j = round(b / 2^22)
@@ -225,41 +222,39 @@ static void sincos2pi_u32(uint32_t b, double* s_out, double* c_out) {
   *c_out = fma(C, cx, -(S * sx));
 }
 
-/* The split of e^y as smc_math.h exp_split: t = fma(y, 64 / ln 2, 1.5 2^52) rounds y 64 / ln 2 to the
- * integer n = 64 m + j (t's low word), n = t - 1.5 2^52, r = y - n ln2/64 (Cody-Waite, two fused steps),
- * e^r - 1 to r^5; e^y = 2^m T (1 + em1), T = 2^(j/64) from the table. */
-static void exp_split(double y, double* T, double* em1, int* m) {
-  const double t = fma(y, 92.33248261689366, 6755399441055744.0);
+/* 2^(ys/256) as smc_math.h exp2s_split / exp2s_f64 (the f64 device path exponent in units of ln 2 / 256):
+ * t = ys + 1.5 2^52 rounds ys to n = 256 m + j (t's low word), rr = ys - n exactly, 2^(rr/256) - 1 to
+ * degree 4 (E1..E4), 2^m T (1 + em1) with T = 2^(j/256) from the table.  The oracle's reference mode
+ * keeps libm exp. */
+static void exp2s_split(double ys, double* T, double* em1, int* m) {
+  const double t = ys + 6755399441055744.0;
   const int ni = (int)(uint32_t)d2u(t);
-  const double n = t - 6755399441055744.0;
-  double r = fma(-n, 0.010830424696223417, y);
-  r = fma(-n, 2.572804622327669e-14, r);
-  double q = 0.008333333333333333;
-  q = fma(q, r, 0.041666666666666664);
-  q = fma(q, r, 0.16666666666666666);
-  q = fma(q, r, 0.5);
-  *T = kF64Exp2Tab[ni & 63];
-  *em1 = fma(q, r * r, r);
-  *m = ni >> 6;
+  const double rr = ys - (t - 6755399441055744.0);
+  double q = kF64ExpE4;
+  q = fma(q, rr, kF64ExpE3);
+  q = fma(q, rr, kF64ExpE2);
+  q = fma(q, rr, kF64ExpE1);
+  *T = kF64Exp2Tab[ni & 255];
+  *em1 = q * rr;
+  *m = ni >> 8;
 }
 
-/* e^y as smc_math.h exp_f64 (the oracle's reference mode keeps libm exp) */
-double oracle_exp_f64(double y) {
+double oracle_exp2s_f64(double ys) {
   double T, em1;
   int m;
-  exp_split(y, &T, &em1, &m);
+  exp2s_split(ys, &T, &em1, &m);
   return ldexp(fma(T, em1, T), m);
 }
 
-/* x e^y as smc_math.h mul_exp_f64, the f64 device log-Euler step: (x T) (1 + em1) scaled by 2^m */
-double oracle_mul_exp_f64(double x, double y) {
+/* x 2^(ys/256) as smc_math.h mul_exp2s_f64, the f64 device log-Euler step */
+double oracle_mul_exp2s_f64(double x, double ys) {
   double T, em1;
   int m;
-  exp_split(y, &T, &em1, &m);
+  exp2s_split(ys, &T, &em1, &m);
   const double xt = x * T;
   return ldexp(fma(xt, em1, xt), m);
 }
-double oracle_log_u32(uint32_t a) { return log_u32(a); }
+double oracle_m2log_u32(uint32_t a) { return m2log_u32(a); }
 void oracle_sincos2pi_u32(uint32_t b, double* s, double* c) { sincos2pi_u32(b, s, c); }
 
 float oracle_log_pos(float u) { return log_pos(u); }
@@ -290,12 +285,12 @@ void oracle_stream_u32(uint64_t seed, uint64_t ordinal, uint64_t group, int64_t 
 }
 
 /* One Box-Muller pair.  f32: 23-bit uniforms and the portable kernels (bit-identical to the
- * device); f64: 32-bit uniforms and the log_u32 / sincos2pi_u32 sequences above (bit-identical). */
+ * device); f64: 32-bit uniforms and the m2log_u32 / sincos2pi_u32 sequences above (bit-identical). */
 static void normal_pair(mwc64x* g, int is_f64, double* z0, double* z1) {
   const uint32_t a = mwc_next(g), b = mwc_next(g);
   if (is_f64) {
-    /* u1 = (a + 1/2) 2^-32, angle b 2^-32 revolutions: smc_math.h log_u32 / sincos2pi_u32 */
-    const double r = sqrt(-2.0 * log_u32(a));
+    /* u1 = (a + 1/2) 2^-32, angle b 2^-32 revolutions: smc_math.h m2log_u32 / sincos2pi_u32 */
+    const double r = sqrt(m2log_u32(a));
     double sn, cs;
     sincos2pi_u32(b, &sn, &cs);
     *z0 = r * cs;

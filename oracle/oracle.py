@@ -73,10 +73,10 @@ def lib() -> ctypes.CDLL:
                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_basket_cholesky.argtypes = [ctypes.c_int32, ctypes.c_double, ctypes.c_void_p]
-        L.oracle_log_u32.argtypes = [ctypes.c_uint32]
-        L.oracle_log_u32.restype = ctypes.c_double
-        L.oracle_exp_f64.argtypes = [ctypes.c_double]
-        L.oracle_exp_f64.restype = ctypes.c_double
+        L.oracle_m2log_u32.argtypes = [ctypes.c_uint32]
+        L.oracle_m2log_u32.restype = ctypes.c_double
+        L.oracle_exp2s_f64.argtypes = [ctypes.c_double]
+        L.oracle_exp2s_f64.restype = ctypes.c_double
         L.oracle_sincos2pi_u32.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_log_pos.argtypes = [ctypes.c_float]
         L.oracle_log_pos.restype = ctypes.c_float
@@ -110,9 +110,9 @@ def stream_u32(seed: int, ordinal: int, group: int, n: int) -> np.ndarray:
     return out
 
 
-def log_u32(a: int) -> float:
-    """ln((a + 1/2) 2^-32): the f64 Box-Muller radius' log (csrc/smc_math.h log_u32)."""
-    return float(lib().oracle_log_u32(a))
+def m2log_u32(a: int) -> float:
+    """-2 ln((a + 1/2) 2^-32): the f64 Box-Muller radius squared (csrc/smc_math.h m2log_u32)."""
+    return float(lib().oracle_m2log_u32(a))
 
 
 def sincos2pi_u32(b: int) -> tuple[float, float]:
@@ -122,9 +122,10 @@ def sincos2pi_u32(b: int) -> tuple[float, float]:
     return s.value, c.value
 
 
-def exp_f64(y: float) -> float:
-    """e^y as the f64 device path recursion computes it (csrc/smc_math.h exp_f64)."""
-    return float(lib().oracle_exp_f64(y))
+def exp2s_f64(ys: float) -> float:
+    """2^(ys / 256) as the f64 device path recursion computes it, the exponent in units of ln 2 / 256
+    (csrc/smc_math.h exp2s_f64)."""
+    return float(lib().oracle_exp2s_f64(ys))
 
 
 def normals(seed: int, ordinal: int, rows: int, cols: int, dtype: str = "float32") -> np.ndarray:

@@ -153,7 +153,8 @@ __device__ __forceinline__ double wave_sum(double x) {
 }
 
 // One step of the path recursion.  f32 log-Euler works in log2 units (coefficients
-// pre-scaled by log2 e) with the portable exp2 of smc_math.h; f64 uses OCML exp.
+// pre-scaled by log2 e) with the portable exp2 of smc_math.h; f64 in units of ln 2 / 256 with
+// smc_math.h mul_exp2s_f64.
 template <typename Real, bool LOG_EULER, bool HW>
 struct Stepper {
   Real a, b;
@@ -168,7 +169,7 @@ struct Stepper {
     const double sq = sqrt(dt);
     if (LOG_EULER) {
       const double drift = c.r - c.d - 0.5 * c.v * c.v;
-      const double scale = sizeof(Real) == 4 ? kLog2e : 1.0;
+      const double scale = sizeof(Real) == 4 ? kLog2e : math::kExpUnit;  // f64: units of ln 2 / 256
       a = static_cast<Real>(drift * dt * scale);
       b = static_cast<Real>(c.v * sq * scale * zscale());
     } else {
@@ -181,7 +182,7 @@ struct Stepper {
     if constexpr (LOG_EULER) {
       if constexpr (sizeof(Real) == 4 && HW) return x * __builtin_amdgcn_exp2f(fmaf(b, z, a));
       else if constexpr (sizeof(Real) == 4) return x * math::exp2_any(fmaf(b, z, a));
-      else return math::mul_exp_f64(x, fma(b, z, a));
+      else return math::mul_exp2s_f64(x, fma(b, z, a));
     }
     if constexpr (sizeof(Real) == 4) return fabsf(fmaf(x, fmaf(b, z, a), x));
     else return fabs(fma(x, fma(b, z, a), x));
@@ -226,7 +227,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(lane_id);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));  // the lane's group stream
   // f32 HW log-Euler: the RNG hands back the step exponents directly (packed path pairs); f64
-  // log-Euler: the exponents too (b folded into the Box-Muller radius), x *= exp_f64(y)
+  // log-Euler: the exponents too (b folded into the Box-Muller radius), x *= 2^(y/256) (mul_exp2s_f64)
   constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
   constexpr bool kY64 = LOG_EULER && sizeof(Real) == 8;
   Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
@@ -240,7 +241,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
     } else if constexpr (kY64) {
       s.f64_log_increments4(step.b, step.a, zl, zh);
 #pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp_f64(math::mul_exp_f64(x[j], zl[j]), zh[j]);
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp2s_f64(math::mul_exp2s_f64(x[j], zl[j]), zh[j]);
     } else {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<HW>(zl[j], zh[j]);
@@ -271,7 +272,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
           else s.f64_log_increments4(step.b, step.a, zl, zh);
         }
 #pragma unroll
-        for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp_f64(x[j], (i & 1) ? zh[j] : zl[j]);
+        for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp2s_f64(x[j], (i & 1) ? zh[j] : zl[j]);
       } else {
         if ((i & 1) == 0) {
           if (tail) {
@@ -368,7 +369,7 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Rea
       advance_packed(x, z);
     } else if constexpr (kY64) {
 #pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp_f64(x[j], z[j]);
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp2s_f64(x[j], z[j]);
     } else {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], z[j]);

@@ -155,19 +155,20 @@ __device__ __forceinline__ void twiddle(int64_t j, int64_t N, double& s_out, dou
 // Fixed IEEE-754 sequences (fma, +, -, *, exact scaling and integer bit manipulation) over tables
 // (smc_f64_tables.h: generated in 60-digit decimal arithmetic, rounded to double), restated op for op by
 // oracle/gbm_oracle.c, so f64 normals are bit-identical on the CPU.  Accuracy against libm
-// (tests/test_oracle.py): ln within 1 ulp, (sin, cos) within 2^-53 absolute, exp within 1 ulp.
-// The f64 path kernel is VALU-issue-bound (PMC, round 4: the VALU busy ~95 % of the launch at ~4 cycles
-// per f64 instruction; LDS bank conflicts of the random table reads do not limit it), so round 4 trades
-// table size for polynomial terms: ln from a 256-point table (degree 6), sin / cos from a 1024-angle
-// table (to x^5 / x^4), exp to degree 5, table indices and the exp split from integer bits, the
-// Box-Muller uniform (a + 1/2) 2^-32 (never 0 or 1: no special case in the radius), and the exp's 2^m
-// applied to the path value as an exponent-field add.  The kernels that run this math copy the tables
+// (tests/test_oracle.py): -2 ln u within 2 ulp, (sin, cos) within 2^-52 absolute, 2^(y/256) within 2 ulp.
+// The f64 path kernel is VALU-issue-bound (PMC, round 4: VALU busy ~95 % of the launch, every VALU
+// instruction, integer or f64, 4 cycles per wave), so the forms minimise instructions per path step
+// (v3, round 4): -2 ln u directly (the -2 folded into the table and the polynomial as exact power-of-two
+// scalings), its table indexed by the top 10 mantissa bits with no range halving (the cancellation near
+// u = 1 is avoided by an exact k LN2_HI + T_HI instead), and the path exponent carried in units of
+// ln 2 / 256 (the scale folded into the step constants), so e^y needs no Cody-Waite reduction, a
+// degree-4 polynomial, a 256-point table and one ldexp.  The kernels that run this math copy the tables
 // into LDS first (f64_tables_load): a global load on the path loop would wait for the wave's outstanding
 // path stores (one vmcnt counter).
 struct alignas(16) F64Tables {
   double2 sc[1024];     // (sin, cos)(2 pi j / 1024)
-  double log[256][3];   // INV, -ln(INV) hi, lo at c = 1 + i/256, i = -128..127 (entry i + 128)
-  double ex[64];        // 2^(j / 64)
+  double log[1025][3];  // -2 INV, -2 T_HI, -2 T_LO at c = 1 + i/1024
+  double ex[256];       // 2^(j / 256)
 };
 
 __device__ __forceinline__ F64Tables& f64_lds() {
@@ -179,39 +180,38 @@ __device__ __forceinline__ F64Tables& f64_lds() {
 __device__ inline void f64_tables_load() {
   F64Tables& t = f64_lds();
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) t.sc[k] = double2{kF64SinCosTab[k][0], kF64SinCosTab[k][1]};
-  for (int k = threadIdx.x; k < 256 * 3; k += blockDim.x) (&t.log[0][0])[k] = (&kF64LogTab[0][0])[k];
-  for (int k = threadIdx.x; k < 64; k += blockDim.x) t.ex[k] = kF64Exp2Tab[k];
+  for (int k = threadIdx.x; k < 1025 * 3; k += blockDim.x) (&t.log[0][0])[k] = (&kF64LogTab[0][0])[k];
+  for (int k = threadIdx.x; k < 256; k += blockDim.x) t.ex[k] = kF64Exp2Tab[k];
   __syncthreads();
 }
 
-// ln((a + 1/2) 2^-32): m = a + 1/2 = 2^e f exactly (<= 33 significant bits); with mh the top 20 mantissa
-// bits, f >= 1 + 0x6A09F 2^-20 (just above sqrt 2) is halved (e + 1), so f is in [0.7071, 1.4143); the
-// table point c = 1 + i/256 nearest f is read off mh (round half up: i = (mh + 2^11) >> 12, halved f:
-// ((mh + 2^12) >> 13) - 128; i = 0 at f = 1, so no cancellation near u = 1); r = f INV - 1 in one fma
-// (|r| <= 0.0028), ln(1 + r) to r^6, then (e - 32) ln 2 + (LOG_HI + (LOG_LO + ln(1 + r))).
-__device__ __forceinline__ double log_u32(uint32_t a) {
+// X = -2 ln((a + 1/2) 2^-32), the Box-Muller radius squared: m = a + 1/2 = 2^e f exactly (f in [1, 2),
+// <= 33 significant bits); table point c = 1 + i/1024 nearest f from the top 10 mantissa bits (round half
+// up: i = (mh + 2^9) >> 10, i = 1024 at f -> 2); r' = -2 (f INV - 1) in one fma (|r'| <= 2^-10);
+// -2 ln(1 + r) = r' + r'^2 Q(r') with Q the r^2..r^5 terms of ln(1 + r), exactly rescaled (D2..D5 =
+// 1/4, 1/12, 1/32, 1/80); then X = (k (-2 LN2_HI) + (-2 T_HI)) + ((k (-2 LN2_LO) + (-2 T_LO)) + that),
+// k = e - 32 in -33..-1, whose first sum is exact (both multiples of 2^-42): near u = 1 (f -> 2, k = -1,
+// c = 2) it is exactly 0 and X the small remainder, with no cancellation.
+__device__ __forceinline__ double m2log_u32(uint32_t a) {
   const double m = static_cast<double>(a) + 0.5;  // exact
   const uint64_t bits = __double_as_longlong(m);
   const uint32_t hw = static_cast<uint32_t>(bits >> 32);
   const uint32_t mh = hw & 0xFFFFFu;
-  const uint32_t h = mh >= 0x6A09Fu ? 1u : 0u;  // halve f (branch-free: shifts and adds by h)
-  const int idx = static_cast<int>(((mh + (0x800u << h)) >> (12u + h)) + 128u - 128u * h);
-  const int e = static_cast<int>((hw >> 20) + h) - 1023;
+  const uint32_t idx = (mh + 0x200u) >> 10;
   const double f = __longlong_as_double(static_cast<long long>(
-      (static_cast<uint64_t>(mh | (0x3FF00000u - (h << 20))) << 32) | (bits & 0xFFFFFFFFull)));
+      (static_cast<uint64_t>(mh | 0x3FF00000u) << 32) | (bits & 0xFFFFFFFFull)));
+  const double k = static_cast<double>(static_cast<int>(hw >> 20) - 1055);
   const double* t = f64_lds().log[idx];
-  const double r = fma(f, t[0], -1.0);
-  double q = -0.16666666666666666;
-  q = fma(q, r, 0.2);
-  q = fma(q, r, -0.25);
-  q = fma(q, r, 0.3333333333333333);
-  q = fma(q, r, -0.5);
+  const double r = fma(f, t[0], 2.0);
+  double q = 0.0125;
+  q = fma(q, r, 0.03125);
+  q = fma(q, r, 0.08333333333333333);
+  q = fma(q, r, 0.25);
   const double p = fma(q, r * r, r);
-  const double k = static_cast<double>(e - 32);
-  return fma(k, 0.6931471805599453, fma(k, 2.3190468138462996e-17, t[1] + (t[2] + p)));
+  return fma(k, kF64M2Ln2Hi, t[1]) + (fma(k, kF64M2Ln2Lo, t[2]) + p);
 }
 
-// sqrt(x) for the Box-Muller radius x = -2 ln u in [1.1e-10, 46.1] (u never 0 or 1): the correctly
+// sqrt(x) for the Box-Muller radius x = -2 ln u in [2.3e-10, 46.1] (u never 0 or 1): the correctly
 // rounded f64 sqrt sequence (rsq seed, one Goldschmidt and two Newton-Raphson corrections) without the
 // denormal / huge-argument scaling and the zero case this range never needs, so the result is the IEEE
 // sqrt the oracle takes.
@@ -244,46 +244,39 @@ __device__ __forceinline__ void sincos2pi_u32(uint32_t b, double& s_out, double&
   c_out = fma(sc.y, cx, -(sc.x * sx));
 }
 
-// The split of e^y: t = fma(y, 64 / ln 2, 1.5 2^52) rounds y 64 / ln 2 to the integer n = 64 m + j held
-// in t's low word (|n| < 2^31), n = t - 1.5 2^52 exactly; r = y - n ln2/64 (Cody-Waite: ln2/64 with 17
-// trailing zero bits plus its remainder, each a fused step; |r| <= 0.0055), e^r - 1 to r^5; e^y =
-// 2^m T (1 + em1) with T = 2^(j/64) from the table.
-struct ExpSplit {
+// Path exponents in units of ln 2 / 256 (kExpUnit: the log-Euler step constants carry the scale):
+// e^y = 2^(ys / 256), ys = y 256 / ln 2.  t = ys + 1.5 2^52 rounds ys to the integer n = 256 m + j held
+// in t's low word (|n| < 2^31), n = t - 1.5 2^52, rr = ys - n exactly (|rr| <= 1/2, Sterbenz);
+// 2^(rr/256) - 1 to degree 4 in rr (E1..E4 = (ln 2 / 256)^k / k!); 2^(ys/256) = 2^m T (1 + em1), T =
+// 2^(j/256) from the table.
+constexpr double kExpUnit = 369.3299304675746;  // 256 / ln 2
+struct Exp2sSplit {
   double T, em1;
   int m;
 };
-__device__ __forceinline__ ExpSplit exp_split(double y) {
-  const double t = fma(y, 92.33248261689366, 6755399441055744.0);
+__device__ __forceinline__ Exp2sSplit exp2s_split(double ys) {
+  const double t = ys + 6755399441055744.0;
   const int ni = static_cast<int>(static_cast<uint32_t>(__double_as_longlong(t)));
-  const double n = t - 6755399441055744.0;
-  double r = fma(-n, 0.010830424696223417, y);
-  r = fma(-n, 2.572804622327669e-14, r);
-  double q = 0.008333333333333333;
-  q = fma(q, r, 0.041666666666666664);
-  q = fma(q, r, 0.16666666666666666);
-  q = fma(q, r, 0.5);
-  return ExpSplit{f64_lds().ex[ni & 63], fma(q, r * r, r), ni >> 6};
+  const double rr = ys - (t - 6755399441055744.0);
+  double q = kF64ExpE4;
+  q = fma(q, rr, kF64ExpE3);
+  q = fma(q, rr, kF64ExpE2);
+  q = fma(q, rr, kF64ExpE1);
+  return Exp2sSplit{f64_lds().ex[ni & 255], q * rr, ni >> 8};
 }
 
-// 2^m x for a normal x and a normal result (no overflow / underflow on the path recursion, |y| < 700):
-// an add to the exponent field, equal to ldexp there.
-__device__ __forceinline__ double scale_exp2(double x, int m) {
-  const uint64_t bits = __double_as_longlong(x);
-  const uint32_t hi = static_cast<uint32_t>(bits >> 32) + (static_cast<uint32_t>(m) << 20);
-  return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | (bits & 0xFFFFFFFFull)));
+// 2^(ys/256) (tests): T (1 + em1) scaled by 2^m.
+__device__ __forceinline__ double exp2s_f64(double ys) {
+  const Exp2sSplit e = exp2s_split(ys);
+  return __builtin_amdgcn_ldexp(fma(e.T, e.em1, e.T), e.m);
 }
 
-// e^y (the f64 recursion of simple paths and the tests): T (1 + em1) scaled by 2^m.
-__device__ __forceinline__ double exp_f64(double y) {
-  const ExpSplit e = exp_split(y);
-  return scale_exp2(fma(e.T, e.em1, e.T), e.m);
-}
-
-// x e^y as the f64 log-Euler step: (x T) (1 + em1) scaled by 2^m.
-__device__ __forceinline__ double mul_exp_f64(double x, double y) {
-  const ExpSplit e = exp_split(y);
+// x 2^(ys/256) as the f64 log-Euler step: (x T) (1 + em1) scaled by 2^m (v_ldexp_f64: exact for the
+// normal values of the path recursion).
+__device__ __forceinline__ double mul_exp2s_f64(double x, double ys) {
+  const Exp2sSplit e = exp2s_split(ys);
   const double xt = x * e.T;
-  return scale_exp2(fma(xt, e.em1, xt), e.m);
+  return __builtin_amdgcn_ldexp(fma(xt, e.em1, xt), e.m);
 }
 
 }  // namespace math

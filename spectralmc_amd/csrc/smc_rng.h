@@ -157,12 +157,12 @@ struct PathStream {
   }
 
   // Two N(0,1) draws, double precision: u1 = (a + 1/2) 2^-32 in (0, 1), angle = b 2^-32 revolutions;
-  // ln u1 and (sin, cos) of the angle from the 32-bit integers (smc_math.h log_u32 / sincos2pi_u32,
+  // -2 ln u1 and (sin, cos) of the angle from the 32-bit integers (smc_math.h m2log_u32 / sincos2pi_u32,
   // restated by the CPU oracle: bit-identical normals), sqrt correctly rounded (sqrt_radius).
   template <bool HW>
   __device__ __forceinline__ void normal_pair(double& z0, double& z1) {
     const uint32_t a = next(), b = next();
-    const double r = math::sqrt_radius(-2.0 * math::log_u32(a));
+    const double r = math::sqrt_radius(math::m2log_u32(a));
     double s, c;
     math::sincos2pi_u32(b, s, c);
     z0 = r * c;
@@ -170,13 +170,14 @@ struct PathStream {
   }
 
   // f64 log-Euler: exponents y = a + (b r) (cos, sin) of the next two steps for the lane's 4 paths (ylo:
-  // step t, yhi: step t + 1), the draws of normal_pair<HW>(double&, double&) with b folded into the
-  // Box-Muller radius (one multiply per pair instead of two)
+  // step t, yhi: step t + 1; a, b in units of ln 2 / 256: smc_math.h mul_exp2s_f64), the draws of
+  // normal_pair<HW>(double&, double&) with b folded into the Box-Muller radius (one multiply per pair
+  // instead of two)
   __device__ __forceinline__ void f64_log_increments4(double b, double a, double (&ylo)[4], double (&yhi)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t ua = next(), ub = next();
-      const double br = math::sqrt_radius(-2.0 * math::log_u32(ua)) * b;
+      const double br = math::sqrt_radius(math::m2log_u32(ua)) * b;
       double s, c;
       math::sincos2pi_u32(ub, s, c);
       ylo[j] = fma(br, c, a);
@@ -189,7 +190,7 @@ struct PathStream {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const uint32_t ua = next(), ub = next();
-      const double br = math::sqrt_radius(-2.0 * math::log_u32(ua)) * b;
+      const double br = math::sqrt_radius(math::m2log_u32(ua)) * b;
       double s, c;
       math::sincos2pi_u32(ub, s, c);
       y[2 * k] = fma(br, c, a);

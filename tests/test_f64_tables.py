@@ -1,4 +1,4 @@
-"""The f64 path-math tables (round 3; round-4 sizes): the device header (spectralmc_amd/csrc/smc_f64_tables.h) and
+"""The f64 path-math tables (round 3; round-4 v3 forms): the device header (spectralmc_amd/csrc/smc_f64_tables.h) and
 the oracle's copy (oracle/f64_tables.h) hold the same bits, and both are what tools/gen_f64_tables.py
 generates (60-digit decimal arithmetic rounded to double), so a hand edit of either breaks parity here
 rather than as an unexplained f64 mismatch on the GPU."""
@@ -30,11 +30,18 @@ def _values(path: str) -> dict[str, list[float]]:
     return out
 
 
+def _consts(path: str) -> dict[str, float]:
+    return {m.group(1): float.fromhex(m.group(2))
+            for m in re.finditer(r"#define (kF64\w+) (-?0x[0-9a-fA-Fp.+-]+)", open(path).read())}
+
+
 def test_device_and_oracle_tables_hold_the_same_bits() -> None:
     dev = _values(os.path.join(ROOT, "spectralmc_amd", "csrc", "smc_f64_tables.h"))
     orc = _values(os.path.join(ROOT, "oracle", "f64_tables.h"))
     assert dev == orc
-    assert [len(dev[k]) for k in ("kF64LogTab", "kF64SinCosTab", "kF64Exp2Tab")] == [256 * 3, 1024 * 2, 64]
+    assert [len(dev[k]) for k in ("kF64LogTab", "kF64SinCosTab", "kF64Exp2Tab")] == [1025 * 3, 1024 * 2, 256]
+    assert _consts(os.path.join(ROOT, "spectralmc_amd", "csrc", "smc_f64_tables.h")) == \
+        _consts(os.path.join(ROOT, "oracle", "f64_tables.h")) == _gen().constants()
 
 
 def test_tables_are_the_generator_output() -> None:
@@ -50,12 +57,21 @@ def test_table_entries_are_near_libm() -> None:
     within 2^-50 absolute, which covers the rounding of the double argument 2 pi j / 256 libm is given;
     the tables themselves are the correctly rounded 60-digit values)."""
     log, sc, ex = _gen().tables()
-    for i, (inv, hi, lo) in zip(range(-128, 128), log):
-        assert inv == 1.0 / (1.0 + i / 256.0)
-        assert abs(hi - (-math.log(inv))) <= 2 * math.ulp(max(abs(hi), 1e-300))
-        assert abs(lo) <= math.ulp(hi) if hi != 0.0 else lo == 0.0
+    consts = _gen().constants()
+    l2hi, l2lo = -consts["kF64M2Ln2Hi"] / 2, -consts["kF64M2Ln2Lo"] / 2
+    assert l2hi == round(l2hi * 2.0**43) / 2.0**43 and abs(l2hi + l2lo - math.log(2)) <= 2 * math.ulp(math.log(2))
+    for i, (m2inv, m2hi, m2lo) in zip(range(0, 1025), log):
+        inv, hi, lo = -m2inv / 2, -m2hi / 2, -m2lo / 2  # stored scaled by -2 (exact)
+        assert inv == 1.0 / (1.0 + i / 1024.0)
+        assert hi == round(hi * 2.0**43) / 2.0**43  # k LN2_HI + T_HI exact for |k| <= 33
+        assert abs((hi + lo) - (-math.log(inv))) <= 2 * math.ulp(max(abs(hi), 1e-300)) if hi else lo == 0.0
+        assert abs(lo) <= 2.0**-43
+    assert (-log[1024][1] / 2, -log[1024][2] / 2) == (l2hi, l2lo)  # c = 2: T = ln 2 exactly as LN2_HI + LN2_LO
     for j, (s, c) in enumerate(sc):
         assert abs(s - math.sin(2 * math.pi * j / 1024)) <= 2 ** -50
         assert abs(c - math.cos(2 * math.pi * j / 1024)) <= 2 ** -50
     for j, v in enumerate(ex):
-        assert abs(v - 2.0 ** (j / 64)) <= math.ulp(v)
+        assert abs(v - 2.0 ** (j / 256)) <= math.ulp(v)
+    for k in range(1, 5):  # (ln 2 / 256)^k / k!
+        assert abs(consts[f"kF64ExpE{k}"] - (math.log(2) / 256) ** k / math.factorial(k)) <= \
+            2 * math.ulp(consts[f"kF64ExpE{k}"])

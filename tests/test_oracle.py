@@ -93,17 +93,19 @@ def test_f64_uniform_transcendentals_are_accurate(oracle) -> None:
     rng = np.random.default_rng(5)
     a_vals = [0, 1, 2, 3, 0x7FFFFFFF, 0xB504F333, 0xFFFFFFFE, 0xFFFFFFFF] + [int(x) for x in rng.integers(0, 2**32, 2000)]
     for a in a_vals:
-        want = math.log((a + 0.5) / 2.0**32)  # (a + 1/2) 2^-32: exact in double, never 0 or 1
-        got = oracle.log_u32(a)
+        want = -2.0 * math.log((a + 0.5) / 2.0**32)  # (a + 1/2) 2^-32: exact in double, never 0 or 1
+        got = oracle.m2log_u32(a)
         assert abs(got - want) <= 2 * math.ulp(want), a
     for b in [0, 1, 2**29 - 1, 2**29, 2**30, 3 * 2**29, 2**31, 2**32 - 2**29, 2**32 - 1] + \
             [int(x) for x in rng.integers(0, 2**32, 2000)]:
         s, c = oracle.sincos2pi_u32(b)
         ws, wc = sincos_ld(b)
         assert abs(s - ws) <= 2.0**-52 and abs(c - wc) <= 2.0**-52, b
-    for y in [-700.0, -50.0, -1e-300, 0.0, 1e-12, 0.34657, 0.5, 1.0, 50.0, 700.0] + list(rng.uniform(-60, 60, 2000)):
-        want = math.exp(y)
-        assert abs(oracle.exp_f64(float(y)) - want) <= 2 * math.ulp(want), y
+    # 2^(ys / 256): ys / 256 is exact, so libm's 2.0 ** (ys / 256) is the correctly rounded value to 1 ulp
+    for ys in [-258000.0, -18000.5, -0.5, -1e-300, 0.0, 1e-12, 0.5, 127.49, 128.0, 18000.0, 258000.0] + \
+            list(rng.uniform(-22000, 22000, 2000)):
+        want = 2.0 ** (ys / 256.0)
+        assert abs(oracle.exp2s_f64(float(ys)) - want) <= 2 * math.ulp(want), ys
 
 
 def test_oracle_normals_are_standard(oracle) -> None:
