@@ -309,9 +309,21 @@ static void normal_pair(mwc64x* g, int is_f64, double* z0, double* z1) {
 /* Normals of one group of 4 paths: z[t][j] for t < rows (f64 holder of dtype values).  Step pairs
  * (t, t + 1): one Box-Muller pair per path j; the last row of an odd count: two pairs, pair k -> paths
  * 2k (z0) and 2k + 1 (z1) (smc_rng.h draw order, round 4). */
+/* Stream span (smc_rng.h, round 4): at T <= 2 a 4-path group draws only 4 T u32 values, so one
+ * Philox-seeded stream serves 4 consecutive groups (16 paths): group g takes the (g mod 4)-th run of
+ * 4 T draws of stream g / 4.  T >= 3: one stream per group. */
+static void group_stream(uint64_t seed, uint64_t ordinal, uint64_t group, int32_t rows, mwc64x* g) {
+  if (rows <= 2) {
+    path_stream(seed, ordinal, group / 4, g);
+    for (int k = 0; k < 4 * rows * (int)(group % 4); ++k) (void)mwc_next(g);
+  } else {
+    path_stream(seed, ordinal, group, g);
+  }
+}
+
 static void group_normals(uint64_t seed, uint64_t ordinal, uint64_t group, int32_t rows, int is_f64, double* z) {
   mwc64x g;
-  path_stream(seed, ordinal, group, &g);
+  group_stream(seed, ordinal, group, rows, &g);
   for (int t = 0; t < rows; t += 2) {
     if (t + 1 < rows) {
       for (int j = 0; j < GROUP; ++j) {

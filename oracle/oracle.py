@@ -261,18 +261,25 @@ def kernel_cf(contracts: np.ndarray, terminal: np.ndarray, terminal_sum: np.ndar
     return out
 
 
+def _wave_shape(timesteps: int, N: int, P: int, normalize: bool) -> bool:
+    """gbm.hip wave_ok: RAW, T <= 2, 1024 | P, 16 | N, N | 1024 (a lane's 16 paths = one stream span of
+    16 adjacent columns)."""
+    return not normalize and timesteps <= 2 and P % 1024 == 0 and N >= 16 and N % 16 == 0 and 1024 % N == 0
+
+
 def engine_wg(timesteps: int, network_size: int, n_paths: int, with_rowsum: bool = False,
               sliced: bool = False, normalize: bool = True) -> int:
     """Lanes whose reduction order an f32 training launch of smc_train_targets follows: 1024 for
     resident_kernel (1 <= T <= 65,536, 4096 | P <= 65,536, N | 4096, 4 <= N <= 1024, no row sums, no
     workspace; gbm.hip resident_ok), P / 4 for packed_kernel (256 <= P <= 2048, P | 4096, 4 | N, N | P:
-    one chunk of P / 4 lanes per contract; gbm.hip packed_ok), 64 for wave_kernel (RAW, T <= 2, 256 | P,
-    4 | N, N | 256: one wave per contract; gbm.hip wave_ok), 512 otherwise."""
+    one chunk of P / 4 lanes per contract; gbm.hip packed_ok), 256 for wave_kernel (one wave per contract
+    walking 1024-path chunks, 16 paths per lane: the column-sum order of 256 four-path lanes, G = 1024 / N
+    batch-row groups; _wave_shape), 512 otherwise."""
     N, P = network_size, n_paths
     if with_rowsum or sliced or not 1 <= timesteps <= 65536:
         return 512
-    if not normalize and timesteps <= 2 and P % 256 == 0 and N >= 4 and N % 4 == 0 and 256 % N == 0:
-        return 64
+    if _wave_shape(timesteps, N, P, normalize):
+        return 256
     if P % 4096 == 0 and P // 4096 <= 16 and 4 <= N <= 1024 and 4096 % N == 0:
         return 1024
     if 256 <= P <= 2048 and 4096 % P == 0 and N >= 4 and N % 4 == 0 and P % N == 0:
@@ -288,8 +295,8 @@ def train_step_order(timesteps: int, network_size: int, n_paths: int, normalize:
     W = 1
     while W < 8 and P > W * 65536:
         W *= 2
-    if engine_wg(timesteps, N, P, normalize=normalize) == 64:
-        return 64, 1
+    if _wave_shape(timesteps, N, P, normalize):
+        return 256, 1
     ok = (1 <= timesteps <= 65536 and P % (W * 4096) == 0 and P // (W * 4096) <= 16 and 4 <= N <= 1024
           and 4096 % N == 0)
     return (1024, W) if ok else (engine_wg(timesteps, N, P, normalize=normalize), 1)

@@ -225,7 +225,7 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
   const bool store_all = STRAIGHT ? STRAIGHT_ALL : a.store == SMC_STORE_ALL;
   const int lane_id = lid < 0 ? static_cast<int>(threadIdx.x) : lid;  // the lane's 4-path slot in the chunk
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(lane_id);
-  PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));  // the lane's group stream
+  PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane), T);  // the lane's group stream
   // f32 HW log-Euler: the RNG hands back the step exponents directly (packed path pairs); f64
   // log-Euler: the exponents too (b folded into the Box-Muller radius), x *= 2^(y/256) (mul_exp2s_f64)
   constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
@@ -338,14 +338,28 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
 // stay in registers from row to row (no replay of earlier rows, no per-row branches).  STORE_ALL:
 // row t at row_base + t * pitch; else only the terminal row, at row_base.  The lane's 4 terminal
 // values go to x_out and their sum (f32 sum for f32 paths, then f64) is added to acc.
+// lane_rows_s: the same on a stream the caller positioned at the group's first draw (wave_kernel walks
+// a whole stream span, smc_rng.h).
+template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
+__device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
+                                            int64_t chunk, Real* contract_base, int T, int64_t pitch, double& acc,
+                                            Real (&x_out)[kPathsPerLane], int lane_id);
+
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                           uint64_t ordinal, int64_t chunk, Real* contract_base, int T, int64_t pitch,
                                           double& acc, Real (&x_out)[kPathsPerLane], int lid = -1) {
-  using V4 = typename Vec4T<Real>::type;
   const int lane_id = lid < 0 ? static_cast<int>(threadIdx.x) : lid;  // the lane's 4-path slot in the chunk
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(lane_id);
-  PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane));
+  PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane), T);
+  lane_rows_s<Real, LOG_EULER, HW, STORE_ALL>(s, step, x0, chunk, contract_base, T, pitch, acc, x_out, lane_id);
+}
+
+template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
+__device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
+                                            int64_t chunk, Real* contract_base, int T, int64_t pitch, double& acc,
+                                            Real (&x_out)[kPathsPerLane], int lane_id) {
+  using V4 = typename Vec4T<Real>::type;
   constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
   constexpr bool kY64 = LOG_EULER && sizeof(Real) == 8;  // exponents drawn directly (lane_paths)
   Real x[kPathsPerLane], zl[kPathsPerLane], zh[kPathsPerLane];
@@ -1320,18 +1334,22 @@ __global__ __launch_bounds__(kResThreads) void packed_kernel(EngineArgs a) {
 
 // ---- wave_kernel: one wave per contract (RAW normalisation, T <= 2) -------------------------------
 // RAW targets need no terminal sum, so a contract's payoffs can be added up as its paths finish, and a
-// whole contract fits one wave: its 64 lanes walk the contract in 256-path chunks (4 paths per lane),
-// add each chunk's payoffs to the lane's four column sums, and after the last chunk the wave alone takes
-// the M-mean and the FFT from its own LDS -- no workgroup barrier per contract.  At the reference's
-// lock-step shape (T = 1, N = 16, M = 4096, RAW: tests/test_gbm_trainer.py:122-142) the 1024-thread
-// resident kernel's per-contract barriers and serial CF phase cost as much as the paths themselves
-// (profiles/r04/ab_lockstep_decomposition.txt).  Orders (oracle kernel mode, wg = 64): item (q, g) =
-// (lane mod N/4, 4 lane / N) adds batch rows m = g, g + 256/N, ... ascending from 0.0 (chunk order), the
-// column sums add g in order from 0.0, the M-mean, then the FFT of fft_row.  Persistent: wave w of the
-// grid runs contracts w, w + (all waves), ...; with a.sobol (smc_train_step) each wave draws its
-// contract's Sobol row and the last workgroup advances the cursor.
+// whole contract fits one wave: its 64 lanes walk the contract in 1024-path chunks, each lane taking 16
+// consecutive paths = one stream span (smc_rng.h: at T <= 2 one Philox-10 seed serves 4 groups of 4
+// paths, drawn in group order), adding each path's payoff to its 16 column sums; after the last chunk the
+// wave alone takes the M-mean and the FFT from its own LDS -- no workgroup barrier per contract.  At the
+// reference's lock-step shape (T = 1, N = 16, M = 4096, RAW: tests/test_gbm_trainer.py:122-142) the
+// 1024-thread resident kernel's per-contract barriers and serial CF phase cost as much as the paths
+// themselves (profiles/r04/ab_lockstep_decomposition.txt), and the per-group Philox seed was the largest
+// part of the paths (T = 1: 4 draws per seed).  Shapes: N a multiple of 16 dividing 1024, so a lane's 16
+// paths are 16 adjacent columns of one batch row.  Orders (oracle kernel mode, wg = 256: G = 1024 / N
+// batch-row groups): lane l adds its columns' rows m = 16 l / N, + G, ... ascending from 0.0 (chunk
+// order), the wave adds the G partials of a column in order from 0.0, the M-mean, then the FFT of
+// fft_row.  Persistent: wave w of the grid runs contracts w, w + (all waves), ...; with a.sobol
+// (smc_train_step) each wave draws its contract's Sobol row and the last workgroup advances the cursor.
 constexpr int kWaveThreads = 256;
-constexpr int kWaveChunk = 64 * kPathsPerLane;  // 256 paths per chunk
+constexpr int kWaveLanePaths = PathStream::kSpanGroups * kPathsPerLane;  // 16 paths per lane and chunk
+constexpr int kWaveChunk = 64 * kWaveLanePaths;                           // 1024 paths per chunk
 constexpr int kWaveMaxT = 2;
 
 size_t wave_lds_bytes(int N) {
@@ -1339,15 +1357,18 @@ size_t wave_lds_bytes(int N) {
   return (static_cast<size_t>(kWaveThreads / 64) * per_wave + 2 * static_cast<size_t>(N)) * sizeof(double);
 }
 
-template <bool LOG_EULER, bool HW, bool STORE_ALL>
-__global__ __launch_bounds__(kWaveThreads) void wave_kernel(EngineArgs a) {
+// 4 waves per SIMD (<= 128 VGPRs): the lock-step batch of 4096 contracts is then exactly one contract
+// per resident wave (256 CUs x 16 waves) instead of 1.33 rounds at 3 waves per SIMD.
+template <bool LOG_EULER, bool HW, bool STORE_ALL, int TT>  // TT = T (1 or 2): no runtime step loop
+__global__ __launch_bounds__(kWaveThreads) __attribute__((amdgpu_waves_per_eu(4))) void wave_kernel(EngineArgs a) {
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int N = a.N, M = a.M, T = a.T;
+  const int N = a.N, M = a.M;
+  constexpr int T = TT;
   const int64_t P = a.P;
   const int64_t pitch = a.pitch ? a.pitch : P;
-  const int cols = N / 4, G = kWaveChunk / N;  // column quads, batch rows per chunk
-  const int q = lane % cols, g = lane / cols;
+  const int G = kWaveChunk / N;  // batch rows per chunk
+  const int g = kWaveLanePaths * lane / N, n0 = kWaveLanePaths * lane % N;  // the lane's row and columns
   const int per_wave = kWaveChunk + 3 * N + 8;
   double* part = lds + wave * per_wave;  // [G][N]
   double* avg = part + kWaveChunk;       // [N]
@@ -1379,17 +1400,25 @@ __global__ __launch_bounds__(kWaveThreads) void wave_kernel(EngineArgs a) {
     const float x0 = static_cast<float>(c.X0);
     const Payoff<float> pay(a, PayoffPre<float>(c), 1.0);  // RAW: scale 1
     float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * T * pitch : b * pitch);
-    double colsum[kPathsPerLane] = {0.0, 0.0, 0.0, 0.0};
+    double colsum[kWaveLanePaths];
+#pragma unroll
+    for (int k = 0; k < kWaveLanePaths; ++k) colsum[k] = 0.0;
     double acc = 0.0;  // (the terminal sum: not needed for RAW targets)
     for (int64_t chunk = 0; chunk < P; chunk += kWaveChunk) {
-      float xt[kPathsPerLane];
-      lane_rows<float, LOG_EULER, HW, STORE_ALL>(a, step, x0, static_cast<uint64_t>(ord0 + b), chunk, base, T, pitch,
-                                                 acc, xt, lane);
+      // the lane's span: stream (chunk + 16 lane) / 16, its 4 groups in order
+      PathStream s(a.seed, static_cast<uint64_t>(ord0 + b),
+                   static_cast<uint64_t>((chunk + kWaveLanePaths * lane) / kWaveLanePaths));
 #pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) colsum[j] += static_cast<double>(pay(xt[j]));
+      for (int j = 0; j < PathStream::kSpanGroups; ++j) {
+        float xt[kPathsPerLane];
+        lane_rows_s<float, LOG_EULER, HW, STORE_ALL>(s, step, x0, chunk, base, T, pitch, acc, xt,
+                                                     PathStream::kSpanGroups * lane + j);
+#pragma unroll
+        for (int i = 0; i < kPathsPerLane; ++i) colsum[kPathsPerLane * j + i] += static_cast<double>(pay(xt[i]));
+      }
     }
 #pragma unroll
-    for (int j = 0; j < kPathsPerLane; ++j) part[g * N + 4 * q + j] = colsum[j];
+    for (int k = 0; k < kWaveLanePaths; ++k) part[g * N + n0 + k] = colsum[k];
     wave_lds_sync();
     for (int n = lane; n < N; n += 64) {
       double t = 0.0;
@@ -1414,8 +1443,8 @@ __global__ __launch_bounds__(kWaveThreads) void wave_kernel(EngineArgs a) {
 
 bool wave_ok(const EngineArgs& a, bool f32) {
   return f32 && a.simulate && a.targets && !a.normalize && !a.all_rows && a.slices <= 1 && a.res_slices <= 1 &&
-         a.T >= 1 && a.T <= kWaveMaxT && a.P % kWaveChunk == 0 && a.N >= 4 && a.N % 4 == 0 &&
-         kWaveChunk % a.N == 0 && (a.pitch == 0 || (a.pitch % 4 == 0 && a.pitch >= a.P));
+         a.T >= 1 && a.T <= kWaveMaxT && a.P % kWaveChunk == 0 && a.N >= kWaveLanePaths &&
+         a.N % kWaveLanePaths == 0 && kWaveChunk % a.N == 0 && (a.pitch == 0 || (a.pitch % 4 == 0 && a.pitch >= a.P));
 }
 
 bool packed_ok(const EngineArgs& a, bool f32) {
@@ -1546,7 +1575,7 @@ __global__ __launch_bounds__(256) void normals_kernel(uint64_t seed, uint64_t or
   if constexpr (sizeof(Real) == 8) math::f64_tables_load();  // before any thread leaves
   const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;  // path group
   if (g * kPathsPerLane >= cols) return;
-  PathStream s(seed, ordinal, static_cast<uint64_t>(g));
+  PathStream s(seed, ordinal, static_cast<uint64_t>(g), rows);
   const Real zs = sizeof(Real) == 4 ? static_cast<Real>(PathStream::kNormalScale<HW>) : Real(1);
   Real z0[kPathsPerLane], z1[kPathsPerLane];
   for (int t = 0; t < rows; ++t) {
@@ -1767,7 +1796,7 @@ int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
 
 template <bool LOG_EULER, bool HW, bool STORE_ALL>
 int32_t launch_wave_k(const EngineArgs& a, hipStream_t stream) {
-  auto kernel = wave_kernel<LOG_EULER, HW, STORE_ALL>;
+  auto kernel = a.T == 1 ? wave_kernel<LOG_EULER, HW, STORE_ALL, 1> : wave_kernel<LOG_EULER, HW, STORE_ALL, 2>;
   const size_t lds = wave_lds_bytes(a.N);
   if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -72,6 +72,20 @@ struct PathStream {
     x ^= static_cast<uint32_t>(x == 0xFFFFFFFFu && c == kMwcA - 1u);
   }
 
+  // Stream span (round 4): at T <= 2 a 4-path group draws only 4 T u32 values, so one Philox-seeded
+  // stream serves kSpanGroups consecutive groups (16 paths) and the Philox-10 seed is paid once per 16
+  // paths instead of once per 4: group g takes the (g mod 4)-th run of 4 T draws of stream g / 4.
+  // T >= 3: one stream per group.  This constructor positions the stream at group g's first draw (a
+  // kernel that walks a whole span, wave_kernel, seeds stream g / 4 once and draws the groups in order).
+  static constexpr int kSpanGroups = 4;
+  __device__ __forceinline__ PathStream(uint64_t mc_seed, uint64_t ordinal, uint64_t group, int T)
+      : PathStream(mc_seed, ordinal, T <= 2 ? group / kSpanGroups : group) {
+    if (T <= 2) {
+      const int skip = 4 * T * static_cast<int>(group % kSpanGroups);
+      for (int k = 0; k < skip; ++k) (void)next();
+    }
+  }
+
   __device__ __forceinline__ uint32_t next() {
     const uint32_t r = x ^ c;
     const uint64_t t = static_cast<uint64_t>(kMwcA) * x + c;

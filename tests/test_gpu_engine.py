@@ -63,10 +63,12 @@ def test_device_sobol_far_index_matches_host() -> None:
 
 
 # ------------------------------------------------------------------------------ RNG
+@pytest.mark.parametrize("rows", [17, 1, 2])
 @pytest.mark.parametrize("dtype", ["float32", "float64"])
-def test_normals_match_oracle(oracle, dtype) -> None:
-    """f32: bit-exact (portable Box-Muller); f64: libm vs OCML transcendentals, 1e-12."""
-    rows, cols = 17, 5003
+def test_normals_match_oracle(oracle, dtype, rows) -> None:
+    """f32: bit-exact (portable Box-Muller); f64: the table-driven f64 math restated, 1e-12 (bit-exact in
+    practice).  rows 1, 2: the stream span of small T (4 groups per Philox-seeded stream)."""
+    cols = 5003
     tdt = torch.float32 if dtype == "float32" else torch.float64
     z = torch.empty((rows, cols), dtype=tdt, device=DEV)
     _lib.check(_L().smc_normals(7, 5, rows, cols, 0 if dtype == "float32" else 1, _lib.ptr(z), None))
@@ -623,24 +625,25 @@ def test_packed_train_step_matches_oracle(oracle, golden, B, T, N, M, normalize,
 
 WAVE_CASES = [  # (B, T, N, M, store): RAW, T <= 2 -> wave_kernel, one wave per contract
     (4096, 1, 16, 4096, _lib.STORE_ALL),      # the reference's lock-step shape at C2's batch (bench "lockstep")
-    (333, 2, 64, 64, _lib.STORE_ALL),          # T = 2, more contracts than one per wave? (no: < 4096 waves)
+    (333, 2, 64, 64, _lib.STORE_ALL),          # T = 2: 8 draws per group, 4 groups per stream span
     (5000, 1, 256, 16, _lib.STORE_TERMINAL),   # more contracts than resident waves: two rounds; N = 256
+    (70, 2, 1024, 2, _lib.STORE_TERMINAL),     # N = 1024: one batch row per chunk
 ]
 
 
 @pytest.mark.parametrize("B,T,N,M,store", WAVE_CASES)
 def test_wave_train_step_matches_oracle(oracle, golden, B, T, N, M, store) -> None:
     """RAW targets at T <= 2 (the reference's lock-step trainer shape, tests/test_gbm_trainer.py:122-142):
-    smc_train_step runs one wave per contract (wave_kernel: payoffs added as the chunks finish, the
-    M-mean and FFT by the wave alone).  Portable math bit-exact with the kernel-mode oracle in the wave's
-    order (wg = 64); hw math within 1e-5 of the reference mode; contracts equal the Sobol draw; the
+    smc_train_step runs one wave per contract (wave_kernel: 16 paths = one stream span per lane,
+    payoffs added as the chunks finish, the M-mean and FFT by the wave alone).  Portable math bit-exact
+    with the kernel-mode oracle in the wave's order (wg = 256); hw math within 1e-5 of the reference mode; contracts equal the Sobol draw; the
     stored terminal rows equal the kernel-mode paths; the sync area is left zeroed."""
     L = _L()
     P = N * M
     pitch = int(L.smc_path_pitch(P, 0))
     assert L.smc_train_step_kernel(T, N, M, _lib.QUERY_RAW, pitch) == b"wave_kernel"
     assert L.smc_train_step_kernel(T, N, M, 0, pitch) != b"wave_kernel"  # NORMALIZE needs the terminal sum first
-    assert oracle.train_step_order(T, N, P, normalize=False) == (64, 1)
+    assert oracle.train_step_order(T, N, P, normalize=False) == (256, 1)
     eng = SobolEngine(6, 7, 0)
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
@@ -669,9 +672,9 @@ def test_wave_train_step_matches_oracle(oracle, golden, B, T, N, M, store) -> No
             sub = np.arange(0, B, 7)  # every 7th contract (its own normal ordinal): the oracle loops per contract
             for b in sub[:64]:
                 kt, _ = oracle.kernel_targets(contracts[b:b + 1], T, N, M, seed=43, ordinal0=3 + int(b),
-                                              normalize=False, wg=64)
+                                              normalize=False, wg=256)
                 np.testing.assert_array_equal(got[b:b + 1], kt)
-            kp, _, _ = oracle.kernel_paths(contracts[:2], T, P, 43, ordinal0=3, want_paths=True, wg=64)
+            kp, _, _ = oracle.kernel_paths(contracts[:2], T, P, 43, ordinal0=3, want_paths=True, wg=256)
             if store == _lib.STORE_ALL:
                 np.testing.assert_array_equal(paths[:2, :, :P].cpu().numpy(), kp)
             else:

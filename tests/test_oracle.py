@@ -61,6 +61,34 @@ def test_oracle_stream_is_mwc64x(oracle, seed, ordinal, group) -> None:
     assert got.tolist() == _mwc64x_reference(seed, ordinal, group, 200)
 
 
+@pytest.mark.parametrize("rows", [1, 2, 3])
+def test_oracle_stream_span_at_small_t(oracle, rows) -> None:
+    """Stream span (smc_rng.h, round 4): at T <= 2 group g (paths 4g .. 4g + 3) takes the (g mod 4)-th run
+    of 4 T draws of the stream of g / 4 (one Philox-10 seed per 16 paths); T >= 3: one stream per group.
+    Restated here from the raw streams and the f64 Box-Muller pieces: pair k of a group is
+    (a, b) -> sqrt(-2 ln u(a)) (cos, sin)(2 pi b 2^-32); T = 1 takes pairs 0, 1 for paths (0, 1), (2, 3);
+    T = 2 one pair per path (z0 -> row 0, z1 -> row 1)."""
+    seed, ordinal, cols = 7, 3, 64
+    z = oracle.normals(seed, ordinal, rows, cols, "float64")
+    for grp in range(cols // 4):
+        span = rows <= 2
+        words = oracle.stream_u32(seed, ordinal, grp // 4 if span else grp, 64).tolist()
+        if span:
+            words = words[4 * rows * (grp % 4):]
+        pairs = []
+        for k in range(0, 2 * (4 if rows >= 2 else 2), 2):
+            a, b = words[k], words[k + 1]
+            r = math.sqrt(oracle.m2log_u32(a))
+            sn, cs = oracle.sincos2pi_u32(b)
+            pairs.append((r * cs, r * sn))
+        for j in range(4):
+            if rows == 1:
+                want = pairs[j // 2][j % 2]
+                assert z[0, 4 * grp + j] == want, (grp, j)
+            else:
+                assert (z[0, 4 * grp + j], z[1, 4 * grp + j]) == pairs[j], (grp, j)
+
+
 def test_oracle_stream_bits_are_uniform(oracle) -> None:
     """Top-23-bit uniforms of 4096 streams x 64 draws (the draws of one C2 chunk): mean, variance and
     lag-1 / cross-stream correlation at the level a 262,144-sample test resolves."""

@@ -94,6 +94,9 @@ for step in "$@"; do
     py:*)  # py:<tag>:<script and args with , for spaces> (a python tool under its own limit)
       IFS=: read -r _ tag args <<< "$step"
       run "py_$tag" 300 python -u ${args//,/ } ;;
+    profnet:*)  # profnet:<arch>[:compute] -> rocprofv3 kernel stats of the isolated network step
+      IFS=: read -r _ arch comp <<< "$step"
+      cd /tmp && run "profnet_${arch}" 300 rocprofv3 --kernel-trace --stats -d "$OUT/profnet_${arch}" -o run --output-format csv -- python "$ROOT/tools/kprof_net.py" --arch "$arch" --compute "${comp:-mfma}"; cd "$ROOT" ;;
     abnet:*)  # abnet:<tag>:<kprof_net args with , for spaces>:<variant names with ,> (isolated network step)
       IFS=: read -r _ tag args names <<< "$step"
       AB_SCRIPT=tools/kprof_net.py run "abnet_$tag" 900 bash tools/micro/ab.sh "$OUT/abnet_$tag.txt" "${args//,/ }" ${names//,/ } ;;
