@@ -761,19 +761,23 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   const int64_t n0 = static_cast<int64_t>(nb) * kLN;
   constexpr int AV = kLM * kLK / 4 / kLThreads, BV = kLN * kLK / 4 / kLThreads;
   f32x4 ra[AV], rb[BV];
+  // every load is issued (out-of-range pieces read element 0 and are zeroed by a select): a guarded
+  // load compiles to a branch around it, eight per stage
   auto fetch = [&](int k0) {
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       const int i = v * kLThreads + tid, r = i / (kLK / 4), q = i % (kLK / 4);
       const bool ok = m0 + r < Mrows && k0 + 4 * q < K;
-      ra[v] = ok ? *reinterpret_cast<const f32x4*>(A + static_cast<int64_t>(m0 + r) * lda + kbeg + k0 + 4 * q)
-                 : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 x = *reinterpret_cast<const f32x4*>(
+          A + (ok ? static_cast<int64_t>(m0 + r) * lda + kbeg + k0 + 4 * q : 0));
+      ra[v] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
       const int i = v * kLThreads + tid, r = i / (kLK / 4), q = i % (kLK / 4);
-      rb[v] = n0 + r < Nrows && k0 + 4 * q < K ? *reinterpret_cast<const f32x4*>(B + (n0 + r) * ldb + kbeg + k0 + 4 * q)
-                                               : f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool ok = n0 + r < Nrows && k0 + 4 * q < K;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(B + (ok ? (n0 + r) * ldb + kbeg + k0 + 4 * q : 0));
+      rb[v] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
   auto put = [&](int buf) {
@@ -814,37 +818,50 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   for (int i = 0; i < kLTM; ++i)
 #pragma unroll
     for (int j = 0; j < kLTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nst = (K + kLK - 1) / kLK;
+  // full K stages run their kLK / 16 blocks unconditionally; the last, partial stage (K a multiple of 16)
+  // its remaining blocks: no per-block branch around the MFMAs (each made the accumulators round-trip
+  // through VGPRs at the join)
+  const int nfull = K / kLK, tail = (K % kLK) / 16;
+  const int nst = nfull + (tail ? 1 : 0);
+  f32x4 af[2][kLTM], bf[2][kLTN];
+  auto ld = [&](int buf, int s, int kb) {
+#pragma unroll
+    for (int i = 0; i < kLTM; ++i)
+      af[s][i] = *reinterpret_cast<const f32x4*>(&sa[buf][((wave * kLTM + i) * 16 + c) * kLLd + kb + 4 * g]);
+#pragma unroll
+    for (int j = 0; j < kLTN; ++j)
+      bf[s][j] = *reinterpret_cast<const f32x4*>(&sb[buf][(j * 16 + c) * kLLd + kb + 4 * g]);
+  };
+  auto mma = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < kLTM; ++i)
+#pragma unroll
+      for (int j = 0; j < kLTN; ++j) acc[i][j] = OpF32::mmav(acc[i][j], af[s][i], bf[s][j]);
+  };
   fetch(0);
   put(0);
   __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1, k0 = st * kLK;
-    if (st + 1 < nst) fetch(k0 + kLK);
-    f32x4 af[2][kLTM], bf[2][kLTN];
-    auto ld = [&](int s, int kb) {
-#pragma unroll
-      for (int i = 0; i < kLTM; ++i)
-        af[s][i] = *reinterpret_cast<const f32x4*>(&sa[buf][((wave * kLTM + i) * 16 + c) * kLLd + kb + 4 * g]);
-#pragma unroll
-      for (int j = 0; j < kLTN; ++j)
-        bf[s][j] = *reinterpret_cast<const f32x4*>(&sb[buf][(j * 16 + c) * kLLd + kb + 4 * g]);
-    };
-    ld(0, 0);
+  // the full K stages: the kLK / 16 blocks unconditionally (no branch around the MFMAs, whose join made
+  // the accumulators round-trip through VGPRs); the next stage's loads in flight meanwhile
+  for (int st = 0; st < nfull; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) fetch((st + 1) * kLK);
+    ld(buf, 0, 0);
 #pragma unroll
     for (int kb = 0; kb < kLK; kb += 16) {
       const int s = (kb / 16) & 1;
-      if (kb + 16 < kLK) ld(s ^ 1, kb + 16);
-      if (k0 + kb < K) {  // uniform: K is a multiple of 16
-#pragma unroll
-        for (int i = 0; i < kLTM; ++i)
-#pragma unroll
-          for (int j = 0; j < kLTN; ++j) acc[i][j] = OpF32::mmav(acc[i][j], af[s][i], bf[s][j]);
-      }
+      if (kb + 16 < kLK) ld(buf, s ^ 1, kb + 16);
+      mma(s);
     }
     if (st + 1 < nst) put(buf ^ 1);
     __syncthreads();
   }
+  // the partial last stage (K a multiple of 16): its remaining blocks
+  for (int b = 0; b < tail; ++b) {
+    ld(nfull & 1, 0, 16 * b);
+    mma(0);
+  }
+  if (tail) __syncthreads();  // the epilogue tile reuses the stage buffers
 
   // ---- epilogue, through LDS: the accumulators go to a [feature][row] tile; each thread then takes
   // 4 features of one batch row (row-major outputs, 16-B stores along the features) and finally whole
