@@ -340,10 +340,12 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
 // values go to x_out and their sum (f32 sum for f32 paths, then f64) is added to acc.
 // lane_rows_s: the same on a stream the caller positioned at the group's first draw (wave_kernel walks
 // a whole stream span, smc_rng.h).
+// stage (LDS, optional): the rows go there instead of to HBM, row r at stage + r * stage_stride + 4 lane_id
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                             int64_t chunk, Real* contract_base, int T, int64_t pitch, double& acc,
-                                            Real (&x_out)[kPathsPerLane], int lane_id);
+                                            Real (&x_out)[kPathsPerLane], int lane_id, Real* stage = nullptr,
+                                            int stage_stride = 0);
 
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
@@ -358,7 +360,8 @@ __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Rea
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                             int64_t chunk, Real* contract_base, int T, int64_t pitch, double& acc,
-                                            Real (&x_out)[kPathsPerLane], int lane_id) {
+                                            Real (&x_out)[kPathsPerLane], int lane_id, Real* stage,
+                                            int stage_stride) {
   using V4 = typename Vec4T<Real>::type;
   constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
   constexpr bool kY64 = LOG_EULER && sizeof(Real) == 8;  // exponents drawn directly (lane_paths)
@@ -395,7 +398,12 @@ __device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, L
     v.y = x[1];
     v.z = x[2];
     v.w = x[3];
-    store_row(row, lane_off, v);
+    if (stage) {
+      *reinterpret_cast<V4*>(stage + kPathsPerLane * lane_id) = v;
+      stage += stage_stride;
+    } else {
+      store_row(row, lane_off, v);
+    }
   };
 #pragma unroll 1
   for (int t = 0; t + 1 < T; t += 2) {
@@ -1351,6 +1359,9 @@ constexpr int kWaveThreads = 256;
 constexpr int kWaveLanePaths = PathStream::kSpanGroups * kPathsPerLane;  // 16 paths per lane and chunk
 constexpr int kWaveChunk = 64 * kWaveLanePaths;                           // 1024 paths per chunk
 constexpr int kWaveMaxT = 2;
+#ifndef SMC_WAVE_DENSE
+#define SMC_WAVE_DENSE 1
+#endif
 
 size_t wave_lds_bytes(int N) {
   const size_t per_wave = kWaveChunk + 3 * static_cast<size_t>(N) + 8;  // part [G][N], avg, re, im, row
@@ -1404,6 +1415,8 @@ __global__ __launch_bounds__(kWaveThreads) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
     for (int k = 0; k < kWaveLanePaths; ++k) colsum[k] = 0.0;
     double acc = 0.0;  // (the terminal sum: not needed for RAW targets)
+    float* stage = reinterpret_cast<float*>(part);  // [rows][1024] f32: part is free until the chunks end
+    constexpr int kRows = STORE_ALL ? TT : 1;
     for (int64_t chunk = 0; chunk < P; chunk += kWaveChunk) {
       // the lane's span: stream (chunk + 16 lane) / 16, its 4 groups in order
       PathStream s(a.seed, static_cast<uint64_t>(ord0 + b),
@@ -1412,9 +1425,25 @@ __global__ __launch_bounds__(kWaveThreads) __attribute__((amdgpu_waves_per_eu(4)
       for (int j = 0; j < PathStream::kSpanGroups; ++j) {
         float xt[kPathsPerLane];
         lane_rows_s<float, LOG_EULER, HW, STORE_ALL>(s, step, x0, chunk, base, T, pitch, acc, xt,
-                                                     PathStream::kSpanGroups * lane + j);
+                                                     PathStream::kSpanGroups * lane + j,
+                                                     SMC_WAVE_DENSE ? stage : nullptr, kWaveChunk);
 #pragma unroll
         for (int i = 0; i < kPathsPerLane; ++i) colsum[kPathsPerLane * j + i] += static_cast<double>(pay(xt[i]));
+      }
+      if constexpr (SMC_WAVE_DENSE) {
+        // the chunk's rows from LDS: each store instruction 64 lanes x 16 B contiguous (a lane's own 64 B
+        // would make every instruction a quarter-dense 4 KiB stripe)
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+          char* rowp = reinterpret_cast<char*>(base + (STORE_ALL ? r * pitch : 0) + chunk);
+#pragma unroll
+          for (int k = 0; k < kWaveChunk / 256; ++k) {
+            const float4 v = *reinterpret_cast<const float4*>(stage + r * kWaveChunk + 256 * k + kPathsPerLane * lane);
+            store_row(rowp + 1024 * k, static_cast<uint32_t>(16 * lane), v);
+          }
+        }
+        wave_lds_sync();  // the stage is rewritten by the next chunk
       }
     }
 #pragma unroll

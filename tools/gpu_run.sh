@@ -91,6 +91,9 @@ for step in "$@"; do
     ab:*)  # ab:<tag>:<kprof_step args with , for spaces>:<variant names with ,> (tools/micro/ab.sh)
       IFS=: read -r _ tag args names <<< "$step"
       run "ab_$tag" 900 bash tools/micro/ab.sh "$OUT/ab_$tag.txt" "${args//,/ }" ${names//,/ } ;;
+    probe:*)  # probe:<binary under tools/micro/v> (a stand-alone microbenchmark)
+      IFS=: read -r _ name <<< "$step"
+      run "probe_$name" 180 "tools/micro/v/$name" ;;
     py:*)  # py:<tag>:<script and args with , for spaces> (a python tool under its own limit)
       IFS=: read -r _ tag args <<< "$step"
       run "py_$tag" 300 python -u ${args//,/ } ;;

@@ -19,7 +19,8 @@ def main() -> None:
                 for row in csv.DictReader(fh):
                     if a.kernel not in row["Kernel_Name"]:
                         continue
-                    k = (row["Kernel_Name"].split("(")[0][-60:], row["Counter_Name"])
+                    name = row["Kernel_Name"].replace("(anonymous namespace)::", "")
+                    k = (name.split("(")[0][-60:], row["Counter_Name"])
                     disp = int(row["Dispatch_Id"])
                     vals[k][disp] = vals[k].get(disp, 0.0) + float(row["Counter_Value"])
         print(d)
