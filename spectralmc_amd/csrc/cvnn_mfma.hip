@@ -538,6 +538,9 @@ __device__ void wgrad_bookkeeping(const MArgs& a, int64_t item, int wave, int la
   }
 }
 
+#ifndef SMC_WGRAD_KS_F32
+#define SMC_WGRAD_KS_F32 32  // f32 batch rows per K stage (the bf16 stage's 36 KiB of LDS)
+#endif
 constexpr int kWgBlock = 64;  // output block edge
 constexpr int kWgStage = 64;  // batch rows per K stage (bf16; 32 for f32: the same 36 KiB of LDS)
 
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
   using V = typename Op::V;
   constexpr int KB = Op::KB, KQ = KB / 4;
   constexpr int ES = static_cast<int>(sizeof(T));
-  constexpr int KS = ES == 2 ? kWgStage : kWgStage / 2;  // batch rows per K stage
+  constexpr int KS = ES == 2 ? kWgStage : SMC_WGRAD_KS_F32;  // batch rows per K stage
   constexpr int LD = KS + 16 / ES;                       // LDS row stride (elements): odd multiple of 16 B
   constexpr int PER = kWgBlock * KS / kThreads;          // elements each thread stages per operand
   constexpr int NV = PER * ES / 16;                   // 16-byte loads per operand per thread
@@ -737,13 +740,17 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   // workgroup w runs on XCD w % 8; each XCD takes a contiguous eighth of the batch blocks with every
   // feature block, and reads only its eighth of the row operand (B) and the whole weight matrix (A)
   // into its own L2, instead of every XCD streaming all of B past one feature block
+  // (NB not a multiple of 8: the grid is rounded up to 8 equal XCD ranges and the workgroups past the
+  // last batch block return at once)
   const int MB = static_cast<int>(a.lgemm_mb);
-  const int NB = static_cast<int>(gridDim.x) / MB;
+  const int NB = static_cast<int>(a.bp / kLN);
   int mb, nb;
-  if (SMC_LGEMM_XCD && NB % 8 == 0) {
+  if (SMC_LGEMM_XCD) {
+    const int per = (NB + 7) >> 3;
     const int xcd = static_cast<int>(blockIdx.x) & 7, local = static_cast<int>(blockIdx.x) >> 3;
-    nb = xcd * (NB >> 3) + local / MB;
+    nb = xcd * per + local / MB;
     mb = local % MB;
+    if (nb >= NB) return;  // uniform, before any barrier
   } else {
     mb = static_cast<int>(blockIdx.x) % MB;
     nb = static_cast<int>(blockIdx.x) / MB;
@@ -1145,17 +1152,18 @@ int32_t launch_layered(const Plan& p, hipStream_t s) {
   if (int32_t rc = check_launch("cvnn lpack_kernel")) return rc;
   const unsigned by = static_cast<unsigned>(a.bp / kLN);
   const int L = a.n_layers;
-  MArgs g = a;  // lgemm_mb: the launch's feature blocks (1-D grid of lgemm_mb x by workgroups)
+  MArgs g = a;  // lgemm_mb: the launch's feature blocks (1-D grid of lgemm_mb x (by rounded to 8) workgroups)
+  const unsigned byx = SMC_LGEMM_XCD ? (by + 7) / 8 * 8 : by;
   for (int l = 0; l < L; ++l) {
     g.lgemm_mb = (a.layer[l].wout + kLM - 1) / kLM;
-    const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * by);
+    const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * byx);
     if (l + 1 < L) hipLaunchKernelGGL(lgemm_kernel<kLFwd>, grid, dim3(kLThreads), 0, s, g, l);
     else hipLaunchKernelGGL(lgemm_kernel<kLLast>, grid, dim3(kLThreads), 0, s, g, l);
     if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
   }
   for (int l = L - 1; l >= 1; --l) {
     g.lgemm_mb = (a.layer[l].win + kLM - 1) / kLM;
-    const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * by);
+    const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * byx);
     hipLaunchKernelGGL(lgemm_kernel<kLBwd>, grid, dim3(kLThreads), 0, s, g, l);
     if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
   }

@@ -38,7 +38,7 @@ namespace {
 // rows_kernel occupancy: 8 waves per SIMD (<= 64 VGPRs) = 4 workgroups per CU, so C2's 4096 contracts
 // are exactly 4 rounds of 1024 persistent workgroups (at 69 VGPRs: 3 per CU, 5.33 rounds)
 #ifndef SMC_ROWS_WAVES_F64
-#define SMC_ROWS_WAVES_F64 6
+#define SMC_ROWS_WAVES_F64 5
 #endif
 #ifndef SMC_ROWS_WAVES
 #define SMC_ROWS_WAVES 8
@@ -385,8 +385,7 @@ __device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, L
     if constexpr (kPacked) {
       advance_packed(x, z);
     } else if constexpr (kY64) {
-#pragma unroll
-      for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp2s_f64(x[j], z[j]);
+      math::mul_exp2s_f64_x4(x, z);
     } else {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], z[j]);
@@ -827,10 +826,11 @@ __global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
 // contract by blockIdx.x and every later one from the counter, so a workgroup that starts late (a
 // concurrent network kernel held its slot) takes fewer contracts instead of finishing last; the
 // last workgroup out resets the counters.  Which workgroup runs a contract changes no result.
-// f64 rows run at 6 waves per SIMD (SMC_ROWS_WAVES_F64; round 4 A/B on MI355X, C2-f64: 9.01 ms at 6 vs
-// 9.20-9.28 ms at 8 waves, and 9.49-9.53 ms with the CF phase fused into this kernel, which then re-read
-// the terminal row while its own path math waited): the f64 path math is VALU-bound and the larger
-// register budget removes its spills.
+// f64 rows run at 5 waves per SIMD (SMC_ROWS_WAVES_F64; round 4 A/Bs on MI355X, C2-f64: v2 math 9.01 ms
+// at 6 vs 9.20-9.28 ms at 8 waves, and 9.49-9.53 ms with the CF phase fused into this kernel, which then
+// re-read the terminal row while its own path math waited; v3 math 8.47-8.50 ms at 5 vs 8.65-8.67 ms at
+// 6, where the 80-VGPR budget spilled outside the path loop): the larger register budget is worth more
+// than the sixth wave.
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof(Real) == 8 ? SMC_ROWS_WAVES_F64
                                                                                               : SMC_ROWS_WAVES)))
