@@ -676,7 +676,10 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
 #ifndef SMC_LGEMM_XCD
 #define SMC_LGEMM_XCD 1
 #endif
-constexpr int kLM = SMC_LGEMM_M, kLN = 64, kLK = SMC_LGEMM_K, kLLd = kLK + 4;  // tile (features x batch rows), K stage, LDS stride
+#ifndef SMC_LGEMM_N
+#define SMC_LGEMM_N 64
+#endif
+constexpr int kLM = SMC_LGEMM_M, kLN = SMC_LGEMM_N, kLK = SMC_LGEMM_K, kLLd = kLK + 4;  // tile (features x batch rows), K stage, LDS stride
 constexpr int kLThreads = 256;  // 4 waves x (kLM / 4 features x 64 rows); kLM = 64: 512 workgroups at H = 256 (263 vs 269 us per step with 128)
 constexpr int kLTM = kLM / 4 / 16, kLTN = kLN / 16;           // 16 x 16 tiles per wave
 enum { kLFwd = 0, kLLast = 1, kLBwd = 2 };
