@@ -97,6 +97,9 @@ def parse() -> argparse.Namespace:
     return ap.parse_args()
 
 
+ON_CHIP_KERNELS = ("resident_kernel", "wave_kernel", "packed_kernel", "basket_resident_kernel")
+
+
 def algorithmic_bytes_per_contract(T: int, N: int, M: int, store_all: bool, esz: int = 4) -> int:
     """SURVEY §8(d): path matrix store + terminal-row re-read + complex targets (+ 48 B contract in);
     esz = 4 (f32 paths, complex64 targets) or 8 (f64, complex128)."""
@@ -321,10 +324,17 @@ def main() -> None:
     kernel_ms = ev0.elapsed_time(ev1) / (args.kernel_iters * launches_per_call)
     contracts_per_launch = min(eng.chunk, eng.B)
     if n_assets:
-        bytes_launch = eng.algorithmic_bytes_per_contract() * contracts_per_launch
+        bytes_survey = eng.algorithmic_bytes_per_contract() * contracts_per_launch
     else:
-        bytes_launch = algorithmic_bytes_per_contract(T, N, M, pricer.store_paths, esz) * contracts_per_launch + \
+        bytes_survey = algorithmic_bytes_per_contract(T, N, M, pricer.store_paths, esz) * contracts_per_launch + \
             48 * contracts_per_launch
+    # the kernel's own algorithmic bytes: SURVEY §8(d)'s per-contract figure counts a terminal-row re-read
+    # (P values per asset) that the kernels keeping the terminal row on chip never make; for those the
+    # figure with it would credit bytes nobody moves (at the lock-step shape it is twice the real
+    # traffic and implies more than the HBM peak)
+    on_chip = eng.kernel_name in ON_CHIP_KERNELS
+    reread = ((n_assets or 1) * P * (4 if n_assets else esz) * contracts_per_launch) if on_chip else 0
+    bytes_launch = bytes_survey - reread
     # live: HIP events on the MC stream around each MC-part launch inside the timed region
     # (Sobol draw + path/CF kernel + cursor update; the path/CF kernel is >99 % of it)
     live = [a.elapsed_time(b_) for a, b_ in (session.mc_events or [])]
@@ -466,6 +476,10 @@ def main() -> None:
                                  "of this run records each overlapped launch from its dispatch to its end"
                                  if lanes > 1 else None),
                      "algorithmic_bytes_per_launch": bytes_launch,
+                     "algorithmic_bytes_survey_per_launch": bytes_survey,
+                     "bytes_note": ("the kernel keeps each contract's terminal row on chip: achieved counts the path "
+                                    "store, targets and contract rows, not the terminal re-read of SURVEY 8(d)'s "
+                                    "per-contract figure (algorithmic_bytes_survey_per_launch)" if on_chip else None),
                      "contracts_per_launch": contracts_per_launch,
                      "measured_stream_gbs": stream_gbs,
                      "frac_of_measured_write": (achieved / stream_gbs["write"]) if "write" in stream_gbs else None},

@@ -539,7 +539,10 @@ __device__ void wgrad_bookkeeping(const MArgs& a, int64_t item, int wave, int la
 }
 
 #ifndef SMC_WGRAD_KS_F32
-#define SMC_WGRAD_KS_F32 32  // f32 batch rows per K stage (the bf16 stage's 36 KiB of LDS)
+// f32 batch rows per K stage: 16 (20 KiB of LDS, 8 workgroups per CU) runs C2/H = 256's 1216 weight-
+// gradient items in one round where 32 (36 KiB, 4 per CU) left a second round of 192 (round-4 A/B:
+// isolated H = 256 network 251-253 -> 243 us, profiles/r04/ab_wgrad_stage.txt)
+#define SMC_WGRAD_KS_F32 16
 #endif
 constexpr int kWgBlock = 64;  // output block edge
 constexpr int kWgStage = 64;  // batch rows per K stage (bf16; 32 for f32: the same 36 KiB of LDS)

@@ -385,7 +385,8 @@ __device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, L
     if constexpr (kPacked) {
       advance_packed(x, z);
     } else if constexpr (kY64) {
-      math::mul_exp2s_f64_x4(x, z);
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) x[j] = math::mul_exp2s_f64(x[j], z[j]);
     } else {
 #pragma unroll
       for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], z[j]);

@@ -279,87 +279,5 @@ __device__ __forceinline__ double mul_exp2s_f64(double x, double ys) {
   return __builtin_amdgcn_ldexp(fma(xt, e.em1, xt), e.m);
 }
 
-// The same on 4 independent arguments, written in stages so that the 4 table reads of a stage are in
-// flight together (the scheduler otherwise finishes one argument's dependency chain -- a table read
-// and its wait, then the next -- before starting the next; round-4 PMC: the f64 path kernel waited on
-// instruction dependencies ~60 % of its wave cycles).  Bit-identical to 4 calls of the scalar forms.
-__device__ __forceinline__ void m2log_u32_x4(const uint32_t (&a)[4], double (&X)[4]) {
-  double f[4], k[4], t0[4], t1[4], t2[4];
-  uint32_t idx[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const double m = static_cast<double>(a[j]) + 0.5;
-    const uint64_t bits = __double_as_longlong(m);
-    const uint32_t hw = static_cast<uint32_t>(bits >> 32);
-    const uint32_t mh = hw & 0xFFFFFu;
-    idx[j] = (mh + 0x200u) >> 10;
-    f[j] = __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(mh | 0x3FF00000u) << 32) |
-                                                       (bits & 0xFFFFFFFFull)));
-    k[j] = static_cast<double>(static_cast<int>(hw >> 20) - 1055);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const double* t = f64_lds().log[idx[j]];
-    t0[j] = t[0];
-    t1[j] = t[1];
-    t2[j] = t[2];
-  }
-  __builtin_amdgcn_sched_barrier(0);  // keep the 4 reads issued before their first use
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const double r = fma(f[j], t0[j], 2.0);
-    double q = 0.0125;
-    q = fma(q, r, 0.03125);
-    q = fma(q, r, 0.08333333333333333);
-    q = fma(q, r, 0.25);
-    const double p = fma(q, r * r, r);
-    X[j] = fma(k[j], kF64M2Ln2Hi, t1[j]) + (fma(k[j], kF64M2Ln2Lo, t2[j]) + p);
-  }
-}
-
-__device__ __forceinline__ void sincos2pi_u32_x4(const uint32_t (&b)[4], double (&s_out)[4], double (&c_out)[4]) {
-  double x[4];
-  double2 sc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t jj = ((b[j] + (1u << 21)) >> 22) & 1023u;
-    x[j] = static_cast<double>(static_cast<int32_t>(b[j] - (jj << 22))) * 1.4629180792671596e-09;
-    sc[j] = f64_lds().sc[jj];
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const double u = x[j] * x[j];
-    const double sp = fma(u, 0.008333333333333333, -0.16666666666666666);
-    const double sx = fma(sp * u, x[j], x[j]);
-    const double cp = fma(u, 0.041666666666666664, -0.5);
-    const double cx = fma(cp, u, 1.0);
-    s_out[j] = fma(sc[j].x, cx, sc[j].y * sx);
-    c_out[j] = fma(sc[j].y, cx, -(sc[j].x * sx));
-  }
-}
-
-__device__ __forceinline__ void mul_exp2s_f64_x4(double (&x)[4], const double (&ys)[4]) {
-  double rr[4], T[4];
-  int ni[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const double t = ys[j] + 6755399441055744.0;
-    ni[j] = static_cast<int>(static_cast<uint32_t>(__double_as_longlong(t)));
-    rr[j] = ys[j] - (t - 6755399441055744.0);
-    T[j] = f64_lds().ex[ni[j] & 255];
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    double q = kF64ExpE4;
-    q = fma(q, rr[j], kF64ExpE3);
-    q = fma(q, rr[j], kF64ExpE2);
-    q = fma(q, rr[j], kF64ExpE1);
-    const double xt = x[j] * T[j];
-    x[j] = __builtin_amdgcn_ldexp(fma(xt, q * rr[j], xt), ni[j] >> 8);
-  }
-}
-
 }  // namespace math
 }  // namespace smc

@@ -188,20 +188,14 @@ struct PathStream {
   // normal_pair<HW>(double&, double&) with b folded into the Box-Muller radius (one multiply per pair
   // instead of two)
   __device__ __forceinline__ void f64_log_increments4(double b, double a, double (&ylo)[4], double (&yhi)[4]) {
-    uint32_t ua[4], ub[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      ua[j] = next();
-      ub[j] = next();
-    }
-    double X[4], s[4], c[4];
-    math::m2log_u32_x4(ua, X);  // the 4 pairs' table reads in flight together
-    math::sincos2pi_u32_x4(ub, s, c);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const double br = math::sqrt_radius(X[j]) * b;
-      ylo[j] = fma(br, c[j], a);
-      yhi[j] = fma(br, s[j], a);
+      const uint32_t ua = next(), ub = next();
+      const double br = math::sqrt_radius(math::m2log_u32(ua)) * b;
+      double s, c;
+      math::sincos2pi_u32(ub, s, c);
+      ylo[j] = fma(br, c, a);
+      yhi[j] = fma(br, s, a);
     }
   }
 
