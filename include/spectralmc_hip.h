@@ -202,7 +202,8 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
  * stride becomes an odd multiple of 4 KiB (power-of-two strides alias in HBM). */
 int64_t smc_path_pitch(int64_t n_paths, int32_t dtype);
 /* The [rows][cols] N(0,1) matrix of contract ordinal m (the values smc_gbm_simulate
- * draws for path p, step t, laid out [t][p]). */
+ * draws for path p, step t, laid out [t][p]; rows = the contract's T: at T <= 2 one
+ * Philox-seeded stream serves 4 consecutive 4-path groups, the stream span of smc_rng.h). */
 int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t cols,
                     int32_t dtype, void* out_dev, void* stream);
 
