@@ -538,6 +538,9 @@ __device__ void wgrad_bookkeeping(const MArgs& a, int64_t item, int wave, int la
   }
 }
 
+#ifndef SMC_WGRAD_ROWMAJOR
+#define SMC_WGRAD_ROWMAJOR 1  // layered plans: wgrad reads Z_l / dU_l row-major, lgemm writes no ^T copies
+#endif
 #ifndef SMC_WGRAD_KS_F32
 // f32 batch rows per K stage: 16 (20 KiB of LDS, 8 workgroups per CU) runs C2/H = 256's 1216 weight-
 // gradient items in one round where 32 (36 KiB, 4 per CU) left a second round of 192 (round-4 A/B:
@@ -546,6 +549,39 @@ __device__ void wgrad_bookkeeping(const MArgs& a, int64_t item, int wave, int la
 #endif
 constexpr int kWgBlock = 64;  // output block edge
 constexpr int kWgStage = 64;  // batch rows per K stage (bf16; 32 for f32: the same 36 KiB of LDS)
+
+// the weight-gradient block's partials (dA, dB, biases) of segment s from the accumulators
+__device__ __forceinline__ void wgrad_store(const MArgs& a, const MLayer& ly, int s, int64_t stride, int f_base,
+                                            int k_base, int wm, int wn, int g, int c, const f32x4 (&acc)[2][2]) {
+  float* part = a.partials + s * stride;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int fbase = f_base + wm * 32 + i * 16 + 4 * g;
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      float y[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(acc[i][jt][r], 1, 64);
+      const int k = k_base + wn * 32 + jt * 16 + c;
+      if ((c & 1) == 0 && k < ly.kx) {
+        const int kk = k >> 1;
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const int j = (fbase + r) >> 1;
+          if (j >= ly.no) continue;
+          if (kk < ly.ni) {
+            const int64_t w = static_cast<int64_t>(j) * ly.ni + kk;
+            part[ly.w_re + w] = acc[i][jt][r] + y[r + 1];
+            part[ly.w_im + w] = acc[i][jt][r + 1] - y[r];
+          } else if (kk == ly.ni) {  // the ones column: bias gradients
+            if (ly.b_re >= 0) part[ly.b_re + j] = acc[i][jt][r];
+            if (ly.b_im >= 0) part[ly.b_im + j] = acc[i][jt][r + 1];
+          }
+        }
+      }
+    }
+  }
+}
 
 template <class Op>
 __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
@@ -628,34 +664,95 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
     if (st + 1 < nst) put(buf ^ 1);
     __syncthreads();
   }
-  float* part = a.partials + s * stride;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int fbase = f_base + wm * 32 + i * 16 + 4 * g;
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      float y[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(acc[i][jt][r], 1, 64);
-      const int k = k_base + wn * 32 + jt * 16 + c;
-      if ((c & 1) == 0 && k < ly.kx) {
-        const int kk = k >> 1;
-#pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          const int j = (fbase + r) >> 1;
-          if (j >= ly.no) continue;
-          if (kk < ly.ni) {
-            const int64_t w = static_cast<int64_t>(j) * ly.ni + kk;
-            part[ly.w_re + w] = acc[i][jt][r] + y[r + 1];
-            part[ly.w_im + w] = acc[i][jt][r + 1] - y[r];
-          } else if (kk == ly.ni) {  // the ones column: bias gradients
-            if (ly.b_re >= 0) part[ly.b_re + j] = acc[i][jt][r];
-            if (ly.b_im >= 0) part[ly.b_im + j] = acc[i][jt][r + 1];
-          }
-        }
-      }
-    }
+  wgrad_store(a, ly, s, stride, f_base, k_base, wm, wn, g, c, acc);
+}
+
+// wgrad for layered plans (round 4): the operands straight from the row-major Z_l [bp][kx] and
+// dU_l [bp][wout] the layered GEMMs write anyway, so their epilogues store no ^T copies.  Each K stage
+// stages KS batch rows x 64 features of both operands (16-B loads along the features, the row stride
+// 68 floats: lanes c and the 4 row groups g hit distinct banks); a lane's MFMA operand k-values are the
+// 4 batch rows 4 g .. 4 g + 3 of the block -- the same (row, MFMA) assignment as wgrad_kernel's
+// transposed fragments, so the partials are bit-identical to it.
+template <int KS>
+__global__ __launch_bounds__(kThreads) void wgrad_rm_kernel(MArgs a) {
+  constexpr int LD = kWgBlock + 4;  // 4 LD = 16 (mod 64): the 4 row groups g read distinct banks
+  constexpr int NV = KS * kWgBlock / 4 / kThreads;  // 16-B loads per operand per thread and stage
+  static_assert(NV >= 1 && KS % 16 == 0, "whole 16-row MFMA blocks per stage");
+  __shared__ __attribute__((aligned(16))) float stage[2][2][KS * LD];  // [buffer][A = dU, B = Z]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, c = lane & 15;
+  const float* ws = static_cast<const float*>(a.opws);
+  const int64_t stride = a.n_params + 1;
+  const int64_t seg_rows = a.bp / a.segs;
+  int64_t item = blockIdx.x;
+  int l = 0;
+  while (l < a.n_layers && item >= a.layer[l].items) item -= a.layer[l].items, ++l;
+  if (l == a.n_layers) {
+    wgrad_bookkeeping(a, item, wave, lane);
+    return;
   }
+  const MLayer& ly = a.layer[l];
+  const int nkb = (ly.kx + kWgBlock - 1) / kWgBlock;
+  const int s = static_cast<int>(item % a.segs);
+  const int64_t rest = item / a.segs;
+  const int kblk = static_cast<int>(rest % nkb);
+  const int fblk = static_cast<int>(rest / nkb);
+  const int f_base = fblk * kWgBlock, k_base = kblk * kWgBlock;
+  const int64_t b0 = s * seg_rows;
+  const float* G = ws + ly.dr;  // [bp][wout]
+  const float* Z = ws + ly.zr;  // [bp][kx]
+  f32x4 ra[NV], rb[NV];
+  auto fetch = [&](int64_t kb) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = v * kThreads + tid, r = i / (kWgBlock / 4), q = 4 * (i % (kWgBlock / 4));
+      const int64_t row = b0 + kb + r;
+      const bool oa = f_base + q < ly.wout, ob = k_base + q < ly.kx;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(G + (oa ? row * ly.wout + f_base + q : 0));
+      const f32x4 y = *reinterpret_cast<const f32x4*>(Z + (ob ? row * ly.kx + k_base + q : 0));
+      ra[v] = oa ? x : f32x4{0.f, 0.f, 0.f, 0.f};
+      rb[v] = ob ? y : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int i = v * kThreads + tid, r = i / (kWgBlock / 4), q = 4 * (i % (kWgBlock / 4));
+      *reinterpret_cast<f32x4*>(&stage[buf][0][r * LD + q]) = ra[v];
+      *reinterpret_cast<f32x4*>(&stage[buf][1][r * LD + q]) = rb[v];
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nst = static_cast<int>(seg_rows / KS);
+  fetch(0);
+  put(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) fetch(static_cast<int64_t>(st + 1) * KS);
+#pragma unroll
+    for (int kb = 0; kb < KS; kb += 16) {
+      f32x4 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          af[i][r] = stage[buf][0][(kb + 4 * g + r) * LD + wm * 32 + i * 16 + c];
+          bf[i][r] = stage[buf][1][(kb + 4 * g + r) * LD + wn * 32 + i * 16 + c];
+        }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = OpF32::mmav(acc[i][j], af[i], bf[j]);
+    }
+    if (st + 1 < nst) put(buf ^ 1);
+    __syncthreads();
+  }
+  wgrad_store(a, ly, s, stride, f_base, k_base, wm, wn, g, c, acc);
 }
 
 // ---- layered step for wide layers (round 3) ----------------------------------------------------
@@ -936,7 +1033,8 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
       }
     }
     if (f0 < nvalid) *reinterpret_cast<f32x4*>(ws + rm_off + b * rm_ld + f0) = f32x4{o[0], o[1], o[2], o[3]};
-    *reinterpret_cast<f32x4*>(&tile[rr * TLD + 4 * q]) = f32x4{o[0], o[1], o[2], o[3]};  // the ^T copy's values
+    if constexpr (!SMC_WGRAD_ROWMAJOR)
+      *reinterpret_cast<f32x4*>(&tile[rr * TLD + 4 * q]) = f32x4{o[0], o[1], o[2], o[3]};  // the ^T copy's values
   }
   if constexpr (MODE != kLFwd) {
     // modReLU bias share of the block's kLN rows: each thread's rows in order, then the kLN / 8 row
@@ -966,8 +1064,8 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   } else {
     __syncthreads();
   }
-  // phase C: the ^T copy, whole 64-row lines of each feature
-  for (int e = tid; e < kLM * (kLN / 4); e += kLThreads) {
+  // phase C: the ^T copy, whole 64-row lines of each feature (only for the transposed wgrad_kernel)
+  for (int e = tid; e < (SMC_WGRAD_ROWMAJOR ? 0 : kLM * (kLN / 4)); e += kLThreads) {
     const int fr = e / (kLN / 4), q4 = e % (kLN / 4);
     if (m0 + fr < nvalid)
       *reinterpret_cast<f32x4*>(ws + tr_off + static_cast<int64_t>(m0 + fr) * bp + n0 + 4 * q4) =
@@ -982,7 +1080,7 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
         const int64_t b = n0 + e % kLN;
         const float v = k == 2 * ly.no ? 1.0f : 0.0f;
         ws[nx.zr + b * nx.kx + k] = v;
-        ws[nx.zt + static_cast<int64_t>(k) * bp + b] = v;
+        if constexpr (!SMC_WGRAD_ROWMAJOR) ws[nx.zt + static_cast<int64_t>(k) * bp + b] = v;
       }
     }
   }
@@ -1154,7 +1252,8 @@ int32_t launch_fb(const Plan& p, hipStream_t s) {
 
 int32_t launch_layered(const Plan& p, hipStream_t s) {
   const MArgs& a = p.a;
-  hipLaunchKernelGGL(lpack_kernel, dim3(256, 2 * a.n_layers + 2), dim3(kThreads), 0, s, a);
+  // (row-major wgrad: no Z_0^T region)
+  hipLaunchKernelGGL(lpack_kernel, dim3(256, 2 * a.n_layers + (SMC_WGRAD_ROWMAJOR ? 1 : 2)), dim3(kThreads), 0, s, a);
   if (int32_t rc = check_launch("cvnn lpack_kernel")) return rc;
   const unsigned by = static_cast<unsigned>(a.bp / kLN);
   const int L = a.n_layers;
@@ -1173,9 +1272,13 @@ int32_t launch_layered(const Plan& p, hipStream_t s) {
     hipLaunchKernelGGL(lgemm_kernel<kLBwd>, grid, dim3(kLThreads), 0, s, g, l);
     if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
   }
-  // weight gradients from the ^T copies, as after fb_kernel (its 64 x 64 blocks measured faster here
-  // than this file's GEMM tile over batch segments: 70 vs 74-81 us at C2/H=256)
-  hipLaunchKernelGGL(wgrad_kernel<OpF32>, dim3(p.wgrad_grid), dim3(kThreads), 0, s, a);
+  // weight gradients in wgrad_kernel's 64 x 64 blocks over batch segments (they measured faster here than
+  // this file's GEMM tile: 70 vs 74-81 us at C2/H=256), from the row-major Z_l / dU_l (wgrad_rm_kernel,
+  // round 4) or, without SMC_WGRAD_ROWMAJOR, from ^T copies as after fb_kernel
+  if (SMC_WGRAD_ROWMAJOR)
+    hipLaunchKernelGGL(wgrad_rm_kernel<SMC_WGRAD_KS_F32>, dim3(p.wgrad_grid), dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<OpF32>, dim3(p.wgrad_grid), dim3(kThreads), 0, s, a);
   return check_launch("cvnn wgrad_kernel");
 }
 

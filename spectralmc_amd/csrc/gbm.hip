@@ -37,9 +37,6 @@ namespace {
 
 // rows_kernel occupancy: 8 waves per SIMD (<= 64 VGPRs) = 4 workgroups per CU, so C2's 4096 contracts
 // are exactly 4 rounds of 1024 persistent workgroups (at 69 VGPRs: 3 per CU, 5.33 rounds)
-#ifndef SMC_F64_DENSE
-#define SMC_F64_DENSE 0  // f64 rows_kernel row stores staged through LDS (lane_rows_s dense)
-#endif
 #ifndef SMC_ROWS_WAVES_F64
 #define SMC_ROWS_WAVES_F64 5
 #endif
@@ -344,31 +341,27 @@ __device__ __forceinline__ void lane_paths(const EngineArgs& a, const Stepper<Re
 // lane_rows_s: the same on a stream the caller positioned at the group's first draw (wave_kernel walks
 // a whole stream span, smc_rng.h).
 // stage (LDS, optional): the rows go there instead of to HBM, row r at stage + r * stage_stride + 4 lane_id
-// dense (LDS, f64 only, optional): the wave's 2 KiB row pieces go through it so that each store
-// instruction is 64 lanes x 16 B contiguous instead of every other 16 B of 2 KiB
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                             int64_t chunk, Real* contract_base, int T, int64_t pitch, double& acc,
                                             Real (&x_out)[kPathsPerLane], int lane_id, Real* stage = nullptr,
-                                            int stage_stride = 0, double* dense = nullptr);
+                                            int stage_stride = 0);
 
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __device__ __forceinline__ void lane_rows(const EngineArgs& a, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                           uint64_t ordinal, int64_t chunk, Real* contract_base, int T, int64_t pitch,
-                                          double& acc, Real (&x_out)[kPathsPerLane], int lid = -1,
-                                          double* dense = nullptr) {
+                                          double& acc, Real (&x_out)[kPathsPerLane], int lid = -1) {
   const int lane_id = lid < 0 ? static_cast<int>(threadIdx.x) : lid;  // the lane's 4-path slot in the chunk
   const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(lane_id);
   PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane), T);
-  lane_rows_s<Real, LOG_EULER, HW, STORE_ALL>(s, step, x0, chunk, contract_base, T, pitch, acc, x_out, lane_id,
-                                              nullptr, 0, dense);
+  lane_rows_s<Real, LOG_EULER, HW, STORE_ALL>(s, step, x0, chunk, contract_base, T, pitch, acc, x_out, lane_id);
 }
 
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 __device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, LOG_EULER, HW>& step, Real x0,
                                             int64_t chunk, Real* contract_base, int T, int64_t pitch, double& acc,
                                             Real (&x_out)[kPathsPerLane], int lane_id, Real* stage,
-                                            int stage_stride, double* dense) {
+                                            int stage_stride) {
   using V4 = typename Vec4T<Real>::type;
   constexpr bool kPacked = HW && LOG_EULER && sizeof(Real) == 4;
   constexpr bool kY64 = LOG_EULER && sizeof(Real) == 8;  // exponents drawn directly (lane_paths)
@@ -408,21 +401,6 @@ __device__ __forceinline__ void lane_rows_s(PathStream& s, const Stepper<Real, L
     if (stage) {
       *reinterpret_cast<V4*>(stage + kPathsPerLane * lane_id) = v;
       stage += stage_stride;
-    } else if constexpr (sizeof(Real) == 8) {
-      if (dense) {  // the wave's 256 doubles through LDS (a wave's LDS operations complete in order)
-        typedef double v2d __attribute__((ext_vector_type(2)));
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        const int ln = lane_id & 63;
-        *reinterpret_cast<V4*>(dense + kPathsPerLane * ln) = v;
-        const v2d p0 = *reinterpret_cast<const v2d*>(dense + 2 * ln);
-        const v2d p1 = *reinterpret_cast<const v2d*>(dense + 2 * (64 + ln));
-        const __amdgpu_buffer_rsrc_t r = row_rsrc(row);
-        const uint32_t wbase = 2048u * static_cast<uint32_t>(lane_id >> 6);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, p0), r, wbase + 16u * ln, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4f, p1), r, wbase + 1024u + 16u * ln, 0, 0);
-      } else {
-        store_row(row, lane_off, v);
-      }
     } else {
       store_row(row, lane_off, v);
     }
@@ -875,9 +853,7 @@ void rows_kernel(EngineArgs a) {
     for (int64_t chunk = 0; chunk < a.P; chunk += kChunk) {
       Real xt[kPathsPerLane];
       lane_rows<Real, LOG_EULER, HW, STORE_ALL>(a, step, x0, static_cast<uint64_t>(ord0 + b), chunk, base, T, pitch,
-                                                acc, xt, -1,
-                                                (SMC_F64_DENSE && sizeof(Real) == 8 && STORE_ALL)
-                                                    ? lds + 2 * kWaves + 256 * (threadIdx.x >> 6) : nullptr);
+                                                acc, xt);
     }
     // wave sums in a double-buffered LDS slot: the next contract writes the other slot
     const double w = wave_sum(acc);
@@ -1801,10 +1777,7 @@ int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
 
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
 int32_t launch_rows_k(const EngineArgs& a, hipStream_t stream) {
-  // f64 STORE_ALL with SMC_F64_DENSE: a 2 KiB row-piece stage per wave after the wave sums
-  const size_t lds1 = (2 * kWaves + (SMC_F64_DENSE && sizeof(Real) == 8 && STORE_ALL ? 256 * kWaves : 0)) *
-                      sizeof(double),
-               lds2 = lds_bytes(a.T, a.N, true);
+  const size_t lds1 = 2 * kWaves * sizeof(double), lds2 = lds_bytes(a.T, a.N, true);
   auto k1 = rows_kernel<Real, LOG_EULER, HW, STORE_ALL>;
   auto k2 = cf_kernel<Real>;
   if (lds2 > kMaxLds) return fail(SMC_ERR_INVALID_SHAPE, "engine: network_size exceeds the LDS budget");
