@@ -773,9 +773,6 @@ __global__ __launch_bounds__(kThreads) void wgrad_rm_kernel(MArgs a) {
 #ifndef SMC_LGEMM_M
 #define SMC_LGEMM_M 64
 #endif
-#ifndef SMC_LGEMM_XCD
-#define SMC_LGEMM_XCD 1
-#endif
 #ifndef SMC_LGEMM_N
 #define SMC_LGEMM_N 64
 #endif
@@ -848,15 +845,12 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   const int MB = static_cast<int>(a.lgemm_mb);
   const int NB = static_cast<int>(a.bp / kLN);
   int mb, nb;
-  if (SMC_LGEMM_XCD) {
+  {
     const int per = (NB + 7) >> 3;
     const int xcd = static_cast<int>(blockIdx.x) & 7, local = static_cast<int>(blockIdx.x) >> 3;
     nb = xcd * per + local / MB;
     mb = local % MB;
     if (nb >= NB) return;  // uniform, before any barrier
-  } else {
-    mb = static_cast<int>(blockIdx.x) % MB;
-    nb = static_cast<int>(blockIdx.x) / MB;
   }
   const int64_t kbeg = 0;
   const MLayer& ly = a.layer[l];
@@ -1258,7 +1252,7 @@ int32_t launch_layered(const Plan& p, hipStream_t s) {
   const unsigned by = static_cast<unsigned>(a.bp / kLN);
   const int L = a.n_layers;
   MArgs g = a;  // lgemm_mb: the launch's feature blocks (1-D grid of lgemm_mb x (by rounded to 8) workgroups)
-  const unsigned byx = SMC_LGEMM_XCD ? (by + 7) / 8 * 8 : by;
+  const unsigned byx = (by + 7) / 8 * 8;
   for (int l = 0; l < L; ++l) {
     g.lgemm_mb = (a.layer[l].wout + kLM - 1) / kLM;
     const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * byx);

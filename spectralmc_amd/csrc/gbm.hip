@@ -1360,9 +1360,6 @@ constexpr int kWaveThreads = 256;
 constexpr int kWaveLanePaths = PathStream::kSpanGroups * kPathsPerLane;  // 16 paths per lane and chunk
 constexpr int kWaveChunk = 64 * kWaveLanePaths;                           // 1024 paths per chunk
 constexpr int kWaveMaxT = 2;
-#ifndef SMC_WAVE_DENSE
-#define SMC_WAVE_DENSE 1
-#endif
 
 size_t wave_lds_bytes(int N) {
   const size_t per_wave = kWaveChunk + 3 * static_cast<size_t>(N) + 8;  // part [G][N], avg, re, im, row
@@ -1427,11 +1424,11 @@ __global__ __launch_bounds__(kWaveThreads) __attribute__((amdgpu_waves_per_eu(4)
         float xt[kPathsPerLane];
         lane_rows_s<float, LOG_EULER, HW, STORE_ALL>(s, step, x0, chunk, base, T, pitch, acc, xt,
                                                      PathStream::kSpanGroups * lane + j,
-                                                     SMC_WAVE_DENSE ? stage : nullptr, kWaveChunk);
+                                                     stage, kWaveChunk);
 #pragma unroll
         for (int i = 0; i < kPathsPerLane; ++i) colsum[kPathsPerLane * j + i] += static_cast<double>(pay(xt[i]));
       }
-      if constexpr (SMC_WAVE_DENSE) {
+      {
         // the chunk's rows from LDS: each store instruction 64 lanes x 16 B contiguous (a lane's own 64 B
         // would make every instruction a quarter-dense 4 KiB stripe)
         wave_lds_sync();
