@@ -100,6 +100,9 @@ for step in "$@"; do
     profnet:*)  # profnet:<arch>[:compute] -> rocprofv3 kernel stats of the isolated network step
       IFS=: read -r _ arch comp <<< "$step"
       cd /tmp && run "profnet_${arch}" 300 rocprofv3 --kernel-trace --stats -d "$OUT/profnet_${arch}" -o run --output-format csv -- python "$ROOT/tools/kprof_net.py" --arch "$arch" --compute "${comp:-mfma}"; cd "$ROOT" ;;
+    pmcnet:*)  # pmcnet:<arch>:<counters with ,> -> one PMC pass over the isolated network step
+      IFS=: read -r _ arch ctrs <<< "$step"; tag="${arch}_$(echo "$ctrs" | tr ',' '_' | cut -c1-40)"
+      cd /tmp && run "pmcnet_$tag" 180 rocprofv3 --kernel-trace --pmc ${ctrs//,/ } -d "$OUT/pmcnet_$tag" -o run --output-format csv -- python "$ROOT/tools/kprof_net.py" --arch "$arch" --compute mfma --iters 5; cd "$ROOT" ;;
     abnet:*)  # abnet:<tag>:<kprof_net args with , for spaces>:<variant names with ,> (isolated network step)
       IFS=: read -r _ tag args names <<< "$step"
       AB_SCRIPT=tools/kprof_net.py run "abnet_$tag" 900 bash tools/micro/ab.sh "$OUT/abnet_$tag.txt" "${args//,/ }" ${names//,/ } ;;
