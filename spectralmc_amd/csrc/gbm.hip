@@ -823,10 +823,10 @@ __global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
 // of each 2048-path chunk through all T rows in registers (lane_rows: no replay, one rolled loop), the
 // f64 terminal-row sum into the row padding for cf_kernel.  Terminal-sum order: lane over its chunks,
 // wave butterfly, waves 0..7 (oracle kernel mode, wg = 512; paths_kernel's order).
-// With a contract queue (a.res_queue, smc_train_step's sync area) each workgroup takes its first
-// contract by blockIdx.x and every later one from the counter, so a workgroup that starts late (a
-// concurrent network kernel held its slot) takes fewer contracts instead of finishing last; the
-// last workgroup out resets the counters.  Which workgroup runs a contract changes no result.
+// Contracts are assigned statically: the round-3 contract queue (every contract after the first from a
+// counter, for workgroups that start late beside a network kernel) cost a store drain per contract at
+// its queue barrier, and rows shapes run the step on one stream anyway (round 4, C2-f64: rows_kernel
+// 7.64 ms with the queue against ~6.9 without).
 // f64 rows run at 5 waves per SIMD (SMC_ROWS_WAVES_F64; round 4 A/Bs on MI355X, C2-f64: v2 math 9.01 ms
 // at 6 vs 9.20-9.28 ms at 8 waves, and 9.49-9.53 ms with the CF phase fused into this kernel, which then
 // re-read the terminal row while its own path math waited; v3 math 8.47-8.50 ms at 5 vs 8.65-8.67 ms at
@@ -841,10 +841,8 @@ void rows_kernel(EngineArgs a) {
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
   const int64_t pitch = a.pitch ? a.pitch : a.P;
   const int T = a.T;
-  __shared__ int64_t next_b;
-  const bool dyn = a.res_queue != nullptr;
   int parity = 0;
-  for (int64_t b = blockIdx.x; b < a.B; parity ^= 1) {
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x, parity ^= 1) {
     const Contract c = load_contract(a.contracts + b * 6);
     const Stepper<Real, LOG_EULER, HW> step(c, T);
     const Real x0 = static_cast<Real>(c.X0);
@@ -864,23 +862,6 @@ void rows_kernel(EngineArgs a) {
       double tot = 0.0;
       for (int k = 0; k < kWaves; ++k) tot += ws[k];
       *pad_sum<Real>(a, b) = tot;
-    }
-    if (dyn) {
-      // next_b is rewritten only after the next contract's lds_barrier: every thread has read it
-      if (threadIdx.x == 0)
-        next_b = static_cast<int64_t>(gridDim.x) +
-                 __hip_atomic_fetch_add(a.res_queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      b = next_b;
-    } else {
-      b += gridDim.x;
-    }
-  }
-  if (dyn && threadIdx.x == 0) {
-    // every workgroup made its last queue fetch before it arrives here
-    if (__hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-      __hip_atomic_store(a.res_queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -2069,14 +2050,12 @@ int32_t smc_cf_targets(const double* contracts_dev, int64_t n_contracts, int32_t
   return dispatch_engine(a, dtype, as_stream(stream));
 }
 
-// smc_train_targets; step_sync (smc_train_step's sync area, or NULL): its done counter and contract
-// queue for rows_kernel's dynamic contracts
+// smc_train_targets (and smc_train_step's fallback for the shapes its fused launch does not take)
 static int32_t train_targets(const double* contracts_dev, int64_t n_contracts, int32_t timesteps, int32_t network_size,
                              int32_t batches_per_mc_run, uint64_t mc_seed, const int64_t* ordinal_dev,
                              int64_t ordinal0, int32_t scheme, int32_t normalization, int32_t dtype, int32_t store_mode,
                              void* paths_dev, int64_t path_pitch, int64_t chunk_contracts, double* rowsum_dev,
-                             void* targets_dev, void* workspace_dev, int64_t workspace_size, void* stream,
-                             char* step_sync) {
+                             void* targets_dev, void* workspace_dev, int64_t workspace_size, void* stream) {
   const int64_t P = static_cast<int64_t>(network_size) * batches_per_mc_run;
   if (network_size <= 0 || batches_per_mc_run <= 0)
     return fail(SMC_ERR_INVALID_SHAPE, "smc_train_targets: network_size and batches_per_mc_run must be > 0");
@@ -2110,10 +2089,6 @@ static int32_t train_targets(const double* contracts_dev, int64_t n_contracts, i
                  rowsum_dev ? rowsum_dev + off * timesteps : nullptr,
                  static_cast<char*>(targets_dev) + static_cast<size_t>(off) * network_size * csz, path_pitch,
                  W, partials, arrivals, queues};
-    if (step_sync && W <= 1) {
-      a.done = reinterpret_cast<uint32_t*>(step_sync);
-      a.res_queue = reinterpret_cast<uint32_t*>(step_sync + 64);
-    }
     if (int32_t st = dispatch_engine(a, dtype, as_stream(stream))) return st;
   }
   return SMC_OK;
@@ -2126,7 +2101,7 @@ int32_t smc_train_targets(const double* contracts_dev, int64_t n_contracts, int3
                           void* workspace_dev, int64_t workspace_size, void* stream) {
   return train_targets(contracts_dev, n_contracts, timesteps, network_size, batches_per_mc_run, mc_seed, ordinal_dev,
                        ordinal0, scheme, normalization, dtype, store_mode, paths_dev, path_pitch, chunk_contracts,
-                       rowsum_dev, targets_dev, workspace_dev, workspace_size, stream, nullptr);
+                       rowsum_dev, targets_dev, workspace_dev, workspace_size, stream);
 }
 
 int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const double* lower_dev, const double* upper_dev,
@@ -2219,7 +2194,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
     return st;
   if (int32_t st = train_targets(contracts_dev, n_contracts, timesteps, network_size, batches_per_mc_run, mc_seed,
                                  cursor_dev + 1, index_offset, scheme, normalization, dtype, store_mode, paths_dev,
-                                 path_pitch, chunk_contracts, nullptr, targets_dev, nullptr, 0, stream, sync))
+                                 path_pitch, chunk_contracts, nullptr, targets_dev, nullptr, 0, stream))
     return st;
   hipLaunchKernelGGL(advance_cursor_kernel, dim3(1), dim3(64), 0, s, cursor_dev, advance);
   return check_launch("advance_cursor_kernel");

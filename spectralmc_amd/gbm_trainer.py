@@ -804,9 +804,9 @@ class TrainingSession:
         cur = torch.cuda.current_stream(dev)
         self._hip_streams: list[int] = []  # CU-masked streams this session created (destroyed at close)
         # rows_kernel (f64, the f32 shapes no resident launch takes) keeps every CU slot for its whole
-        # duration (persistent, 8 waves per SIMD, contracts from a queue): a concurrent network part
-        # gets no tail to run in and only stretches it (C2 in f64: 10.55 ms/step overlapped, 10.35
-        # sequential), so those shapes run the step on one stream
+        # duration (persistent, contracts from a queue): a concurrent network part gets no tail to run
+        # in and only stretches it (C2 in f64, round 3: 10.55 ms/step overlapped, 10.35 sequential), so
+        # those shapes run the step on one stream
         overlap = pricer.overlap_mc and not getattr(self.engine, "kernel_name", "").startswith("rows_")
         if overlap:
             # the network part is a few short launches: a high-priority queue lets its workgroups

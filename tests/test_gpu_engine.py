@@ -480,10 +480,11 @@ ROWS_STEP_CASES = [  # (B, T, N, M, dtype, store, chunk): smc_train_step shapes 
 
 
 @pytest.mark.parametrize("B,T,N,M,dtype,store,chunk", ROWS_STEP_CASES)
-def test_rows_train_step_dynamic_queue_equals_targets(golden, B, T, N, M, dtype, store, chunk) -> None:
-    """smc_train_step on the rows_kernel shapes hands contracts out from the sync area's queue (first
-    contract by workgroup index, the rest from the counter); bit-identical to smc_train_targets'
-    static striding (the oracle-checked path), over three steps; the queue is reset (sync zeroed)."""
+def test_rows_train_step_equals_targets(golden, B, T, N, M, dtype, store, chunk) -> None:
+    """smc_train_step on the rows_kernel shapes (Sobol draw, rows_kernel + cf_kernel, cursor update;
+    contracts striped statically over the persistent workgroups since round 4) is bit-identical to the
+    separate draw + smc_train_targets (the oracle-checked path) over three steps, and leaves the sync
+    area zeroed."""
     L = _L()
     if B is None:
         B = 4 * 4 * torch.cuda.get_device_properties(0).multi_processor_count + 5
