@@ -525,8 +525,8 @@ def test_rows_train_step_equals_targets(golden, B, T, N, M, dtype, store, chunk)
 
 def test_c2_f64_timed_call_matches_oracle(oracle, golden) -> None:
     """The f64 C2 MC part exactly as the bench times it: smc_train_step at T = 16, N = M = 256
-    (P = 65,536: rows_kernel + the contract queue + cf_kernel), B = 2500 contracts (more than two rounds
-    of the persistent grid), two steps; every 80th contract against the oracle's reference-mode f64
+    (P = 65,536: rows_kernel with contracts striped over the persistent grid + cf_kernel), B = 2500
+    contracts (more than two rounds of the persistent grid), two steps; every 80th contract against the oracle's reference-mode f64
     targets (the reference's f64 recursion with libm exp on this build's f64 normals, numpy-order FFT)
     at 1e-10 norm-relative (reference gbm.py:241-250 computes the recursion in f64)."""
     L = _L()
