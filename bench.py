@@ -332,7 +332,7 @@ def main() -> None:
     # (P values per asset) that the kernels keeping the terminal row on chip never make; for those the
     # figure with it would credit bytes nobody moves (at the lock-step shape it is twice the real
     # traffic and implies more than the HBM peak)
-    on_chip = eng.kernel_name in ON_CHIP_KERNELS
+    on_chip = eng.kernel_name.split("(")[0] in ON_CHIP_KERNELS  # "resident_kernel(sliced)": C3
     reread = ((n_assets or 1) * P * (4 if n_assets else esz) * contracts_per_launch) if on_chip else 0
     bytes_launch = bytes_survey - reread
     # live: HIP events on the MC stream around each MC-part launch inside the timed region

@@ -431,6 +431,11 @@ class GbmCVNNPricer:
     #: C2/H=256 ~0.26 ms of whole-chip work): more CUs, so the network still hides under the path kernel
     network_cus_wide: int = 64
     network_cu_pattern: str = "low"
+    #: ... only when one path launch does at least this many path-steps (contracts x paths x T): beside a
+    #: short launch the masked network outlasts it (the reference's e2e shape, 3.4e7 path-steps: 0.114
+    #: ms/step unmasked against 0.222 masked; the lock-step shape, 2.7e8: 0.308 masked against 0.329;
+    #: profiles/r04/netcus_small_shapes.jsonl)
+    network_cu_min_path_steps: int = 1 << 27
     #: launches whose workgroups wait for each other (the sliced resident kernel, C3; the resident
     #: basket kernel, C5) need every workgroup of a group co-resident.  A collective that spins on a
     #: few CUs while it waits for a slow peer (RCCL in data-parallel runs) can hold those CUs past the
@@ -817,8 +822,11 @@ class TrainingSession:
             narrow = fused is not None and max(t.in_features for t in fused.table) < 128
             cus = torch.cuda.get_device_properties(dev).multi_processor_count
             net_cus = pricer.network_cus if narrow else (pricer.network_cus_wide if fused is not None else 0)
-            if (net_cus > 0 and getattr(self.engine, "kernel_name", "") in WHOLE_CONTRACT_KERNELS
-                    and cus >= 2 * net_cus):
+            eng = self.engine
+            path_steps = min(getattr(eng, "chunk", 0), getattr(eng, "B", 0)) * getattr(eng, "P", 0) * \
+                getattr(eng, "T", 0)
+            if (net_cus > 0 and getattr(eng, "kernel_name", "") in WHOLE_CONTRACT_KERNELS
+                    and cus >= 2 * net_cus and path_steps >= pricer.network_cu_min_path_steps):
                 # the network on its own CUs beside the path kernels (CU-masked HIP streams); the path
                 # kernel sizes its persistent grid to its stream's CUs (gbm.hip resident_grid).  Only for
                 # the whole-contract resident launch (C2, the lock-step shape) and a fused network: a
