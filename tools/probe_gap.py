@@ -51,8 +51,15 @@ def main() -> None:
     stream = torch.cuda.Stream(device=dev)
     cycles = int(args.sleep_us * 2.4e3)  # ~2.4 GHz shader clock
 
-    def launch():
-        eng.launch_targets(_lib.stream_handle(stream), None, 0)
+    slot0 = prog.slots[0]
+
+    def launch(mode: str = ""):
+        if mode == "enqueue":  # the MC part exactly as the step enqueues it (draw, targets, cursor)
+            eng.enqueue_step(slot0)
+        elif mode == "slot":  # the targets launch on the last drawn contracts, device ordinal
+            eng.launch_targets(_lib.stream_handle(stream), _lib.ptr(eng.cursor[1:2]), 0, slot0)
+        else:
+            eng.launch_targets(_lib.stream_handle(stream), None, 0)
 
     def net():
         if fused is not None:
@@ -65,7 +72,7 @@ def main() -> None:
         with torch.cuda.stream(stream):
             for e0, e1 in ev:
                 e0.record(stream)
-                launch()
+                launch(mode)
                 e1.record(stream)
                 if mode == "sleep":
                     torch.cuda._sleep(cycles)
@@ -74,7 +81,10 @@ def main() -> None:
         torch.cuda.synchronize()
         return [a.elapsed_time(b) for a, b in ev]
 
-    for mode in ("alone", "sleep", "network", "alone"):
+    c = eng.buffers.contracts
+    print("engine-buffer contracts: min %.4g max %.4g; slot contracts: min %.4g max %.4g" % (
+        float(c.min()), float(c.max()), float(slot0.contracts.min()), float(slot0.contracts.max())), flush=True)
+    for mode in ("alone", "slot", "enqueue", "sleep", "network", "alone"):
         t = run(mode)
         print(f"{mode:8s} " + " ".join(f"{x:.3f}" for x in t) + f"  | last half mean {sum(t[len(t)//2:])/(len(t)-len(t)//2):.3f}",
               flush=True)
