@@ -303,8 +303,12 @@ def main() -> None:
     stream = torch.cuda.Stream(device=dev)
     L = _lib.lib()
     launches_per_call = (eng.B + eng.chunk - 1) // eng.chunk
+    prog = session.program
+    # the contracts of the last timed step: the engine's own buffers are never drawn into when the steps
+    # write their slots directly, and the path kernels run faster on all-zero contracts (C2-f64 rows_kernel
+    # + cf_kernel: 7.43 ms on zeros, 8.04 ms on drawn contracts; profiles/r04/probe_gap_f64.txt)
+    last = prog.slots[(session.steps - 1) % len(prog.slots)] if getattr(prog, "direct", False) else None
     with torch.cuda.stream(stream):
-        b = eng.buffers
 
         def run_kernel() -> None:
             # the launch(es) the training step makes: smc_train_step (Sobol draw, targets and cursor
@@ -312,7 +316,7 @@ def main() -> None:
             if getattr(eng, "_uses_train_step", False):
                 eng.enqueue_step()
             else:
-                eng.launch_targets(_lib.stream_handle(stream), None, 0)
+                eng.launch_targets(_lib.stream_handle(stream), None, 0, last)
 
         run_kernel()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
