@@ -1,0 +1,45 @@
+"""Shader clock and VALU issue rate per dispatch from a rocprofv3 --pmc run that collected GRBM_GUI_ACTIVE
+(GPU-clock cycles the graphics block was busy, one value per XCD) and optionally SQ_INSTS_VALU / SQ_BUSY_CYCLES.
+    clock_MHz  = GRBM_GUI_ACTIVE (mean over XCD instances) / dispatch duration
+    valu_frac  = SQ_INSTS_VALU x 4 cycles / (SIMDs x GRBM cycles): VALU issue slots used at the clock the
+                 kernel actually ran at (each wave64 VALU instruction holds its SIMD 4 cycles; 4 SIMDs per CU)
+Usage: python tools/pmc_clock.py DIR [--kernel SUBSTRING] [--cus 256]"""
+import argparse
+import csv
+import glob
+from collections import defaultdict
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--kernel", default="")
+    ap.add_argument("--cus", type=int, default=256)
+    a = ap.parse_args()
+    per: dict[int, dict] = defaultdict(lambda: {"ctr": defaultdict(float), "inst": defaultdict(int)})
+    for f in glob.glob(f"{a.dir}/**/*counter_collection.csv", recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if a.kernel not in row["Kernel_Name"]:
+                    continue
+                d = per[int(row["Dispatch_Id"])]
+                d["name"] = row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-40:]
+                d["dur"] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9
+                c = row["Counter_Name"]
+                d["ctr"][c] += float(row["Counter_Value"])
+                d["inst"][c] += 1
+    for disp in sorted(per):
+        d = per[disp]
+        g, n = d["ctr"].get("GRBM_GUI_ACTIVE"), d["inst"].get("GRBM_GUI_ACTIVE", 1)
+        line = f"{disp:5d} {d['name']:40s} {d['dur'] * 1e3:8.3f} ms"
+        if g:
+            cyc = g / n
+            line += f"  clock {cyc / d['dur'] / 1e6:6.0f} MHz"
+            v = d["ctr"].get("SQ_INSTS_VALU")
+            if v:
+                line += f"  VALU {v / d['dur'] / 1e9:6.1f} G wave-inst/s, issue frac {v * 4 / (a.cus * 4 * cyc):.2f}"
+        print(line)
+
+
+if __name__ == "__main__":
+    main()
