@@ -1,6 +1,6 @@
 """Per-kernel averages of every counter in rocprofv3 --pmc output directories (counter_collection CSVs),
 summed over the agent's instances (XCDs / SEs), the first dispatch of each kernel skipped when there are
-more.  Usage: python tools/pmc_counters.py DIR [DIR ...] [--kernel SUBSTRING]"""
+more.  Usage: python tools/pmc_counters.py DIR|CSV [DIR|CSV ...] [--kernel SUBSTRING]"""
 import argparse
 import csv
 import glob
@@ -14,7 +14,10 @@ def main() -> None:
     a = ap.parse_args()
     for d in a.dirs:
         vals: dict[tuple[str, str], dict[int, float]] = defaultdict(dict)
-        for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        # a counter_collection CSV, or a directory (every run under it: give one run per directory, as
+        # dispatch ids of different runs collide)
+        files = [d] if d.endswith(".csv") else glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
+        for f in files:
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     if a.kernel not in row["Kernel_Name"]:
