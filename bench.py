@@ -397,7 +397,8 @@ def main() -> None:
                        "CU slot for its whole duration; gbm_trainer.py)"
                        if session.engine.kernel_name.startswith("rows_") or not pricer.overlap_mc else
                        "in the step it is enqueued on its own stream and its workgroups take the CUs the path "
-                       "kernels leave (32 CU-masked CUs at C2; else the tails)")}
+                       "kernels leave" + (f" ({session.network_cus_used} CU-masked CUs)" if session.network_cus_used else
+                                            " (no CU masks: the tails)"))}
 
     # ---- measured HBM ceilings on this device (STREAM-style, 8 GiB buffers) --------------
     stream_gbs = {}
@@ -474,8 +475,8 @@ def main() -> None:
                      # time per launch and the fraction of peak it corresponds to
                      "kernel_ms_steady": steady_ms,
                      "frac_steady": (bytes_launch / (steady_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if steady_ms else None,
-                     "mc_note": ("consecutive path launches overlap (2 MC lanes on the CUs the network's 32 "
-                                 "masked CUs leave); kernel_ms = the launch alone on the whole chip, "
+                     "mc_note": (f"consecutive path launches overlap ({lanes} MC lanes on the CUs the network's "
+                                 f"{session.network_cus_used} masked CUs leave); kernel_ms = the launch alone on the whole chip, "
                                  "kernel_ms_steady = launch spacing in the timed region; a rocprofv3 trace "
                                  "of this run records each overlapped launch from its dispatch to its end"
                                  if lanes > 1 else None),

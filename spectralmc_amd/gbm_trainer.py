@@ -808,6 +808,7 @@ class TrainingSession:
         self.engine.set_position(self.sobol_skip, pricer._mc_engine.ordinal)
         cur = torch.cuda.current_stream(dev)
         self._hip_streams: list[int] = []  # CU-masked streams this session created (destroyed at close)
+        self.network_cus_used = 0  # CUs of the network's CU-masked stream (0: no masks)
         # rows_kernel (f64, the f32 shapes no resident launch takes) keeps every CU slot for its whole
         # duration (persistent, contracts from a queue): a concurrent network part gets no tail to run
         # in and only stretches it (C2 in f64, round 3: 10.55 ms/step overlapped, 10.35 sequential), so
@@ -833,6 +834,7 @@ class TrainingSession:
                 # narrow one (fb_kernel path, ~70 us of whole-chip work at C2) on network_cus, a wide one
                 # (C2/H=256: 0.26 ms) on network_cus_wide (on 32 CUs it outlasted the path kernel: 3.39
                 # vs 3.30 ms/step)
+                self.network_cus_used = net_cus
                 net_mask, mc_mask = _cu_masks(dev, net_cus, pricer.network_cu_pattern)
                 self.stream = _masked_stream(dev, net_mask, self._hip_streams)
                 self.mc_streams = [_masked_stream(dev, mc_mask, self._hip_streams) for _ in range(lanes)]
