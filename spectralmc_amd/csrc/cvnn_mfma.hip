@@ -826,40 +826,192 @@ __global__ __launch_bounds__(kThreads) void lpack_kernel(MArgs a) {
   }
 }
 
+// XCD-aware tile order: the 1-D grid's consecutive workgroups go round-robin to the 8 XCDs, so
+// workgroup w runs on XCD w % 8; each XCD takes a contiguous eighth of the batch blocks with every
+// feature block, and reads only its eighth of the row operand (B) and the whole weight matrix (A)
+// into its own L2, instead of every XCD streaming all of B past one feature block
+// (NB not a multiple of 8: the grid is rounded up to 8 equal XCD ranges and the workgroups past the
+// last batch block return at once).  False: this workgroup has no tile.
+__device__ __forceinline__ bool lgemm_tile(const MArgs& a, int& mb, int& nb) {
+  const int MB = static_cast<int>(a.lgemm_mb);
+  const int NB = static_cast<int>(a.bp / kLN);
+  const int per = (NB + 7) >> 3;
+  const int xcd = static_cast<int>(blockIdx.x) & 7, local = static_cast<int>(blockIdx.x) >> 3;
+  nb = xcd * per + local / MB;
+  mb = local % MB;
+  return nb < NB;
+}
+
+// the epilogue's global inputs (targets / pre-activations) of this thread's rows, loaded before the K
+// loop so that their latency hides behind it: two waves per SIMD cannot hide a load latency per row
+constexpr int kLRows = kLN / (kLThreads / (kLM / 4));  // epilogue rows per thread (4)
+template <int MODE>
+__device__ __forceinline__ void lgemm_prefetch(const MArgs& a, int l, int m0, int64_t n0, float2 (&in)[kLRows][2]) {
+  const int tid = threadIdx.x;
+  const MLayer& lo = MODE == kLBwd ? a.layer[l - 1] : a.layer[l];
+  const int N = lo.no;
+  const int q = tid % (kLM / 4), rb0 = tid / (kLM / 4);
+  const int f0 = m0 + 4 * q;
+#pragma unroll
+  for (int k = 0; k < kLRows; ++k) {
+    const int64_t b = n0 + rb0 + k * (kLThreads / (kLM / 4));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int jj = (f0 >> 1) + h;
+      in[k][h] = float2{0.0f, 0.0f};
+      if (MODE == kLLast && jj < N && b < a.batch) in[k][h] = *reinterpret_cast<const float2*>(a.targets + (b * N + jj) * 2);
+      if (MODE == kLBwd && jj < N && lo.pre >= 0) in[k][h] = *reinterpret_cast<const float2*>(a.fws + lo.pre + b * (2 * N) + 2 * jj);
+    }
+  }
+}
+
+// ---- epilogue, from the [row][feature] tile of the accumulators in LDS (written and synchronised by
+// the caller): each thread takes 4 features of one batch row (row-major outputs, 16-B stores along the
+// features) and finally, without SMC_WGRAD_ROWMAJOR, whole 64-row feature lines (the ^T copies, 16-B
+// stores along the batch): every global store is a full 16-B piece of a contiguous line
+constexpr int kLTld = kLM + 4;  // tile row stride (floats): [row][feature], 16-B pieces conflict-free
+template <int MODE>
+__device__ __forceinline__ void lgemm_epilogue(const MArgs& a, int l, int mb, int nb, float* tile, float* part,
+                                               double* red, const float2 (&in)[kLRows][2]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* ws = static_cast<float*>(a.opws);
+  const float* P = a.params;
+  const MLayer& ly = a.layer[l];
+  const MLayer& lo = MODE == kLBwd ? a.layer[l - 1] : ly;  // the layer whose output (gradient) this launch writes
+  const int N = lo.no;
+  const int MB = static_cast<int>(a.lgemm_mb);
+  const int m0 = mb * kLM;
+  const int64_t n0 = static_cast<int64_t>(nb) * kLN;
+  const int q = tid % (kLM / 4), rb0 = tid / (kLM / 4);
+  const int f0 = m0 + 4 * q;
+  const int64_t bp = a.bp;
+  const int64_t blk = nb;  // batch block of kLN rows (= a.rows)
+  // the layer whose output (or output gradient) this launch writes, and its row-major / ^T buffers
+  const MLayer& nx = MODE == kLFwd ? a.layer[l + 1] : ly;
+  const int64_t rm_off = MODE == kLFwd ? nx.zr : lo.dr;
+  const int64_t tr_off = MODE == kLFwd ? nx.zt : lo.gt;
+  const int rm_ld = MODE == kLFwd ? nx.kx : lo.wout;  // row-major row length
+  const int nvalid = MODE == kLFwd ? ly.wout : lo.wout;  // features this launch writes
+  const float scale = 2.0f / static_cast<float>(static_cast<double>(a.batch) * ly.no);
+  double loss = 0.0;
+  float dcs[2] = {0.0f, 0.0f};
+#pragma unroll
+  for (int k = 0; k < kLRows; ++k) {
+    const int rr = rb0 + k * (kLThreads / (kLM / 4));
+    const int64_t b = n0 + rr;
+    const f32x4 x = *reinterpret_cast<const f32x4*>(&tile[rr * kLTld + 4 * q]);
+    float o[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int jj = (f0 >> 1) + h;
+      const float u = x[2 * h], v = x[2 * h + 1];
+      o[2 * h] = o[2 * h + 1] = 0.0f;
+      if constexpr (MODE == kLFwd) {
+        if (jj < ly.no) {
+          if (ly.pre >= 0) *reinterpret_cast<float2*>(a.fws + ly.pre + b * (2 * ly.no) + 2 * jj) = float2{u, v};
+          Act::fwd(ly.act, ly.act == SMC_ACT_MODRELU ? P[ly.act_bias + jj] : 0.0f, u, v, o[2 * h], o[2 * h + 1]);
+        } else {
+          o[2 * h] = 2 * jj == 2 * ly.no ? 1.0f : 0.0f;  // Z_{l+1}'s ones column, then zeros
+        }
+      } else if (jj < N && (MODE == kLBwd || b < a.batch)) {
+        const float cb = lo.act == SMC_ACT_MODRELU ? P[lo.act_bias + jj] : 0.0f;
+        float dc;
+        if constexpr (MODE == kLLast) {
+          float pr, pi;
+          Act::fwd(lo.act, cb, u, v, pr, pi);
+          const float2 t = in[k][h];
+          const float dr = pr - t.x, di = pi - t.y;
+          loss += static_cast<double>(dr * dr) + static_cast<double>(di * di);
+          Act::bwd(lo.act, cb, u, v, scale * dr, scale * di, o[2 * h], o[2 * h + 1], dc);
+        } else {
+          const float2 pre = in[k][h];
+          Act::bwd(lo.act, cb, pre.x, pre.y, u, v, o[2 * h], o[2 * h + 1], dc);
+        }
+        dcs[h] += dc;
+      }
+    }
+    if (f0 < nvalid) *reinterpret_cast<f32x4*>(ws + rm_off + b * rm_ld + f0) = f32x4{o[0], o[1], o[2], o[3]};
+    if constexpr (!SMC_WGRAD_ROWMAJOR)
+      *reinterpret_cast<f32x4*>(&tile[rr * kLTld + 4 * q]) = f32x4{o[0], o[1], o[2], o[3]};  // the ^T copy's values
+  }
+  if constexpr (MODE != kLFwd) {
+    // modReLU bias share of the block's kLN rows: each thread's rows in order, then the kLN / 8 row
+    // groups in order (through LDS, after the ^T tile is complete)
+    if (lo.cpart >= 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) part[rb0 * (kLM / 2) + 2 * q + h] = dcs[h];
+    }
+    if constexpr (MODE == kLLast) {  // block loss partial: thread sums, wave butterfly, waves in order
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) loss += __shfl_xor(loss, off, 64);
+      if (lane == 0) red[wave] = loss;
+    }
+    __syncthreads();
+    if (lo.cpart >= 0 && tid < kLM / 2) {
+      const int jj = m0 / 2 + tid;
+      float s = 0.0f;
+      for (int w = 0; w < kLThreads / (kLM / 4); ++w) s += part[w * (kLM / 2) + tid];
+      if (jj < N) a.fws[lo.cpart + blk * N + jj] = s;
+    }
+    if (MODE == kLLast && tid == 0) {
+      double t = 0.0;
+      for (int w = 0; w < kLThreads / 64; ++w) t += red[w];
+      a.lossp[blk * a.lpb + mb] = t;
+    }
+  } else {
+    __syncthreads();
+  }
+  // phase C: the ^T copy, whole 64-row lines of each feature (only for the transposed wgrad_kernel)
+  for (int e = tid; e < (SMC_WGRAD_ROWMAJOR ? 0 : kLM * (kLN / 4)); e += kLThreads) {
+    const int fr = e / (kLN / 4), q4 = e % (kLN / 4);
+    if (m0 + fr < nvalid)
+      *reinterpret_cast<f32x4*>(ws + tr_off + static_cast<int64_t>(m0 + fr) * bp + n0 + 4 * q4) =
+          f32x4{tile[(4 * q4) * kLTld + fr], tile[(4 * q4 + 1) * kLTld + fr], tile[(4 * q4 + 2) * kLTld + fr],
+                tile[(4 * q4 + 3) * kLTld + fr]};
+  }
+  if constexpr (MODE == kLFwd) {
+    // columns [wout, kx_{l+1}) of Z_{l+1} (the ones column when 2 no is a multiple of 16)
+    if (mb == MB - 1) {
+      for (int e = tid; e < (nx.kx - ly.wout) * kLN; e += kLThreads) {
+        const int k = ly.wout + e / kLN;
+        const int64_t b = n0 + e % kLN;
+        const float v = k == 2 * ly.no ? 1.0f : 0.0f;
+        ws[nx.zr + b * nx.kx + k] = v;
+        if constexpr (!SMC_WGRAD_ROWMAJOR) ws[nx.zt + static_cast<int64_t>(k) * bp + b] = v;
+      }
+    }
+  }
+}
+
+// C[m][n] = sum_k A[m][k] B[n][k]: fwd / last A = Wc [wout][kx], B = Z_l [bp][kx];
+// bwd A = Wc^T [win][wout], B = dU_l [bp][wout]
+struct LOperands {
+  const float* A;
+  const float* B;
+  int K, Mrows;
+};
+template <int MODE>
+__device__ __forceinline__ LOperands lgemm_operands(const MArgs& a, int l) {
+  const MLayer& ly = a.layer[l];
+  const bool bwd = MODE == kLBwd;
+  const float* ws = static_cast<const float*>(a.opws);
+  return LOperands{ws + (bwd ? ly.wct : ly.wc), ws + (bwd ? ly.dr : ly.zr), bwd ? ly.wout : ly.kx,
+                   bwd ? ly.win : ly.wout};
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   __shared__ __attribute__((aligned(16))) float sa[2][kLM * kLLd];
   __shared__ __attribute__((aligned(16))) float sb[2][kLN * kLLd];
   __shared__ double red[kLThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, c = lane & 15;
-  float* ws = static_cast<float*>(a.opws);
-  const float* P = a.params;
-  // C[m][n] = sum_k A[m][k] B[n][k]: fwd / last A = Wc [wout][kx], B = Z_l [bp][kx];
-  // bwd A = Wc^T [win][wout], B = dU_l [bp][wout]
-  // XCD-aware tile order: the 1-D grid's consecutive workgroups go round-robin to the 8 XCDs, so
-  // workgroup w runs on XCD w % 8; each XCD takes a contiguous eighth of the batch blocks with every
-  // feature block, and reads only its eighth of the row operand (B) and the whole weight matrix (A)
-  // into its own L2, instead of every XCD streaming all of B past one feature block
-  // (NB not a multiple of 8: the grid is rounded up to 8 equal XCD ranges and the workgroups past the
-  // last batch block return at once)
-  const int MB = static_cast<int>(a.lgemm_mb);
-  const int NB = static_cast<int>(a.bp / kLN);
   int mb, nb;
-  {
-    const int per = (NB + 7) >> 3;
-    const int xcd = static_cast<int>(blockIdx.x) & 7, local = static_cast<int>(blockIdx.x) >> 3;
-    nb = xcd * per + local / MB;
-    mb = local % MB;
-    if (nb >= NB) return;  // uniform, before any barrier
-  }
-  const int64_t kbeg = 0;
-  const MLayer& ly = a.layer[l];
-  const bool bwd = MODE == kLBwd;
-  const float* A = ws + (bwd ? ly.wct : ly.wc);
-  const float* B = ws + (bwd ? ly.dr : ly.zr);
-  const int K = bwd ? ly.wout : ly.kx;
+  if (!lgemm_tile(a, mb, nb)) return;  // uniform, before any barrier
+  const LOperands op = lgemm_operands<MODE>(a, l);
+  const float* A = op.A;
+  const float* B = op.B;
+  const int K = op.K, Mrows = op.Mrows;
   const int64_t lda = K, ldb = K;
-  const int Mrows = bwd ? ly.win : ly.wout;
   const int64_t Nrows = a.bp;
   const int m0 = mb * kLM;
   const int64_t n0 = static_cast<int64_t>(nb) * kLN;
@@ -872,15 +1024,14 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
     for (int v = 0; v < AV; ++v) {
       const int i = v * kLThreads + tid, r = i / (kLK / 4), q = i % (kLK / 4);
       const bool ok = m0 + r < Mrows && k0 + 4 * q < K;
-      const f32x4 x = *reinterpret_cast<const f32x4*>(
-          A + (ok ? static_cast<int64_t>(m0 + r) * lda + kbeg + k0 + 4 * q : 0));
+      const f32x4 x = *reinterpret_cast<const f32x4*>(A + (ok ? static_cast<int64_t>(m0 + r) * lda + k0 + 4 * q : 0));
       ra[v] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
       const int i = v * kLThreads + tid, r = i / (kLK / 4), q = i % (kLK / 4);
       const bool ok = n0 + r < Nrows && k0 + 4 * q < K;
-      const f32x4 x = *reinterpret_cast<const f32x4*>(B + (ok ? (n0 + r) * ldb + kbeg + k0 + 4 * q : 0));
+      const f32x4 x = *reinterpret_cast<const f32x4*>(B + (ok ? (n0 + r) * ldb + k0 + 4 * q : 0));
       rb[v] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
@@ -896,27 +1047,8 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
       *reinterpret_cast<f32x4*>(&sb[buf][r * kLLd + 4 * q]) = rb[v];
     }
   };
-  // the layer whose output (or output gradient) this launch writes
-  const MLayer& lo = MODE == kLBwd ? a.layer[l - 1] : ly;
-  const int N = lo.no;
-  // epilogue phase B: thread -> features 4q .. 4q + 3 (2 complex outputs) of rows rb0, rb0 + 16, ...
-  const int q = tid % (kLM / 4), rb0 = tid / (kLM / 4);
-  const int f0 = m0 + 4 * q;
-  // the row loop's global inputs (targets / pre-activations), loaded before the K loop so that their
-  // latency hides behind it: two waves per SIMD cannot hide a load latency per row of the epilogue
-  constexpr int kRows = kLN / (kLThreads / (kLM / 4));  // rows per thread (4)
-  float2 in[kRows][2];
-#pragma unroll
-  for (int k = 0; k < kRows; ++k) {
-    const int64_t b = n0 + rb0 + k * (kLThreads / (kLM / 4));
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int jj = (f0 >> 1) + h;
-      in[k][h] = float2{0.0f, 0.0f};
-      if (MODE == kLLast && jj < N && b < a.batch) in[k][h] = *reinterpret_cast<const float2*>(a.targets + (b * N + jj) * 2);
-      if (MODE == kLBwd && jj < N && lo.pre >= 0) in[k][h] = *reinterpret_cast<const float2*>(a.fws + lo.pre + b * (2 * N) + 2 * jj);
-    }
-  }
+  float2 in[kLRows][2];
+  lgemm_prefetch<MODE>(a, l, m0, n0, in);
   f32x4 acc[kLTM][kLTN];
 #pragma unroll
   for (int i = 0; i < kLTM; ++i)
@@ -966,118 +1098,149 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
     mma(0);
   }
   if (tail) __syncthreads();  // the epilogue tile reuses the stage buffers
-
-  // ---- epilogue, through LDS: the accumulators go to a [feature][row] tile; each thread then takes
-  // 4 features of one batch row (row-major outputs, 16-B stores along the features) and finally whole
-  // 64-row feature lines (the ^T copies, 16-B stores along the batch): every global store is a full
-  // 16-B piece of a contiguous line instead of 4-B pieces of 16 lines
-  constexpr int TLD = kLM + 4;  // tile row stride (floats): [row][feature], 16-B pieces conflict-free
-  static_assert(kLN * TLD <= 2 * kLM * kLLd, "tile fits the A stage buffers");
-  float* tile = &sa[0][0];      // [kLN][TLD] over both A stage buffers, free after the K loop
+  static_assert(kLN * kLTld <= 2 * kLM * kLLd, "tile fits the A stage buffers");
+  float* tile = &sa[0][0];  // [kLN][kLTld] over both A stage buffers, free after the K loop
 #pragma unroll
   for (int i = 0; i < kLTM; ++i)
 #pragma unroll
     for (int j = 0; j < kLTN; ++j)
-      *reinterpret_cast<f32x4*>(&tile[(j * 16 + c) * TLD + (wave * kLTM + i) * 16 + 4 * g]) = acc[i][j];
+      *reinterpret_cast<f32x4*>(&tile[(j * 16 + c) * kLTld + (wave * kLTM + i) * 16 + 4 * g]) = acc[i][j];
   __syncthreads();
-  const int64_t bp = a.bp;
-  const int64_t blk = nb;  // batch block of kLN rows (= a.rows)
-  // the layer whose output (or output gradient) this launch writes, and its row-major / ^T buffers
-  const MLayer& nx = MODE == kLFwd ? a.layer[l + 1] : ly;
-  const int64_t rm_off = MODE == kLFwd ? nx.zr : lo.dr;
-  const int64_t tr_off = MODE == kLFwd ? nx.zt : lo.gt;
-  const int rm_ld = MODE == kLFwd ? nx.kx : lo.wout;  // row-major row length
-  const int nvalid = MODE == kLFwd ? ly.wout : lo.wout;  // features this launch writes
-  const float scale = 2.0f / static_cast<float>(static_cast<double>(a.batch) * ly.no);
-  double loss = 0.0;
-  float dcs[2] = {0.0f, 0.0f};
+  lgemm_epilogue<MODE>(a, l, mb, nb, tile, sb[0], red, in);
+}
+
+// ---- the same GEMMs on the bf16 matrix cores, f32-exact operands (round 4) ----------------------
+// An f32 x splits exactly into three bf16 pieces by truncation: h = x with the low 16 bits cleared,
+// m = (x - h) likewise, l = x - h - m (8 significant bits at most, so a bf16 exactly): x = h + m + l.
+// A product a b is then the 9 exact bf16 products of the pieces; each v_mfma_f32_16x16x32_bf16 adds 32
+// of them into the f32 accumulator.  With all 9 (SMC_LGEMM_SPLIT_TERMS 9) the GEMM is f32 arithmetic on
+// exact products (no product rounding at all); with 6 the three smallest (m l, l m, l l: below 2^-22
+// |a b|) are dropped.  Per 32-deep K block a wave runs 4 tiles x 6 or 9 MFMAs of 16 cycles against
+// 4 x 8 f32 MFMAs of 32 cycles.  The pieces are made when a stage is written to LDS (one plane per
+// piece, [row][32 + 8] bf16: 80-B rows, fragment reads 16 B per lane); waves tile the 64 x 64 block
+// 2 x 2 (32 features x 32 rows each: 6 fragment reads per 4 tiles and term).
+#ifndef SMC_LGEMM_SPLIT_TERMS
+#define SMC_LGEMM_SPLIT_TERMS 9
+#endif
+constexpr int kSK = 32, kSLd = kSK + 8;  // K stage (one bf16 MFMA block), LDS row stride (bf16)
+__device__ __forceinline__ void split3(f32x4 x, u16x4& h, u16x4& m, u16x4& lo) {
 #pragma unroll
-  for (int k = 0; k < kRows; ++k) {
-    const int rr = rb0 + k * (kLThreads / (kLM / 4));
-    const int64_t b = n0 + rr;
-    const f32x4 x = *reinterpret_cast<const f32x4*>(&tile[rr * TLD + 4 * q]);
-    float o[4];
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t u = __float_as_uint(x[e]);
+    const uint32_t uh = u & 0xffff0000u;
+    const float r1 = x[e] - __uint_as_float(uh);
+    const uint32_t um = __float_as_uint(r1) & 0xffff0000u;
+    const float r2 = r1 - __uint_as_float(um);
+    h[e] = static_cast<uint16_t>(uh >> 16);
+    m[e] = static_cast<uint16_t>(um >> 16);
+    lo[e] = static_cast<uint16_t>(__float_as_uint(r2) >> 16);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kLThreads) void lgemm_split_kernel(MArgs a, int l) {
+  // two stages x 3 planes x 64 rows x kSLd bf16 for A and for B (30 KiB each); the epilogue's f32 tile
+  // reuses A's
+  __shared__ __attribute__((aligned(16))) uint16_t sa[2][3][kLM * kSLd];
+  __shared__ __attribute__((aligned(16))) uint16_t sb[2][3][kLN * kSLd];
+  __shared__ double red[kLThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int fw = wave & 1, rw = wave >> 1;  // the wave's 32-feature half and 32-row half
+  int mb, nb;
+  if (!lgemm_tile(a, mb, nb)) return;  // uniform, before any barrier
+  const LOperands op = lgemm_operands<MODE>(a, l);
+  const float* A = op.A;
+  const float* B = op.B;
+  const int K = op.K, Mrows = op.Mrows;
+  const int64_t Nrows = a.bp;
+  const int m0 = mb * kLM;
+  const int64_t n0 = static_cast<int64_t>(nb) * kLN;
+  constexpr int AV = kLM * kSK / 4 / kLThreads, BV = kLN * kSK / 4 / kLThreads;  // 2 and 2
+  f32x4 ra[AV], rb[BV];
+  auto fetch = [&](int k0) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int jj = (f0 >> 1) + h;
-      const float u = x[2 * h], v = x[2 * h + 1];
-      o[2 * h] = o[2 * h + 1] = 0.0f;
-      if constexpr (MODE == kLFwd) {
-        if (jj < ly.no) {
-          if (ly.pre >= 0) *reinterpret_cast<float2*>(a.fws + ly.pre + b * (2 * ly.no) + 2 * jj) = float2{u, v};
-          Act::fwd(ly.act, ly.act == SMC_ACT_MODRELU ? P[ly.act_bias + jj] : 0.0f, u, v, o[2 * h], o[2 * h + 1]);
-        } else {
-          o[2 * h] = 2 * jj == 2 * ly.no ? 1.0f : 0.0f;  // Z_{l+1}'s ones column, then zeros
-        }
-      } else if (jj < N && (MODE == kLBwd || b < a.batch)) {
-        const float cb = lo.act == SMC_ACT_MODRELU ? P[lo.act_bias + jj] : 0.0f;
-        float dc;
-        if constexpr (MODE == kLLast) {
-          float pr, pi;
-          Act::fwd(lo.act, cb, u, v, pr, pi);
-          const float2 t = in[k][h];
-          const float dr = pr - t.x, di = pi - t.y;
-          loss += static_cast<double>(dr * dr) + static_cast<double>(di * di);
-          Act::bwd(lo.act, cb, u, v, scale * dr, scale * di, o[2 * h], o[2 * h + 1], dc);
-        } else {
-          const float2 pre = in[k][h];
-          Act::bwd(lo.act, cb, pre.x, pre.y, u, v, o[2 * h], o[2 * h + 1], dc);
-        }
-        dcs[h] += dc;
+    for (int v = 0; v < AV; ++v) {
+      const int i = v * kLThreads + tid, r = i / (kSK / 4), q = i % (kSK / 4);
+      const bool ok = m0 + r < Mrows && k0 + 4 * q < K;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(A + (ok ? static_cast<int64_t>(m0 + r) * K + k0 + 4 * q : 0));
+      ra[v] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      const int i = v * kLThreads + tid, r = i / (kSK / 4), q = i % (kSK / 4);
+      const bool ok = n0 + r < Nrows && k0 + 4 * q < K;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(B + (ok ? (n0 + r) * K + k0 + 4 * q : 0));
+      rb[v] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      const int i = v * kLThreads + tid, r = i / (kSK / 4), q = i % (kSK / 4);
+      u16x4 h, m, lo;
+      split3(ra[v], h, m, lo);
+      *reinterpret_cast<u16x4*>(&sa[buf][0][r * kSLd + 4 * q]) = h;
+      *reinterpret_cast<u16x4*>(&sa[buf][1][r * kSLd + 4 * q]) = m;
+      *reinterpret_cast<u16x4*>(&sa[buf][2][r * kSLd + 4 * q]) = lo;
+    }
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      const int i = v * kLThreads + tid, r = i / (kSK / 4), q = i % (kSK / 4);
+      u16x4 h, m, lo;
+      split3(rb[v], h, m, lo);
+      *reinterpret_cast<u16x4*>(&sb[buf][0][r * kSLd + 4 * q]) = h;
+      *reinterpret_cast<u16x4*>(&sb[buf][1][r * kSLd + 4 * q]) = m;
+      *reinterpret_cast<u16x4*>(&sb[buf][2][r * kSLd + 4 * q]) = lo;
+    }
+  };
+  float2 in[kLRows][2];
+  lgemm_prefetch<MODE>(a, l, m0, n0, in);
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // K a multiple of 16: a last half stage reads zeros past K (fetch zero-fills), no tail loop
+  const int nst = (K + kSK - 1) / kSK;
+  fetch(0);
+  put(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) fetch((st + 1) * kSK);
+    bf16x8 af[3][2], bf[3][2];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[p][i] = *reinterpret_cast<const bf16x8*>(&sa[buf][p][(fw * 32 + i * 16 + c) * kSLd + 8 * g]);
+        bf[p][i] = *reinterpret_cast<const bf16x8*>(&sb[buf][p][(rw * 32 + i * 16 + c) * kSLd + 8 * g]);
       }
-    }
-    if (f0 < nvalid) *reinterpret_cast<f32x4*>(ws + rm_off + b * rm_ld + f0) = f32x4{o[0], o[1], o[2], o[3]};
-    if constexpr (!SMC_WGRAD_ROWMAJOR)
-      *reinterpret_cast<f32x4*>(&tile[rr * TLD + 4 * q]) = f32x4{o[0], o[1], o[2], o[3]};  // the ^T copy's values
-  }
-  if constexpr (MODE != kLFwd) {
-    // modReLU bias share of the block's kLN rows: each thread's rows in order, then the kLN / 8 row
-    // groups in order (through LDS, after the ^T tile is complete)
-    float* part = sb[0];  // [8][kLM / 2] complex outputs
-    if (lo.cpart >= 0) {
+    // smallest terms first; the 4 tiles' MFMAs interleaved (independent accumulators between
+    // dependent ones)
+    constexpr int kTerms = SMC_LGEMM_SPLIT_TERMS;
+    constexpr int ta[9] = {2, 1, 2, 0, 1, 2, 0, 1, 0};  // piece of A per term (l l, m l, l m, h l, m m, l h, h m, m h, h h)
+    constexpr int tb[9] = {2, 2, 1, 2, 1, 0, 1, 0, 0};
 #pragma unroll
-      for (int h = 0; h < 2; ++h) part[rb0 * (kLM / 2) + 2 * q + h] = dcs[h];
-    }
-    if constexpr (MODE == kLLast) {  // block loss partial: thread sums, wave butterfly, waves in order
+    for (int t = 9 - kTerms; t < 9; ++t)
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) loss += __shfl_xor(loss, off, 64);
-      if (lane == 0) red[wave] = loss;
-    }
-    __syncthreads();
-    if (lo.cpart >= 0 && tid < kLM / 2) {
-      const int jj = m0 / 2 + tid;
-      float s = 0.0f;
-      for (int w = 0; w < kLThreads / (kLM / 4); ++w) s += part[w * (kLM / 2) + tid];
-      if (jj < N) a.fws[lo.cpart + blk * N + jj] = s;
-    }
-    if (MODE == kLLast && tid == 0) {
-      double t = 0.0;
-      for (int w = 0; w < kLThreads / 64; ++w) t += red[w];
-      a.lossp[blk * a.lpb + mb] = t;
-    }
-  } else {
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ta[t]][i], bf[tb[t]][j], acc[i][j], 0, 0, 0);
+    if (st + 1 < nst) put(buf ^ 1);
     __syncthreads();
   }
-  // phase C: the ^T copy, whole 64-row lines of each feature (only for the transposed wgrad_kernel)
-  for (int e = tid; e < (SMC_WGRAD_ROWMAJOR ? 0 : kLM * (kLN / 4)); e += kLThreads) {
-    const int fr = e / (kLN / 4), q4 = e % (kLN / 4);
-    if (m0 + fr < nvalid)
-      *reinterpret_cast<f32x4*>(ws + tr_off + static_cast<int64_t>(m0 + fr) * bp + n0 + 4 * q4) =
-          f32x4{tile[(4 * q4) * TLD + fr], tile[(4 * q4 + 1) * TLD + fr], tile[(4 * q4 + 2) * TLD + fr],
-                tile[(4 * q4 + 3) * TLD + fr]};
-  }
-  if constexpr (MODE == kLFwd) {
-    // columns [wout, kx_{l+1}) of Z_{l+1} (the ones column when 2 no is a multiple of 16)
-    if (mb == MB - 1) {
-      for (int e = tid; e < (nx.kx - ly.wout) * kLN; e += kLThreads) {
-        const int k = ly.wout + e / kLN;
-        const int64_t b = n0 + e % kLN;
-        const float v = k == 2 * ly.no ? 1.0f : 0.0f;
-        ws[nx.zr + b * nx.kx + k] = v;
-        if constexpr (!SMC_WGRAD_ROWMAJOR) ws[nx.zt + static_cast<int64_t>(k) * bp + b] = v;
-      }
-    }
-  }
+  static_assert(kLN * kLTld * 4 <= 2 * 3 * kLM * kSLd * 2, "tile fits the A stage buffers");
+  float* tile = reinterpret_cast<float*>(&sa[0][0][0]);  // [kLN][kLTld], free after the K loop
+  // acc[i][j] lane (g, c): features fw 32 + 16 i + 4 g + 0..3 of batch row rw 32 + 16 j + c
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      *reinterpret_cast<f32x4*>(&tile[(rw * 32 + j * 16 + c) * kLTld + fw * 32 + i * 16 + 4 * g]) = acc[i][j];
+  __syncthreads();
+  lgemm_epilogue<MODE>(a, l, mb, nb, tile, reinterpret_cast<float*>(&sb[0][0][0]), red, in);
 }
 
 // ---- host plan ---------------------------------------------------------------------------------
@@ -1244,6 +1407,9 @@ int32_t launch_fb(const Plan& p, hipStream_t s) {
   return SMC_OK;
 }
 
+#ifndef SMC_LGEMM_KERNEL
+#define SMC_LGEMM_KERNEL lgemm_split_kernel
+#endif
 int32_t launch_layered(const Plan& p, hipStream_t s) {
   const MArgs& a = p.a;
   // (row-major wgrad: no Z_0^T region)
@@ -1256,14 +1422,14 @@ int32_t launch_layered(const Plan& p, hipStream_t s) {
   for (int l = 0; l < L; ++l) {
     g.lgemm_mb = (a.layer[l].wout + kLM - 1) / kLM;
     const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * byx);
-    if (l + 1 < L) hipLaunchKernelGGL(lgemm_kernel<kLFwd>, grid, dim3(kLThreads), 0, s, g, l);
-    else hipLaunchKernelGGL(lgemm_kernel<kLLast>, grid, dim3(kLThreads), 0, s, g, l);
+    if (l + 1 < L) hipLaunchKernelGGL(SMC_LGEMM_KERNEL<kLFwd>, grid, dim3(kLThreads), 0, s, g, l);
+    else hipLaunchKernelGGL(SMC_LGEMM_KERNEL<kLLast>, grid, dim3(kLThreads), 0, s, g, l);
     if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
   }
   for (int l = L - 1; l >= 1; --l) {
     g.lgemm_mb = (a.layer[l].win + kLM - 1) / kLM;
     const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * byx);
-    hipLaunchKernelGGL(lgemm_kernel<kLBwd>, grid, dim3(kLThreads), 0, s, g, l);
+    hipLaunchKernelGGL(SMC_LGEMM_KERNEL<kLBwd>, grid, dim3(kLThreads), 0, s, g, l);
     if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
   }
   // weight gradients in wgrad_kernel's 64 x 64 blocks over batch segments (they measured faster here than
