@@ -1109,140 +1109,6 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   lgemm_epilogue<MODE>(a, l, mb, nb, tile, sb[0], red, in);
 }
 
-// ---- the same GEMMs on the bf16 matrix cores, f32-exact operands (round 4) ----------------------
-// An f32 x splits exactly into three bf16 pieces by truncation: h = x with the low 16 bits cleared,
-// m = (x - h) likewise, l = x - h - m (8 significant bits at most, so a bf16 exactly): x = h + m + l.
-// A product a b is then the 9 exact bf16 products of the pieces; each v_mfma_f32_16x16x32_bf16 adds 32
-// of them into the f32 accumulator.  With all 9 (SMC_LGEMM_SPLIT_TERMS 9) the GEMM is f32 arithmetic on
-// exact products (no product rounding at all); with 6 the three smallest (m l, l m, l l: below 2^-22
-// |a b|) are dropped.  Per 32-deep K block a wave runs 4 tiles x 6 or 9 MFMAs of 16 cycles against
-// 4 x 8 f32 MFMAs of 32 cycles.  The pieces are made when a stage is written to LDS (one plane per
-// piece, [row][32 + 8] bf16: 80-B rows, fragment reads 16 B per lane); waves tile the 64 x 64 block
-// 2 x 2 (32 features x 32 rows each: 6 fragment reads per 4 tiles and term).
-#ifndef SMC_LGEMM_SPLIT_TERMS
-#define SMC_LGEMM_SPLIT_TERMS 9
-#endif
-constexpr int kSK = 32, kSLd = kSK + 8;  // K stage (one bf16 MFMA block), LDS row stride (bf16)
-__device__ __forceinline__ void split3(f32x4 x, u16x4& h, u16x4& m, u16x4& lo) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const uint32_t u = __float_as_uint(x[e]);
-    const uint32_t uh = u & 0xffff0000u;
-    const float r1 = x[e] - __uint_as_float(uh);
-    const uint32_t um = __float_as_uint(r1) & 0xffff0000u;
-    const float r2 = r1 - __uint_as_float(um);
-    h[e] = static_cast<uint16_t>(uh >> 16);
-    m[e] = static_cast<uint16_t>(um >> 16);
-    lo[e] = static_cast<uint16_t>(__float_as_uint(r2) >> 16);
-  }
-}
-
-template <int MODE>
-__global__ __launch_bounds__(kLThreads) void lgemm_split_kernel(MArgs a, int l) {
-  // two stages x 3 planes x 64 rows x kSLd bf16 for A and for B (30 KiB each); the epilogue's f32 tile
-  // reuses A's
-  __shared__ __attribute__((aligned(16))) uint16_t sa[2][3][kLM * kSLd];
-  __shared__ __attribute__((aligned(16))) uint16_t sb[2][3][kLN * kSLd];
-  __shared__ double red[kLThreads / 64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, c = lane & 15;
-  const int fw = wave & 1, rw = wave >> 1;  // the wave's 32-feature half and 32-row half
-  int mb, nb;
-  if (!lgemm_tile(a, mb, nb)) return;  // uniform, before any barrier
-  const LOperands op = lgemm_operands<MODE>(a, l);
-  const float* A = op.A;
-  const float* B = op.B;
-  const int K = op.K, Mrows = op.Mrows;
-  const int64_t Nrows = a.bp;
-  const int m0 = mb * kLM;
-  const int64_t n0 = static_cast<int64_t>(nb) * kLN;
-  constexpr int AV = kLM * kSK / 4 / kLThreads, BV = kLN * kSK / 4 / kLThreads;  // 2 and 2
-  f32x4 ra[AV], rb[BV];
-  auto fetch = [&](int k0) {
-#pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      const int i = v * kLThreads + tid, r = i / (kSK / 4), q = i % (kSK / 4);
-      const bool ok = m0 + r < Mrows && k0 + 4 * q < K;
-      const f32x4 x = *reinterpret_cast<const f32x4*>(A + (ok ? static_cast<int64_t>(m0 + r) * K + k0 + 4 * q : 0));
-      ra[v] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      const int i = v * kLThreads + tid, r = i / (kSK / 4), q = i % (kSK / 4);
-      const bool ok = n0 + r < Nrows && k0 + 4 * q < K;
-      const f32x4 x = *reinterpret_cast<const f32x4*>(B + (ok ? (n0 + r) * K + k0 + 4 * q : 0));
-      rb[v] = ok ? x : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  auto put = [&](int buf) {
-#pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      const int i = v * kLThreads + tid, r = i / (kSK / 4), q = i % (kSK / 4);
-      u16x4 h, m, lo;
-      split3(ra[v], h, m, lo);
-      *reinterpret_cast<u16x4*>(&sa[buf][0][r * kSLd + 4 * q]) = h;
-      *reinterpret_cast<u16x4*>(&sa[buf][1][r * kSLd + 4 * q]) = m;
-      *reinterpret_cast<u16x4*>(&sa[buf][2][r * kSLd + 4 * q]) = lo;
-    }
-#pragma unroll
-    for (int v = 0; v < BV; ++v) {
-      const int i = v * kLThreads + tid, r = i / (kSK / 4), q = i % (kSK / 4);
-      u16x4 h, m, lo;
-      split3(rb[v], h, m, lo);
-      *reinterpret_cast<u16x4*>(&sb[buf][0][r * kSLd + 4 * q]) = h;
-      *reinterpret_cast<u16x4*>(&sb[buf][1][r * kSLd + 4 * q]) = m;
-      *reinterpret_cast<u16x4*>(&sb[buf][2][r * kSLd + 4 * q]) = lo;
-    }
-  };
-  float2 in[kLRows][2];
-  lgemm_prefetch<MODE>(a, l, m0, n0, in);
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // K a multiple of 16: a last half stage reads zeros past K (fetch zero-fills), no tail loop
-  const int nst = (K + kSK - 1) / kSK;
-  fetch(0);
-  put(0);
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nst) fetch((st + 1) * kSK);
-    bf16x8 af[3][2], bf[3][2];
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        af[p][i] = *reinterpret_cast<const bf16x8*>(&sa[buf][p][(fw * 32 + i * 16 + c) * kSLd + 8 * g]);
-        bf[p][i] = *reinterpret_cast<const bf16x8*>(&sb[buf][p][(rw * 32 + i * 16 + c) * kSLd + 8 * g]);
-      }
-    // smallest terms first; the 4 tiles' MFMAs interleaved (independent accumulators between
-    // dependent ones)
-    constexpr int kTerms = SMC_LGEMM_SPLIT_TERMS;
-    constexpr int ta[9] = {2, 1, 2, 0, 1, 2, 0, 1, 0};  // piece of A per term (l l, m l, l m, h l, m m, l h, h m, m h, h h)
-    constexpr int tb[9] = {2, 2, 1, 2, 1, 0, 1, 0, 0};
-#pragma unroll
-    for (int t = 9 - kTerms; t < 9; ++t)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ta[t]][i], bf[tb[t]][j], acc[i][j], 0, 0, 0);
-    if (st + 1 < nst) put(buf ^ 1);
-    __syncthreads();
-  }
-  static_assert(kLN * kLTld * 4 <= 2 * 3 * kLM * kSLd * 2, "tile fits the A stage buffers");
-  float* tile = reinterpret_cast<float*>(&sa[0][0][0]);  // [kLN][kLTld], free after the K loop
-  // acc[i][j] lane (g, c): features fw 32 + 16 i + 4 g + 0..3 of batch row rw 32 + 16 j + c
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      *reinterpret_cast<f32x4*>(&tile[(rw * 32 + j * 16 + c) * kLTld + fw * 32 + i * 16 + 4 * g]) = acc[i][j];
-  __syncthreads();
-  lgemm_epilogue<MODE>(a, l, mb, nb, tile, reinterpret_cast<float*>(&sb[0][0][0]), red, in);
-}
-
 // ---- host plan ---------------------------------------------------------------------------------
 struct Plan {
   MArgs a;
@@ -1407,9 +1273,6 @@ int32_t launch_fb(const Plan& p, hipStream_t s) {
   return SMC_OK;
 }
 
-#ifndef SMC_LGEMM_KERNEL
-#define SMC_LGEMM_KERNEL lgemm_split_kernel
-#endif
 int32_t launch_layered(const Plan& p, hipStream_t s) {
   const MArgs& a = p.a;
   // (row-major wgrad: no Z_0^T region)
@@ -1422,14 +1285,14 @@ int32_t launch_layered(const Plan& p, hipStream_t s) {
   for (int l = 0; l < L; ++l) {
     g.lgemm_mb = (a.layer[l].wout + kLM - 1) / kLM;
     const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * byx);
-    if (l + 1 < L) hipLaunchKernelGGL(SMC_LGEMM_KERNEL<kLFwd>, grid, dim3(kLThreads), 0, s, g, l);
-    else hipLaunchKernelGGL(SMC_LGEMM_KERNEL<kLLast>, grid, dim3(kLThreads), 0, s, g, l);
+    if (l + 1 < L) hipLaunchKernelGGL(lgemm_kernel<kLFwd>, grid, dim3(kLThreads), 0, s, g, l);
+    else hipLaunchKernelGGL(lgemm_kernel<kLLast>, grid, dim3(kLThreads), 0, s, g, l);
     if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
   }
   for (int l = L - 1; l >= 1; --l) {
     g.lgemm_mb = (a.layer[l].win + kLM - 1) / kLM;
     const dim3 grid(static_cast<unsigned>(g.lgemm_mb) * byx);
-    hipLaunchKernelGGL(SMC_LGEMM_KERNEL<kLBwd>, grid, dim3(kLThreads), 0, s, g, l);
+    hipLaunchKernelGGL(lgemm_kernel<kLBwd>, grid, dim3(kLThreads), 0, s, g, l);
     if (int32_t rc = check_launch("cvnn lgemm_kernel")) return rc;
   }
   // weight gradients in wgrad_kernel's 64 x 64 blocks over batch segments (they measured faster here than
