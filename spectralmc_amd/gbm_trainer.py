@@ -436,6 +436,10 @@ class GbmCVNNPricer:
     #: ms/step unmasked against 0.222 masked; the lock-step shape, 2.7e8: 0.308 masked against 0.329;
     #: profiles/r04/netcus_small_shapes.jsonl)
     network_cu_min_path_steps: int = 1 << 27
+    #: overlap_mc for the rows_kernel + cf_kernel shapes (f64): step s's network part beside step s+1's
+    #: rows launch, whose persistent workgroups leave registers and LDS for a network workgroup per CU
+    #: at the f64 register budget; False runs those shapes on one stream
+    overlap_rows: bool = True
     #: launches whose workgroups wait for each other (the sliced resident kernel, C3; the resident
     #: basket kernel, C5) need every workgroup of a group co-resident.  A collective that spins on a
     #: few CUs while it waits for a slow peer (RCCL in data-parallel runs) can hold those CUs past the
@@ -813,7 +817,8 @@ class TrainingSession:
         # duration (persistent, contracts from a queue): a concurrent network part gets no tail to run
         # in and only stretches it (C2 in f64, round 3: 10.55 ms/step overlapped, 10.35 sequential), so
         # those shapes run the step on one stream
-        overlap = pricer.overlap_mc and not getattr(self.engine, "kernel_name", "").startswith("rows_")
+        overlap = pricer.overlap_mc and (pricer.overlap_rows or
+                                         not getattr(self.engine, "kernel_name", "").startswith("rows_"))
         if overlap:
             # the network part is a few short launches: a high-priority queue lets its workgroups
             # take CU slots as the long MC kernel frees them instead of queueing behind it
