@@ -813,10 +813,12 @@ class TrainingSession:
         cur = torch.cuda.current_stream(dev)
         self._hip_streams: list[int] = []  # CU-masked streams this session created (destroyed at close)
         self.network_cus_used = 0  # CUs of the network's CU-masked stream (0: no masks)
-        # rows_kernel (f64, the f32 shapes no resident launch takes) keeps every CU slot for its whole
-        # duration (persistent, contracts from a queue): a concurrent network part gets no tail to run
-        # in and only stretches it (C2 in f64, round 3: 10.55 ms/step overlapped, 10.35 sequential), so
-        # those shapes run the step on one stream
+        # rows_kernel (f64, the f32 shapes no resident launch takes) is persistent.  At round 3's 8 waves
+        # per SIMD it left no registers for a concurrent network part, which only stretched it (C2 in f64:
+        # 10.55 ms/step overlapped, 10.35 sequential); at the f64 register budget (two workgroups per CU,
+        # 4 waves per SIMD) a network workgroup fits beside it and the latency-bound f64 network hides
+        # under the VALU-bound path launch (round 4: 8.64-8.71 against 8.81-8.89 ms/step,
+        # profiles/r04/ab_f64_overlap_rows.txt).  overlap_rows=False runs those shapes on one stream.
         overlap = pricer.overlap_mc and (pricer.overlap_rows or
                                          not getattr(self.engine, "kernel_name", "").startswith("rows_"))
         if overlap:
