@@ -780,8 +780,14 @@ __global__ __launch_bounds__(kThreads) void wgrad_rm_kernel(MArgs a) {
 // four 16-lane groups ({0-3, 12-15, 20-27}, ...; MI355X_MICROARCH.md, LDS), and at stride 68 every group
 // had two lanes on one bank quad (PMC: 1.4e6 conflict cycles per H = 256 GEMM); 72 is conflict-free
 constexpr int kLM = SMC_LGEMM_M, kLN = SMC_LGEMM_N, kLK = SMC_LGEMM_K, kLLd = kLK + 8;  // tile (features x batch rows), K stage, LDS stride
-constexpr int kLThreads = 256;  // 4 waves x (kLM / 4 features x 64 rows); kLM = 64: 512 workgroups at H = 256 (263 vs 269 us per step with 128)
-constexpr int kLTM = kLM / 4 / 16, kLTN = kLN / 16;           // 16 x 16 tiles per wave
+#ifndef SMC_LGEMM_THREADS
+#define SMC_LGEMM_THREADS 256
+#endif
+// waves: 4 along the features (kLM / 4 each) x kLWR along the batch rows (kLN / kLWR each); kLM = 64: 512
+// workgroups at H = 256 (263 vs 269 us per step with 128)
+constexpr int kLThreads = SMC_LGEMM_THREADS;
+constexpr int kLWF = 4, kLWR = kLThreads / 64 / kLWF;
+constexpr int kLTM = kLM / kLWF / 16, kLTN = kLN / kLWR / 16;  // 16 x 16 tiles per wave
 enum { kLFwd = 0, kLLast = 1, kLBwd = 2 };
 
 // Wc [wout][kx] with the bias column, Wc^T [win][wout], and Z_0 / Z_0^T from the inputs (+ ones
@@ -1008,6 +1014,7 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   __shared__ __attribute__((aligned(16))) float sb[2][kLN * kLLd];
   __shared__ double red[kLThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int wf = wave % kLWF, wr = wave / kLWF;  // the wave's feature group and row group
   int mb, nb;
   if (!lgemm_tile(a, mb, nb)) return;  // uniform, before any barrier
   const LOperands op = lgemm_operands<MODE>(a, l);
@@ -1066,10 +1073,10 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   auto ld = [&](int buf, int s, int kb) {
 #pragma unroll
     for (int i = 0; i < kLTM; ++i)
-      af[s][i] = *reinterpret_cast<const f32x4*>(&sa[buf][((wave * kLTM + i) * 16 + c) * kLLd + kb + 4 * g]);
+      af[s][i] = *reinterpret_cast<const f32x4*>(&sa[buf][((wf * kLTM + i) * 16 + c) * kLLd + kb + 4 * g]);
 #pragma unroll
     for (int j = 0; j < kLTN; ++j)
-      bf[s][j] = *reinterpret_cast<const f32x4*>(&sb[buf][(j * 16 + c) * kLLd + kb + 4 * g]);
+      bf[s][j] = *reinterpret_cast<const f32x4*>(&sb[buf][((wr * kLTN + j) * 16 + c) * kLLd + kb + 4 * g]);
   };
   auto mma = [&](int s) {
 #pragma unroll
@@ -1107,7 +1114,7 @@ __global__ __launch_bounds__(kLThreads) void lgemm_kernel(MArgs a, int l) {
   for (int i = 0; i < kLTM; ++i)
 #pragma unroll
     for (int j = 0; j < kLTN; ++j)
-      *reinterpret_cast<f32x4*>(&tile[(j * 16 + c) * kLTld + (wave * kLTM + i) * 16 + 4 * g]) = acc[i][j];
+      *reinterpret_cast<f32x4*>(&tile[((wr * kLTN + j) * 16 + c) * kLTld + (wf * kLTM + i) * 16 + 4 * g]) = acc[i][j];
   __syncthreads();
   lgemm_epilogue<MODE>(a, l, mb, nb, tile, sb[0], red, in);
 }
