@@ -44,7 +44,7 @@ def main() -> None:
         open(p, "w").write(s.replace(old, new))
 
     def build(src: str) -> None:
-        cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-fvisibility=hidden",
+        cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--offload-compress", "-fvisibility=hidden",
                "-munsafe-fp-atomics", *a.flags.split(), "-c", f"{src}.hip", "-o", f"{src}.o"]
         subprocess.run(cmd, cwd=csrc, check=True)
 
