@@ -781,10 +781,12 @@ __global__ __launch_bounds__(kThreads) void wgrad_rm_kernel(MArgs a) {
 // had two lanes on one bank quad (PMC: 1.4e6 conflict cycles per H = 256 GEMM); 72 is conflict-free
 constexpr int kLM = SMC_LGEMM_M, kLN = SMC_LGEMM_N, kLK = SMC_LGEMM_K, kLLd = kLK + 8;  // tile (features x batch rows), K stage, LDS stride
 #ifndef SMC_LGEMM_THREADS
-#define SMC_LGEMM_THREADS 256
+#define SMC_LGEMM_THREADS 512
 #endif
 // waves: 4 along the features (kLM / 4 each) x kLWR along the batch rows (kLN / kLWR each); kLM = 64: 512
-// workgroups at H = 256 (263 vs 269 us per step with 128)
+// workgroups at H = 256 (263 vs 269 us per step with 128).  8 waves (2 row groups): 4 waves per SIMD at two
+// workgroups per CU, the isolated H = 256 network 237-240 -> 228-230 us against 4 waves
+// (profiles/r04/net/ab_lgemm_waves.txt)
 constexpr int kLThreads = SMC_LGEMM_THREADS;
 constexpr int kLWF = 4, kLWR = kLThreads / 64 / kLWF;
 constexpr int kLTM = kLM / kLWF / 16, kLTN = kLN / kLWR / 16;  // 16 x 16 tiles per wave
