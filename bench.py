@@ -89,6 +89,8 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--lanes", type=int, default=2, choices=[1, 2, 4], help="MC lanes (pricer.mc_lanes): consecutive path launches "
                     "on alternating streams, each starting in the previous one's tail")
     ap.add_argument("--net-cus", type=int, default=32, help="CUs reserved for the network (pricer.network_cus)")
+    ap.add_argument("--net-cus-small", type=int, default=None,
+                    help="pricer.network_cus_small (network CUs beside launches below --net-cu-min-path-steps)")
     ap.add_argument("--net-cu-min-path-steps", type=int, default=None,
                     help="pricer.network_cu_min_path_steps (CU masks only for launches of at least this many path-steps)")
     ap.add_argument("--net-cus-wide", type=int, default=64,
@@ -274,6 +276,8 @@ def main() -> None:
     pricer.network_cus = args.net_cus
     pricer.network_cus_wide = args.net_cus_wide
     pricer.network_cu_pattern = args.net_cu_pattern
+    if args.net_cus_small is not None:
+        pricer.network_cus_small = args.net_cus_small
     if args.net_cu_min_path_steps is not None:
         pricer.network_cu_min_path_steps = args.net_cu_min_path_steps
     if n_assets:

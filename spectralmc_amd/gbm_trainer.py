@@ -431,11 +431,15 @@ class GbmCVNNPricer:
     #: C2/H=256 ~0.26 ms of whole-chip work): more CUs, so the network still hides under the path kernel
     network_cus_wide: int = 64
     network_cu_pattern: str = "low"
-    #: ... only when one path launch does at least this many path-steps (contracts x paths x T): beside a
-    #: short launch the masked network outlasts it (the reference's e2e shape, 3.4e7 path-steps: 0.114
-    #: ms/step unmasked against 0.222 masked; the lock-step shape, 2.7e8: 0.308 masked against 0.329;
-    #: profiles/r04/netcus_small_shapes.jsonl)
+    #: ... when one path launch does at least this many path-steps (contracts x paths x T): beside a
+    #: shorter launch a 32-CU network outlasts it (the reference's e2e shape, 3.4e7 path-steps: 0.222
+    #: ms/step on 32 masked CUs against 0.114 unmasked; the lock-step shape, 2.7e8: 0.308 masked against
+    #: 0.329; profiles/r04/netcus_small_shapes.jsonl)
     network_cu_min_path_steps: int = 1 << 27
+    #: ... and below it this many (0: no masks): beside a short launch half the chip for the network
+    #: (e2e shape: 0.110 ms/step unmasked, 0.141 on 64 CUs, 0.101 on 128, 0.111 on 160;
+    #: profiles/r04/e2e_network_cus.txt)
+    network_cus_small: int = 128
     #: overlap_mc for the rows_kernel + cf_kernel shapes (f64): step s's network part beside step s+1's
     #: rows launch, whose persistent workgroups leave registers and LDS for a network workgroup per CU
     #: at the f64 register budget; False runs those shapes on one stream
@@ -833,8 +837,10 @@ class TrainingSession:
             eng = self.engine
             path_steps = min(getattr(eng, "chunk", 0), getattr(eng, "B", 0)) * getattr(eng, "P", 0) * \
                 getattr(eng, "T", 0)
+            if path_steps < pricer.network_cu_min_path_steps:
+                net_cus = pricer.network_cus_small
             if (net_cus > 0 and getattr(eng, "kernel_name", "") in WHOLE_CONTRACT_KERNELS
-                    and cus >= 2 * net_cus and path_steps >= pricer.network_cu_min_path_steps):
+                    and cus >= 2 * net_cus):
                 # the network on its own CUs beside the path kernels (CU-masked HIP streams); the path
                 # kernel sizes its persistent grid to its stream's CUs (gbm.hip resident_grid).  Only for
                 # the whole-contract resident launch (C2, the lock-step shape) and a fused network: a
