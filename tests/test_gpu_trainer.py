@@ -389,6 +389,34 @@ def test_overlapped_mc_matches_sequential() -> None:
     assert r_s.final_loss == r_o.final_loss and r_s.final_grad_norm == r_o.final_grad_norm
 
 
+def test_overlapped_rows_network_matches_sequential() -> None:
+    """f64 at P = 2048 (rows_kernel + cf_kernel): step s's network part beside step s+1's rows launch
+    (pricer.overlap_rows, the default) == the one-stream step, bit for bit."""
+    def mk(overlap_rows: bool):
+        sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=16, threads_per_block=256,
+                                    mc_seed=7, buffer_size=512, dtype=Precision.float64)
+        model = make_test_cvnn(n_inputs=6, n_outputs=N, seed=123, dtype=torch.float64)
+        cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
+                                   domain_bounds=make_domain_bounds())
+        p = expect_success(GbmCVNNPricer.create(cfg))
+        p.overlap_rows = overlap_rows
+        return p, model
+
+    seq, m_s = mk(False)
+    ovl, m_o = mk(True)
+    cfg = make_training_config(num_batches=6, batch_size=24)
+    s = expect_success(ovl.open_session(cfg))
+    assert s.engine.kernel_name.startswith("rows_kernel") and s.stream is not s.mc_stream
+    s.close()
+    s = expect_success(seq.open_session(cfg))
+    assert s.stream is s.mc_stream
+    s.close()
+    r_s = expect_success(seq.train(cfg))
+    r_o = expect_success(ovl.train(cfg))
+    assert max_param_diff(m_s, m_o) == 0.0
+    assert r_s.final_loss == r_o.final_loss and r_s.final_grad_norm == r_o.final_grad_norm
+
+
 def test_session_step_without_prefetch_then_close() -> None:
     """A session driven step by step (prefetch on every step, one unused) ends consistently."""
     p, m = _pricer()
