@@ -37,12 +37,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(float* p) {
   return __builtin_amdgcn_make_buffer_rsrc(p, static_cast<short>(0), 0x7fffffff, 0x00020000);
 }
 
-// a 256-thread workgroup writes 16 KiB at `p`: 4 dwordx4 per lane, each store instruction 4 KiB contiguous
-template <bool BUFFER>
+// a 256-thread workgroup writes VEC x 4 KiB at `p`: VEC dwordx4 per lane, each store instruction 4 KiB
+// contiguous
+template <bool BUFFER, int VEC = 4>
 __device__ __forceinline__ void piece(float* p, float x) {
   const v4f v = {x, 2.f, 3.f, static_cast<float>(threadIdx.x)};
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < VEC; ++k) {
     if constexpr (BUFFER)
       __builtin_amdgcn_raw_buffer_store_b128(v, rsrc(p), (k * 256 + threadIdx.x) * 16u, 0, 0);
     else
@@ -50,9 +51,9 @@ __device__ __forceinline__ void piece(float* p, float x) {
   }
 }
 
-template <bool BUFFER>
+template <bool BUFFER, int VEC = 4>
 __global__ __launch_bounds__(256) void lin_np(float* out) {
-  piece<BUFFER>(out + static_cast<int64_t>(blockIdx.x) * PIECE, 1.f);
+  piece<BUFFER, VEC>(out + static_cast<int64_t>(blockIdx.x) * (1024 * VEC), 1.f);
 }
 
 __global__ __launch_bounds__(1024) void lin_persist(float* out, int64_t pieces) {
@@ -78,6 +79,28 @@ __global__ __launch_bounds__(256) void rows_np_resident(float* out) {
   const int64_t j = i % 256, t = (i / 256) % T, c = (i / (256 * T)) % CHUNKS, r = i / (256 * T * CHUNKS);
   const int64_t b = r * 256 + j;
   piece<false>(out + (b * T + t) * PITCH + c * PIECE, 1.f);
+}
+
+// 4 KiB pieces (one dwordx4 per lane per block): contract-major and resident order
+__global__ __launch_bounds__(256) void rows_np_contract_v1(float* out) {
+  const int64_t i = blockIdx.x;
+  const int64_t c = i % (P / 1024), t = (i / (P / 1024)) % T, b = i / ((P / 1024) * T);
+  piece<false, 1>(out + (b * T + t) * PITCH + c * 1024, 1.f);
+}
+// resident order at 4 KiB pieces: round r of 256 contracts, 4096-path chunk c, row t, then the 4 pieces of
+// the row chunk, then the 256 contracts
+__global__ __launch_bounds__(256) void rows_np_resident_v1(float* out) {
+  const int64_t i = blockIdx.x;
+  const int64_t j = i % 256, q = (i / 256) % 4, t = (i / 1024) % T, c = (i / (1024 * T)) % CHUNKS,
+                r = i / (1024 * T * CHUNKS);
+  piece<false, 1>(out + ((r * 256 + j) * T + t) * PITCH + c * PIECE + q * 1024, 1.f);
+}
+// resident order with the 4 pieces of a row chunk outermost inside the chunk: (r, c, q, t, j)
+__global__ __launch_bounds__(256) void rows_np_resident_v1b(float* out) {
+  const int64_t i = blockIdx.x;
+  const int64_t j = i % 256, t = (i / 256) % T, q = (i / (256 * T)) % 4, c = (i / (1024 * T)) % CHUNKS,
+                r = i / (1024 * T * CHUNKS);
+  piece<false, 1>(out + ((r * 256 + j) * T + t) * PITCH + c * PIECE + q * 1024, 1.f);
 }
 
 template <class F>
@@ -111,12 +134,17 @@ int main() {
               (long long)PITCH, total / 1e9);
   for (int rep = 0; rep < 2; ++rep) {
     timeit("memset (whole buffer)", [&] { (void)hipMemsetAsync(out, 0, total); });
-    timeit("lin_np_global", [&] { lin_np<false><<<static_cast<unsigned>(lin_pieces), 256>>>(out); });
+    timeit("lin_np_global vec4", [&] { lin_np<false><<<static_cast<unsigned>(lin_pieces), 256>>>(out); });
+    timeit("lin_np_global vec1", [&] { lin_np<false, 1><<<static_cast<unsigned>(4 * lin_pieces), 256>>>(out); });
+    timeit("lin_np_global vec2", [&] { lin_np<false, 2><<<static_cast<unsigned>(2 * lin_pieces), 256>>>(out); });
     timeit("lin_np_buffer", [&] { lin_np<true><<<static_cast<unsigned>(lin_pieces), 256>>>(out); });
     timeit("lin_persist 256x1024", [&] { lin_persist<<<cus, 1024>>>(out, lin_pieces); });
     timeit("lin_persist 512x1024", [&] { lin_persist<<<2 * cus, 1024>>>(out, lin_pieces); });
     timeit("rows_np_contract", [&] { rows_np_contract<<<static_cast<unsigned>(row_pieces), 256>>>(out); });
     timeit("rows_np_resident", [&] { rows_np_resident<<<static_cast<unsigned>(row_pieces), 256>>>(out); });
+    timeit("rows_np_contract_v1", [&] { rows_np_contract_v1<<<static_cast<unsigned>(4 * row_pieces), 256>>>(out); });
+    timeit("rows_np_resident_v1", [&] { rows_np_resident_v1<<<static_cast<unsigned>(4 * row_pieces), 256>>>(out); });
+    timeit("rows_np_resident_v1b", [&] { rows_np_resident_v1b<<<static_cast<unsigned>(4 * row_pieces), 256>>>(out); });
   }
   CK(hipFree(out));
   return 0;
