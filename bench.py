@@ -86,6 +86,8 @@ def parse() -> argparse.Namespace:
                     help="MC part of step s+1 on its own stream beside step s's network part (pricer.overlap_mc)")
     ap.add_argument("--priority", default="network", choices=["network", "mc", "none"],
                     help="stream with the high queue priority (pricer.high_priority_stream)")
+    ap.add_argument("--lanes-long", type=int, default=None,
+                    help="pricer.mc_lanes_long (MC lanes for long path launches beside a narrow network)")
     ap.add_argument("--lanes", type=int, default=2, choices=[1, 2, 4], help="MC lanes (pricer.mc_lanes): consecutive path launches "
                     "on alternating streams, each starting in the previous one's tail")
     ap.add_argument("--net-cus", type=int, default=32, help="CUs reserved for the network (pricer.network_cus)")
@@ -273,6 +275,8 @@ def main() -> None:
     pricer.overlap_rows = args.overlap_rows == "on"
     pricer.high_priority_stream = args.priority
     pricer.mc_lanes = args.lanes
+    if args.lanes_long is not None:
+        pricer.mc_lanes_long = args.lanes_long
     pricer.network_cus = args.net_cus
     pricer.network_cus_wide = args.net_cus_wide
     pricer.network_cu_pattern = args.net_cu_pattern

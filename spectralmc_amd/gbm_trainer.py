@@ -36,6 +36,7 @@ import torch
 from pydantic import BaseModel, ConfigDict, PositiveInt, ValidationError
 
 from . import _lib
+from .cvnn import ComplexLinear
 from .engine import WHOLE_CONTRACT_KERNELS, StepBuffers, TrainingEngine
 from .errors.gbm import EngineFailure, NormalsUnavailable
 from .errors.sampler import SamplerValidationFailed, SequenceExhausted
@@ -423,6 +424,13 @@ class GbmCVNNPricer:
     #: engine allows it (one whole-contract resident launch per step); with the network on its own
     #: CUs (network_cus) C2 runs 3.08 -> 2.98 ms/step
     mc_lanes: int = 2
+    #: ... and this many when the fused network is narrow (every layer input < 128 real features: the
+    #: fb_kernel path on network_cus CUs) and one path launch does at least mc_lanes_long_path_steps
+    #: path-steps: C2 2.957 -> 2.855-2.888 ms/step with 4 lanes; 4 lanes measured slower at the
+    #: lock-step (0.30 -> 0.36-0.38) and e2e shapes and beside the wide C2/H=256 network (3.03 -> 3.07)
+    #: (profiles/r04/mc_lanes.txt)
+    mc_lanes_long: int = 4
+    mc_lanes_long_path_steps: int = 1 << 30
     #: with engine lanes: CUs reserved for the network part (CU-masked HIP streams, the path kernels on
     #: the rest; 0: none) and their choice of CU ids ("low": the lowest logical ids, which measured
     #: best; "spread": evenly over the id range)
@@ -804,9 +812,15 @@ class TrainingSession:
         if factory is not None:
             self.engine = factory(pricer, config.batch_size, dev, rank, world)
         else:
+            lanes = pricer.mc_lanes if pricer.overlap_mc else 1
+            sp = pricer._cfg.sim_params
+            widest_in = max((m.in_features for m in pricer._cvnn.modules() if isinstance(m, ComplexLinear)), default=0)
+            if (lanes > 1 and pricer.fused_network and 0 < widest_in < 128
+                    and config.batch_size * sp.total_paths() * sp.timesteps >= pricer.mc_lanes_long_path_steps):
+                lanes = pricer.mc_lanes_long
             self.engine = TrainingEngine(pricer._cfg, sampler, config.batch_size, model_dtype=pricer._dtype.to_torch(),
                                          device=dev, rank=rank, world_size=world, store_paths=pricer.store_paths,
-                                         math=pricer.math_mode, lanes=pricer.mc_lanes if pricer.overlap_mc else 1)
+                                         math=pricer.math_mode, lanes=lanes)
         self.params = list(pricer._cvnn.parameters())
         self.program = _StepProgram(pricer, self.engine, adam, self.params, ctx)
         self.sobol_skip0 = pricer._sobol_skip
