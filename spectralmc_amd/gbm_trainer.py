@@ -424,12 +424,12 @@ class GbmCVNNPricer:
     #: engine allows it (one whole-contract resident launch per step); with the network on its own
     #: CUs (network_cus) C2 runs 3.08 -> 2.98 ms/step
     mc_lanes: int = 2
-    #: ... and this many when the fused network is narrow (every layer input < 128 real features: the
+    #: ... and this many when the fused network is narrow (every layer input < 128 complex features: the
     #: fb_kernel path on network_cus CUs) and one path launch does at least mc_lanes_long_path_steps
-    #: path-steps: C2 2.957 -> 2.855-2.888 ms/step with 4 lanes; 4 lanes measured slower at the
-    #: lock-step (0.30 -> 0.36-0.38) and e2e shapes and beside the wide C2/H=256 network (3.03 -> 3.07)
-    #: (profiles/r04/mc_lanes.txt)
-    mc_lanes_long: int = 4
+    #: path-steps.  4 lanes at C2 measured 2.855-2.888 against 2.957 ms/step on one box and 2.970-2.974
+    #: against 2.958 on another; slower at the lock-step (0.30 -> 0.36-0.38) and e2e shapes and beside
+    #: the wide C2/H=256 network (3.03 -> 3.07) (profiles/r04/mc_lanes.txt): the default stays 2
+    mc_lanes_long: int = 2
     mc_lanes_long_path_steps: int = 1 << 30
     #: with engine lanes: CUs reserved for the network part (CU-masked HIP streams, the path kernels on
     #: the rest; 0: none) and their choice of CU ids ("low": the lowest logical ids, which measured

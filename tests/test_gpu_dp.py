@@ -6,7 +6,6 @@ and the graphs around the eager all-reduce."""
 from __future__ import annotations
 
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -18,10 +17,10 @@ pytestmark = pytest.mark.gpu
 T, N, M, B_LOCAL, STEPS = 16, 64, 4, 8, 4
 
 
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _rdzv(outdir: str) -> str:
+    """A file rendezvous in the test's own directory: no TCP port to race other processes for (a port
+    picked free and released can be taken again before the ranks bind it)."""
+    return "file://" + os.path.join(outdir, "rdzv")
 
 
 def _train(batch: int, outfile: str, basket: int = 0) -> None:
@@ -57,12 +56,11 @@ def _train(batch: int, outfile: str, basket: int = 0) -> None:
              **{f"p{i}": p.detach().cpu().numpy() for i, p in enumerate(model.parameters())})
 
 
-def _rank(rank: int, world: int, port: int, outdir: str, basket: int) -> None:
+def _rank(rank: int, world: int, outdir: str, basket: int) -> None:
     import torch.distributed as dist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=_rdzv(outdir), rank=rank, world_size=world)
     try:
         _train(B_LOCAL, os.path.join(outdir, f"rank{rank}.npz"), basket)
     finally:
@@ -72,8 +70,7 @@ def _rank(rank: int, world: int, port: int, outdir: str, basket: int) -> None:
 @pytest.mark.parametrize("basket", [0, 4, -1], ids=["single_asset", "basket4", "resident_lanes"])
 def test_two_ranks_match_one_process_with_the_global_batch(tmp_path, basket) -> None:
     ctx = mp.get_context("spawn")
-    port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, str(tmp_path), basket)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, str(tmp_path), basket)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -91,7 +88,7 @@ def test_two_ranks_match_one_process_with_the_global_batch(tmp_path, basket) -> 
             np.testing.assert_allclose(r0[k], s[k], rtol=1e-4, atol=3e-4)
 
 
-def _rccl_single_rank(port: int, outfile: str, shape: int = 0) -> None:
+def _rccl_single_rank(outdir: str, outfile: str, shape: int = 0) -> None:
     """One RCCL rank driving the data-parallel step program: the network half as the two
     captured graphs around the eager RCCL all-reduce on the network stream, Adam as its own
     launch (fuse_adam off) — the path an 8-GPU node takes, minus the other ranks."""
@@ -100,9 +97,10 @@ def _rccl_single_rank(port: int, outfile: str, shape: int = 0) -> None:
     import spectralmc_amd.dp as dp
     import spectralmc_amd.gbm_trainer  # noqa: F401
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    dist.init_process_group("nccl", init_method=_rdzv(outdir), rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
     try:
         assert dist.get_backend() == "nccl"
         flat = torch.arange(7, dtype=torch.float32, device="cuda")
@@ -124,7 +122,7 @@ def test_rccl_step_program_single_rank_equals_plain_run(tmp_path, shape) -> None
     compilation units, equal to f32 rounding (measured: 32 of 192 weights 1 ulp apart after 4
     steps), and the grad norm's partial sums grouped differently."""
     ctx = mp.get_context("spawn")
-    p = ctx.Process(target=_rccl_single_rank, args=(_free_port(), str(tmp_path / "rccl.npz"), shape))
+    p = ctx.Process(target=_rccl_single_rank, args=(str(tmp_path), str(tmp_path / "rccl.npz"), shape))
     p.start()
     p.join(timeout=600)
     assert p.exitcode == 0, f"RCCL rank exited with {p.exitcode}"
