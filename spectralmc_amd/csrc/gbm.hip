@@ -37,8 +37,11 @@ namespace {
 
 // rows_kernel occupancy: 8 waves per SIMD (<= 64 VGPRs) = 4 workgroups per CU, so C2's 4096 contracts
 // are exactly 4 rounds of 1024 persistent workgroups (at 69 VGPRs: 3 per CU, 5.33 rounds)
+// f64: two 8-wave workgroups per CU (4 waves per SIMD) whatever the budget between 4 and 5 waves, and the
+// 4-wave budget (97 VGPRs) measured 8.27-8.28 against 8.34-8.35 ms for rows + cf at 5 (91 VGPRs)
+// (profiles/r04/ab_f64_waves4.txt)
 #ifndef SMC_ROWS_WAVES_F64
-#define SMC_ROWS_WAVES_F64 5
+#define SMC_ROWS_WAVES_F64 4
 #endif
 #ifndef SMC_ROWS_WAVES
 #define SMC_ROWS_WAVES 8
@@ -827,7 +830,7 @@ __global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
 // counter, for workgroups that start late beside a network kernel) cost a store drain per contract at
 // its queue barrier, and rows shapes run the step on one stream anyway (round 4, C2-f64: rows_kernel
 // 7.64 ms with the queue against ~6.9 without).
-// f64 rows run at 5 waves per SIMD (SMC_ROWS_WAVES_F64; round 4 A/Bs on MI355X, C2-f64: v2 math 9.01 ms
+// f64 rows: SMC_ROWS_WAVES_F64 sets the register budget (round 4 A/Bs on MI355X, C2-f64: v2 math 9.01 ms
 // at 6 vs 9.20-9.28 ms at 8 waves, and 9.49-9.53 ms with the CF phase fused into this kernel, which then
 // re-read the terminal row while its own path math waited; v3 math 8.47-8.50 ms at 5 vs 8.65-8.67 ms at
 // 6, where the 80-VGPR budget spilled outside the path loop): the larger register budget is worth more
