@@ -919,7 +919,7 @@ constexpr int kResMaxT = 1 << 16;  // bound on T for the rolled (T != 16) row lo
 
 size_t resident_lds_bytes(int N) {
   return kResTermBytes +
-         (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 9 + 6 * kResPreDraw + 16) * sizeof(double);
+         (static_cast<size_t>(kResWaves) + 3 * static_cast<size_t>(N) + 9 + 6 * kResPreDraw) * sizeof(double);
 }
 
 // Column sums of the whole-contract CF phase (W = 1, round 4): part[G][N] (G = 4096 / N) as a tree
@@ -994,7 +994,6 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
                                           // the exchanged terminal sum, [7] the last-arriver flag,
                                           // [8] the next dynamically handed-out contract;
   double* pre = row + 9;                  // [kResPreDraw][6] Sobol rows of the first static contracts
-  double* pf = pre + 6 * kResPreDraw;     // [2][8]: the next queued contract's Sobol row [0, 6) and index [6]
   for (int j = tid; j < N; j += kResThreads) math::twiddle(j, N, sn[j], cs[j]);
   const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
   const int64_t sob0 = a.sobol ? a.cursor[0] + a.sobol_index0 : 0;
@@ -1009,12 +1008,6 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   const int64_t n_static0 = (a.B / groups) * a.res_static_q / 4 * groups;
   const bool dyn = a.res_queue != nullptr && (W == 1 || n_static0 > 0);
   const int64_t n_static = dyn ? n_static0 : a.B;
-  // one workgroup per contract taking contracts from the queue: wave 0 takes the NEXT contract and draws
-  // its Sobol row right after the current contract's start (its store queue still short), into pf, so
-  // the hand-off at the contract's end is an LDS read instead of a queue atomic and global loads that
-  // wait for wave 0's path stores behind a barrier the other 15 waves wait at
-  const bool pf_on = dyn && W == 1 && a.sobol != nullptr;
-  bool have_pf = false;  // this contract's Sobol row is in pf[(round & 1) * 8]
   auto grab = [&]() -> int64_t {
     if (tid == 0) reinterpret_cast<int64_t*>(row + 8)[0] = n_static + atomicAdd(a.res_queue, 1u);
     lds_barrier();
@@ -1023,13 +1016,7 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
   auto next = [&](int64_t b) -> int64_t {
     if (b + groups < n_static) return b + groups;
     if (!dyn) return a.B;
-    if (W == 1) {
-      if (pf_on) {  // prefetched during this contract (slot of the next round)
-        have_pf = true;
-        return reinterpret_cast<const int64_t*>(pf + ((round + 1) & 1) * 8 + 6)[0];
-      }
-      return grab();
-    }
+    if (W == 1) return grab();
     return reinterpret_cast<const int64_t*>(row + 8)[0];  // learned in this contract's exchange
   };
   // the Sobol rows of the first kResPreDraw static contracts are drawn here, before any path store:
@@ -1056,9 +1043,6 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
     if (a.sobol && static_cast<int64_t>(round) < n_pre) {  // drawn at kernel start
       const double* r = pre + static_cast<int64_t>(round) * 6;
       c = Contract{r[0], r[1], r[2], r[3], r[4], r[5]};
-    } else if (a.sobol && have_pf) {  // drawn during the previous contract
-      const double* r = pf + (round & 1) * 8;
-      c = Contract{r[0], r[1], r[2], r[3], r[4], r[5]};
     } else if (a.sobol) {  // draw the contract (sobol_sampler.py:222-246) instead of a separate kernel
       if (tid < 6) {
         const double v = sobol_coord(a.sobol, a.sobol_dim, tid, static_cast<uint64_t>(sob0 + b), a.lower, a.upper);
@@ -1072,19 +1056,6 @@ __global__ __launch_bounds__(kResThreads) void resident_kernel(EngineArgs a) {
       c = Contract{row[0], row[1], row[2], row[3], row[4], row[5]};
     } else {
       c = load_contract(a.contracts + b * 6);
-    }
-    if (pf_on && b + groups >= n_static && wave == 0) {  // the next hand-off, read back in next(b)
-      int64_t nb = 0;
-      if (lane == 0) nb = n_static + atomicAdd(a.res_queue, 1u);
-      nb = __shfl(nb, 0);
-      double* r = pf + ((round + 1) & 1) * 8;
-      if (lane < 6 && nb < a.B) {
-        const double v = sobol_coord(a.sobol, a.sobol_dim, lane, static_cast<uint64_t>(sob0 + nb), a.lower, a.upper);
-        r[lane] = v;
-        a.contracts_out[nb * 6 + lane] = v;
-        if (a.cvnn_out) a.cvnn_out[nb * 6 + lane] = static_cast<float>(v);
-      }
-      if (lane == 0) reinterpret_cast<int64_t*>(r + 6)[0] = nb;
     }
     const int T = T16 ? kRowBlock : a.T;
     const Stepper<float, LOG_EULER, HW> step(c, T);
