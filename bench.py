@@ -70,9 +70,13 @@ NETWORK_COMPUTE = {"c3": "bf16"}  # default "auto": f32 on the f32 MFMA kernels
 MFMA_PEAK_TFLOPS = {"mfma_bf16": 2516.6, "mfma_f32": 157.3, "valu": 157.3}  # MI355X_MICROARCH.md, dense
 
 
-def parse() -> argparse.Namespace:
+def parse(argv: list[str] | None = None) -> argparse.Namespace:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); N > 1 without a launcher starts the N ranks itself")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1: nccl (= RCCL over xGMI) or gloo (rehearsal: with fewer "
+                         "GPUs than ranks, rank r runs on GPU r mod device_count)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
@@ -102,7 +106,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--kernel-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget for the CPU-baseline sample")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 ON_CHIP_KERNELS = ("resident_kernel", "wave_kernel", "packed_kernel", "basket_resident_kernel")
@@ -225,12 +229,13 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
     return line
 
 
-def main() -> None:
-    args = parse()
+def make_pricer(args: argparse.Namespace, dev):
+    """The pricer of one bench configuration with the bench's step policy (MC lanes, CU-masked network
+    stream, graphs, math mode ...) set from ``args`` (``parse([])`` gives the defaults the driver runs);
+    tests/test_gpu_c2_session.py trains this exact object against the oracle.  Returns (pricer, model)."""
     import torch
-    import torch.distributed as dist
 
-    from spectralmc_amd import _lib, dp
+    from spectralmc_amd.gbm import ForwardNormalization
     from spectralmc_amd.gbm_trainer import GbmCVNNPricer
     from spectralmc_amd.models.numerical import Precision
     from tests.helpers import (
@@ -240,28 +245,16 @@ def main() -> None:
         make_gbm_cvnn_config,
         make_simulation_params,
         make_test_cvnn,
-        make_training_config,
     )
 
-    ctx = dp.init_from_env()
-    world = ctx.world_size if ctx else 1
-    rank = ctx.rank if ctx else 0
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    dev = torch.device("cuda", torch.cuda.current_device())
-
     B, T, N, M, widths, desc = CONFIGS[args.config]
-    P = N * M
     f64 = SIM_DTYPE.get(args.config) == "float64"
-    esz = 8 if f64 else 4
     sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=M, threads_per_block=256,
                                 mc_seed=7, buffer_size=512, dtype=Precision.float64 if f64 else Precision.float32)
     n_assets = BASKET_ASSETS.get(args.config, 0)
     n_inputs = 3 * n_assets + 4 if n_assets else 6
     model = make_test_cvnn(n_inputs=n_inputs, n_outputs=N, seed=123, dtype=torch.float64 if f64 else torch.float32,
                            device=dev, hidden_layers=len(widths), hidden_width=widths[0])
-    from spectralmc_amd.gbm import ForwardNormalization
-
     norm = ForwardNormalization.RAW if args.config in RAW_NORMALIZATION else ForwardNormalization.NORMALIZE
     cfg = make_gbm_cvnn_config(model, sim_params=sp,
                                bs_config=make_black_scholes_config(sim_params=sp, normalization=norm),
@@ -289,6 +282,67 @@ def main() -> None:
 
         use_basket_engine(pricer, BasketConfig(n_assets=n_assets, timesteps=T, network_size=N, batches_per_mc_run=M,
                                                mc_seed=7, math=args.math), store_paths=pricer.store_paths)
+    return pricer, model
+
+
+def launcher_command(argv: list[str], gpus: int, port: int, script: str | None = None) -> list[str]:
+    """The torch.distributed.run command that starts `gpus` ranks of this script with the same arguments
+    (the driver's own form: one node, 127.0.0.1 rendezvous)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__), *argv]
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return int(sk.getsockname()[1])
+
+
+def maybe_launch_ranks(args: argparse.Namespace, argv: list[str], script: str | None = None) -> int | None:
+    """`bench.py --gpus N` (N > 1) started without a launcher (no WORLD_SIZE in the environment): run the
+    N ranks as ONE child process tree through torch.distributed.run and return its exit code.  Called
+    before anything touches the GPU (this process only waits); None when this process is a rank or N = 1."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between processes)
+    return subprocess.call(launcher_command(argv, args.gpus, free_port(), script), env=env)
+
+
+def main() -> None:
+    argv = sys.argv[1:]
+    args = parse(argv)
+    rc = maybe_launch_ranks(args, argv)
+    if rc is not None:
+        sys.exit(rc)
+    import torch
+    import torch.distributed as dist
+
+    from spectralmc_amd import _lib, dp
+    from tests.helpers import expect_success, make_training_config
+
+    if args.backend == "gloo" and "LOCAL_RANK" in os.environ:  # rehearsal: rank r on GPU r mod #GPUs
+        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]) % max(1, torch.cuda.device_count()))
+    ctx = dp.init_from_env(backend=args.backend if int(os.environ.get("WORLD_SIZE", "1")) > 1 else None)
+    world = ctx.world_size if ctx else 1
+    rank = ctx.rank if ctx else 0
+    if world != args.gpus:
+        # a line for another world size than asked would be mislabelled in the driver's scaling table
+        print(f"bench.py: --gpus {args.gpus} but the job has {world} rank(s)", file=sys.stderr)
+        sys.exit(3)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    B, T, N, M, widths, desc = CONFIGS[args.config]
+    P = N * M
+    f64 = SIM_DTYPE.get(args.config) == "float64"
+    esz = 8 if f64 else 4
+    n_assets = BASKET_ASSETS.get(args.config, 0)
+    n_inputs = 3 * n_assets + 4 if n_assets else 6
+    pricer, model = make_pricer(args, dev)
     tcfg = make_training_config(num_batches=args.warmup + args.steps, batch_size=B, learning_rate=1e-2)
     session = expect_success(pricer.open_session(tcfg))
 
@@ -299,6 +353,8 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     session.mc_events = []  # HIP events around each MC-part launch on its stream (timed region)
+    if ctx:
+        session.program.ar_events = []  # ... and around each step's all-reduce on the network stream
     t0 = time.perf_counter()
     for _ in range(args.steps):
         expect_success(session.step())
@@ -312,6 +368,34 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final = session.close()
+
+    # ---- data parallel: the step's one all-reduce (flat [grads..., loss] buffer) -----------------
+    data_parallel = None
+    if ctx:
+        ar = [a.elapsed_time(b_) for a, b_ in (session.program.ar_events or [])]
+        flat = session.program.flat.clone()
+        s_ar = torch.cuda.Stream(device=dev)
+        iters = 20
+        dist.barrier()
+        with torch.cuda.stream(s_ar):
+            ctx.all_reduce_mean(flat)  # warm
+            a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a0.record(s_ar)
+            for _ in range(iters):
+                ctx.all_reduce_mean(flat)
+            a1.record(s_ar)
+        a1.synchronize()
+        iso = torch.tensor([a0.elapsed_time(a1) / iters], dtype=torch.float64, device=dev)
+        dist.all_reduce(iso, op=dist.ReduceOp.MAX)
+        data_parallel = {"backend": args.backend, "world": world,
+                         "rccl_world": world if args.backend == "nccl" else None,
+                         "allreduce_bytes": flat.numel() * flat.element_size(),
+                         "allreduce_per_step": 1,
+                         "allreduce_ms_in_step": (sum(ar) / len(ar)) if ar else None,
+                         "allreduce_ms_isolated": float(iso.item()),
+                         "note": "allreduce_ms_in_step: HIP events around each step's eager all-reduce (sum, then / "
+                                 "world) on the network stream inside the timed region (rank 0); isolated: 20 "
+                                 "back-to-back all-reduces of the same buffer after it, max over ranks"}
 
     # ---- dominant kernel, timed alone with HIP events on its own stream ----------------
     eng = session.engine
@@ -510,6 +594,7 @@ def main() -> None:
                      "measured_stream_gbs": stream_gbs,
                      "frac_of_measured_write": (achieved / stream_gbs["write"]) if "write" in stream_gbs else None},
         "network": network,
+        "data_parallel": data_parallel,
         "final_loss": final.loss,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 11
+#define SMC_ABI_VERSION 12
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -186,8 +186,9 @@ int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32
                                   int32_t dtype, int64_t path_pitch);
 /* Name of the kernel smc_train_step launches for this shape ("resident_kernel",
  * "resident_kernel(sliced)", or smc_train_targets_kernel's name).  Static string.  dtype may carry
- * SMC_QUERY_RAW: the shape's targets use RAW normalisation (one-wave-per-contract shapes). */
-#define SMC_QUERY_RAW 0x100
+ * SMC_QUERY_RAW: the shape's targets use RAW normalisation (one-wave-per-contract shapes); a bit of its
+ * own (ABI 12: it was 0x100, SMC_MATH_HW's bit in smc_normals' dtype). */
+#define SMC_QUERY_RAW 0x1000
 const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
                                   int32_t dtype, int64_t path_pitch);
 /* Workspace bytes smc_train_targets needs for sliced contracts (0: P too small to slice). */

@@ -33,13 +33,13 @@ NORM_RAW = 0
 NORM_NORMALIZE = 1
 DTYPE_F32 = 0
 DTYPE_F64 = 1
-QUERY_RAW = 0x100  # smc_train_step_kernel / smc_train_targets_kernel: the targets use RAW normalisation
+QUERY_RAW = 0x1000  # smc_train_step_kernel / smc_train_targets_kernel: the targets use RAW normalisation
 STORE_TERMINAL = 1
 MATH_HW = 0x100
 TRAIN_DYNAMIC = 0x200
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 

@@ -1453,7 +1453,9 @@ __global__ __launch_bounds__(kWaveThreads) __attribute__((amdgpu_waves_per_eu(4)
 }
 
 bool wave_ok(const EngineArgs& a, bool f32) {
-  return f32 && a.simulate && a.targets && !a.normalize && !a.all_rows && a.slices <= 1 && a.res_slices <= 1 &&
+  // any P (res_slices is ignored: one wave walks the whole contract, so smc_train_step takes it where the
+  // sliced resident kernel would otherwise exchange between workgroups)
+  return f32 && a.simulate && a.targets && !a.normalize && !a.all_rows && a.slices <= 1 &&
          a.T >= 1 && a.T <= kWaveMaxT && a.P % kWaveChunk == 0 && a.N >= kWaveLanePaths &&
          a.N % kWaveLanePaths == 0 && kWaveChunk % a.N == 0 && (a.pitch == 0 || (a.pitch % 4 == 0 && a.pitch >= a.P));
 }

@@ -263,6 +263,9 @@ class _StepProgram:
         self.imag_in = eb.imag_in  # constant zeros
         self.targets = [b.targets for b in self.slots]
         self.mc_graphs: list[torch.cuda.CUDAGraph] = []  # per slot
+        #: when a list: HIP events recorded around each data-parallel all-reduce on the stream that runs it
+        #: (bench.py reports the all-reduce time per step)
+        self.ar_events: list[tuple[torch.cuda.Event, torch.cuda.Event]] | None = None
         self.step_graphs: list[torch.cuda.CUDAGraph] = []  # per slot: MC + network (one stream)
         self.nn_graphs: list[list[torch.cuda.CUDAGraph]] = []  # per slot
         # network half on the fused HIP kernels when the architecture allows (net.py)
@@ -286,7 +289,8 @@ class _StepProgram:
         if lanes > 1:
             # slot k's step runs on lane k % lanes; steps take the lanes in turn because lanes divides
             # SLOTS (GbmCVNNPricer.open_session rejects other values)
-            assert self.SLOTS % lanes == 0
+            if self.SLOTS % lanes:
+                raise ValueError(f"{lanes} MC lanes do not divide the {self.SLOTS} step slots")
             self.engine.enqueue_step(out, lane=slot)
         else:
             self.engine.enqueue_step(out)
@@ -321,8 +325,16 @@ class _StepProgram:
         self.loss.copy_(self.loss_slot[0])
 
     def reduce(self) -> None:
-        if self.dp is not None:
+        if self.dp is None:
+            return
+        if self.ar_events is None:
             self.dp.all_reduce_mean(self.flat)
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        self.dp.all_reduce_mean(self.flat)
+        e1.record()
+        self.ar_events.append((e0, e1))
 
     # -- eager / graph execution ------------------------------------------------------------
     @property
@@ -597,12 +609,13 @@ class GbmCVNNPricer:
         """Set up a device training session (engine buffers, Adam, step program) for ``config``."""
         if isinstance(self._sampler_result, Failure):
             return Failure(SamplerInitFailed(error=self._sampler_result.error))
-        lanes = self.mc_lanes if self.overlap_mc else 1
-        if not isinstance(lanes, int) or lanes < 1 or _StepProgram.SLOTS % lanes:
-            # a lane's device cursor assumes it runs every lanes-th step; the step slots (whose graphs
-            # bind a lane) cycle mod SLOTS, so lanes must divide SLOTS
-            return Failure(InvalidTrainerConfig(
-                message=f"mc_lanes must divide {_StepProgram.SLOTS} (1, 2 or 4), got {lanes!r}"))
+        for name in ("mc_lanes", "mc_lanes_long"):
+            lanes = getattr(self, name) if self.overlap_mc else 1
+            if not isinstance(lanes, int) or lanes < 1 or _StepProgram.SLOTS % lanes:
+                # a lane's device cursor assumes it runs every lanes-th step; the step slots (whose graphs
+                # bind a lane) cycle mod SLOTS, so lanes must divide SLOTS
+                return Failure(InvalidTrainerConfig(
+                    message=f"{name} must divide {_StepProgram.SLOTS} (1, 2 or 4), got {lanes!r}"))
         adam_res = self._make_adam(config.learning_rate)
         if isinstance(adam_res, Failure):
             return adam_res
@@ -851,7 +864,9 @@ class TrainingSession:
             eng = self.engine
             path_steps = min(getattr(eng, "chunk", 0), getattr(eng, "B", 0)) * getattr(eng, "P", 0) * \
                 getattr(eng, "T", 0)
-            if path_steps < pricer.network_cu_min_path_steps:
+            if path_steps < pricer.network_cu_min_path_steps and fused is not None:
+                # (a torch-module network keeps the whole chip: network_cus_small was measured with the fused
+                # network only, profiles/r04/e2e_network_cus.txt)
                 net_cus = pricer.network_cus_small
             if (net_cus > 0 and getattr(eng, "kernel_name", "") in WHOLE_CONTRACT_KERNELS
                     and cus >= 2 * net_cus):

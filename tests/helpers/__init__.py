@@ -127,3 +127,17 @@ __all__ = ["expect_success", "expect_failure", "seed_all_rngs", "make_test_cvnn"
            "max_param_diff", "ThreadsPerBlock", "DEFAULT_TIMESTEPS", "DEFAULT_NETWORK_SIZE",
            "DEFAULT_BATCHES_PER_RUN", "DEFAULT_THREADS_PER_BLOCK", "DEFAULT_MC_SEED", "DEFAULT_BUFFER_SIZE",
            "RTOL_FLOAT32", "ATOL_FLOAT32", "RTOL_FLOAT64", "ATOL_FLOAT64"]
+
+
+def poisoned(shape, dtype: torch.dtype, device) -> torch.Tensor:
+    """An output buffer for a kernel under test, pre-filled with NaN (floating / complex) or a sentinel
+    (integers) instead of ``torch.empty``: the caching allocator often hands a test the block a previous,
+    correct call just filled, so an element a kernel never writes would otherwise pass unseen."""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    if dtype.is_floating_point or dtype.is_complex:
+        return t.fill_(float("nan"))
+    return t.fill_(-0x5A5A5A5A if dtype in (torch.int32, torch.int64) else 0x5A)
+
+
+def poisoned_like(x: torch.Tensor) -> torch.Tensor:
+    return poisoned(x.shape, x.dtype, x.device)

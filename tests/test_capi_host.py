@@ -183,6 +183,13 @@ def test_train_targets_kernel_choice() -> None:
     raw = _lib.QUERY_RAW
     assert L.smc_train_targets_kernel(1, 16, 65536, raw, 66560, 0) == b"wave_kernel"        # lock-step, RAW
     assert L.smc_train_step_kernel(1, 16, 4096, raw, 66560) == b"wave_kernel"
+    # any P: one wave walks the whole contract (P > 65,536 took the sliced resident kernel)
+    assert L.smc_train_step_kernel(1, 16, 8192, raw, L.smc_path_pitch(131072, 0)) == b"wave_kernel"
+    assert L.smc_train_step_kernel(2, 64, 4096, raw, 0) == b"wave_kernel"          # P = 262,144
+    # QUERY_RAW has its own bit: a dtype carrying SMC_MATH_HW is a NORMALIZE query
+    assert _lib.QUERY_RAW & _lib.MATH_HW == 0
+    assert L.smc_train_step_kernel(1, 16, 8192, _lib.MATH_HW, 0) == b"resident_kernel(sliced)"
+    assert L.smc_train_step_kernel(1, 16, 4096, _lib.MATH_HW, 0) == b"resident_kernel"
     assert L.smc_train_targets_kernel(3, 16, 65536, raw, 66560, 0) == b"resident_kernel"    # RAW, T > 2
     assert L.smc_train_targets_kernel(16, 128, 512, 0, 1024, 0) == b"packed_kernel"         # e2e shape, P = 512
     assert L.smc_train_targets_kernel(17, 2048, 65536, 0, 66560, 0) == rows                 # N > 1024, T != 16

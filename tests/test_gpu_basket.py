@@ -24,6 +24,7 @@ from tests.helpers import (
     make_simulation_params,
     make_test_cvnn,
     make_training_config,
+    poisoned,
 )
 
 pytestmark = pytest.mark.gpu
@@ -49,8 +50,8 @@ def test_portable_bit_exact_vs_oracle(oracle, A, T, resident) -> None:
     want_paths, want_sum, want_t = oracle.basket_kernel(c, A, T, 64, 64, cfg.mc_seed, ordinal0=3, want_paths=True,
                                                         wg=wg, slices=W)
     cd = torch.from_numpy(c).to(DEV)
-    paths = torch.empty((B, A, T, cfg.total_paths), dtype=torch.float32, device=DEV)
-    tsum = torch.empty((B, A), dtype=torch.float64, device=DEV)
+    paths = poisoned((B, A, T, cfg.total_paths), torch.float32, DEV)
+    tsum = poisoned((B, A), torch.float64, DEV)
     got = basket_targets(cd, cfg, ordinal0=3, paths=paths, terminal_sum=tsum, resident=resident)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(paths.cpu().numpy(), want_paths)
@@ -72,7 +73,7 @@ def test_resident_sliced_bit_exact(oracle, A, N, M, B) -> None:
     c = _contracts(oracle, cfg, B, skip=3)
     _, want_sum, want = oracle.basket_kernel(c, A, 16, N, M, cfg.mc_seed, ordinal0=5, wg=wg, slices=W)
     cd = torch.from_numpy(c).to(DEV)
-    tsum = torch.empty((B, A), dtype=torch.float64, device=DEV)
+    tsum = poisoned((B, A), torch.float64, DEV)
     got = basket_targets(cd, cfg, ordinal0=5, terminal_sum=tsum)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(tsum.cpu().numpy(), want_sum)
@@ -80,7 +81,7 @@ def test_resident_sliced_bit_exact(oracle, A, N, M, B) -> None:
     # the full path matrix at the padded pitch: same targets, stored rows equal the oracle's
     if B <= 11:
         pitch = int(_lib.lib().smc_path_pitch(cfg.total_paths, 0))
-        paths = torch.empty((B, A, 16, pitch), dtype=torch.float32, device=DEV)
+        paths = poisoned((B, A, 16, pitch), torch.float32, DEV)
         again = basket_targets(cd, cfg, ordinal0=5, paths=paths, pitch=pitch)
         np.testing.assert_array_equal(again.cpu().numpy(), want)
         want_paths, _, _ = oracle.basket_kernel(c[:2], A, 16, N, M, cfg.mc_seed, ordinal0=5, want_paths=True,
@@ -113,8 +114,8 @@ def test_resident_hw_close_to_split_pair(oracle) -> None:
     cfg = BasketConfig(n_assets=4, timesteps=16, network_size=256, batches_per_mc_run=512, math="hw")
     B = 24
     c = torch.from_numpy(_contracts(oracle, cfg, B, skip=9)).to(DEV)
-    t1 = torch.empty((B, 4), dtype=torch.float64, device=DEV)
-    t2 = torch.empty((B, 4), dtype=torch.float64, device=DEV)
+    t1 = poisoned((B, 4), torch.float64, DEV)
+    t2 = poisoned((B, 4), torch.float64, DEV)
     res = basket_targets(c, cfg, terminal_sum=t1).cpu().numpy()
     split = basket_targets(c, cfg, terminal_sum=t2, resident=False).cpu().numpy()
     np.testing.assert_allclose(t1.cpu().numpy(), t2.cpu().numpy(), rtol=1e-12)
@@ -130,14 +131,14 @@ def test_multi_round_and_general_shapes_bit_exact(oracle, A, N, M, B) -> None:
     c = _contracts(oracle, cfg, B, skip=5)
     _, want_sum, want = oracle.basket_kernel(c, A, 4, N, M, cfg.mc_seed, ordinal0=11)
     cd = torch.from_numpy(c).to(DEV)
-    tsum = torch.empty((B, A), dtype=torch.float64, device=DEV)
+    tsum = poisoned((B, A), torch.float64, DEV)
     got = basket_targets(cd, cfg, ordinal0=11, terminal_sum=tsum)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(tsum.cpu().numpy(), want_sum)
     np.testing.assert_array_equal(got.cpu().numpy(), want)
     if B > 600:  # full path matrix, padded pitch
         pitch = int(_lib.lib().smc_path_pitch(cfg.total_paths, 0))
-        paths = torch.empty((B, A, 4, pitch), dtype=torch.float32, device=DEV)
+        paths = poisoned((B, A, 4, pitch), torch.float32, DEV)
         again = basket_targets(cd, cfg, ordinal0=11, paths=paths, pitch=pitch)
         np.testing.assert_array_equal(again.cpu().numpy(), want)
 
@@ -151,7 +152,7 @@ def test_terminal_store_and_padded_pitch_same_targets(oracle) -> None:
     cd = torch.from_numpy(c).to(DEV)
     got_term = basket_targets(cd, cfg)
     pitch = int(_lib.lib().smc_path_pitch(cfg.total_paths, 0))
-    paths = torch.empty((B, 4, 16, pitch), dtype=torch.float32, device=DEV)
+    paths = poisoned((B, 4, 16, pitch), torch.float32, DEV)
     got_all = basket_targets(cd, cfg, paths=paths, pitch=pitch)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(got_term.cpu().numpy(), want)
@@ -166,7 +167,7 @@ def test_hw_math_within_tolerance(oracle) -> None:
     wg, W = oracle.basket_order(4, 16, 256, 64)
     assert W == 4
     _, want_sum, want = oracle.basket_kernel(c, 4, 16, 256, 64, cfg.mc_seed, wg=wg, slices=W)
-    tsum = torch.empty((B, 4), dtype=torch.float64, device=DEV)
+    tsum = poisoned((B, 4), torch.float64, DEV)
     got = basket_targets(torch.from_numpy(c).to(DEV), cfg, terminal_sum=tsum).cpu().numpy()
     np.testing.assert_allclose(tsum.cpu().numpy(), want_sum, rtol=1e-4)
     scale = np.abs(want).max(axis=1, keepdims=True) + 1e-30
@@ -182,7 +183,7 @@ def test_correlation_and_forward_statistics(oracle) -> None:
     X0 = np.array([100.0, 50.0, 10.0])
     row = np.concatenate([[100.0, Tm, r, rho], X0, d, v])
     c = torch.from_numpy(np.tile(row, (2, 1))).to(DEV)
-    paths = torch.empty((2, A, T, cfg.total_paths), dtype=torch.float32, device=DEV)
+    paths = poisoned((2, A, T, cfg.total_paths), torch.float32, DEV)
     basket_targets(c, cfg, paths=paths)
     lr = np.log(paths[0, :, -1, :].double().cpu().numpy() / X0[:, None])
     corr = np.corrcoef(lr)
@@ -220,8 +221,8 @@ def test_chunked_launches_match_single_launch(oracle, M) -> None:
 def test_bad_shapes_fail_loudly() -> None:
     cfg = BasketConfig(n_assets=2, timesteps=4, network_size=64, batches_per_mc_run=32)
     c = torch.zeros((2, cfg.dim), dtype=torch.float64, device=DEV)
-    t = torch.empty((2, 64), dtype=torch.complex64, device=DEV)
-    p = torch.empty((2, 2, 2048), dtype=torch.float32, device=DEV)
+    t = poisoned((2, 64), torch.complex64, DEV)
+    p = poisoned((2, 2, 2048), torch.float32, DEV)
     L = _lib.lib()
     st = L.smc_basket_train_targets(_lib.ptr(c), 2, 9, 4, 64, 32, 7, None, 0, 0, 1, _lib.STORE_TERMINAL,
                                     _lib.ptr(p), 0, 2, None, _lib.ptr(t), None, 0, None)

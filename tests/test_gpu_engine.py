@@ -12,6 +12,7 @@ import torch
 
 from spectralmc_amd import _lib
 from spectralmc_amd.sobol_sampler import SobolEngine, draw_device
+from tests.helpers import poisoned, poisoned_like
 
 pytestmark = pytest.mark.gpu
 
@@ -39,8 +40,8 @@ def test_device_sobol_bit_exact(golden, seed, skip) -> None:
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
     hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
-    out = torch.empty((96, 6), dtype=torch.float64, device=DEV)
-    out32 = torch.empty((96, 6), dtype=torch.float32, device=DEV)
+    out = poisoned((96, 6), torch.float64, DEV)
+    out32 = poisoned((96, 6), torch.float32, DEV)
     idx = torch.tensor([skip], dtype=torch.int64, device=DEV)
     draw_device(tables, 6, idx, 0, 96, lo, hi, out, out32)
     torch.cuda.synchronize()
@@ -56,7 +57,7 @@ def test_device_sobol_far_index_matches_host() -> None:
     tables = torch.from_numpy(SobolEngine(6, 99).tables().view(np.int32)).to(DEV)
     lo = torch.zeros(6, dtype=torch.float64, device=DEV)
     hi = torch.ones(6, dtype=torch.float64, device=DEV)
-    out = torch.empty((1000, 6), dtype=torch.float64, device=DEV)
+    out = poisoned((1000, 6), torch.float64, DEV)
     draw_device(tables, 6, None, start, 1000, lo, hi, out)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), host)
@@ -70,7 +71,7 @@ def test_normals_match_oracle(oracle, dtype, rows) -> None:
     practice).  rows 1, 2: the stream span of small T (4 groups per Philox-seeded stream)."""
     cols = 5003
     tdt = torch.float32 if dtype == "float32" else torch.float64
-    z = torch.empty((rows, cols), dtype=tdt, device=DEV)
+    z = poisoned((rows, cols), tdt, DEV)
     _lib.check(_L().smc_normals(7, 5, rows, cols, 0 if dtype == "float32" else 1, _lib.ptr(z), None))
     torch.cuda.synchronize()
     want = oracle.normals(7, 5, rows, cols, dtype)
@@ -103,8 +104,8 @@ def test_paths_match_oracle(oracle, golden, T, P, scheme, dtype) -> None:
     c[:, 2] = np.minimum(c[:, 2], 3.0)  # keep the extreme-variance corner out of a 1e-5 check
     tdt = torch.float32 if dtype == "float32" else torch.float64
     cd = torch.from_numpy(c).to(DEV)
-    paths = torch.empty((6, T, P), dtype=tdt, device=DEV)
-    rowsum = torch.empty((6, T), dtype=torch.float64, device=DEV)
+    paths = poisoned((6, T, P), tdt, DEV)
+    rowsum = poisoned((6, T), torch.float64, DEV)
     _lib.check(_L().smc_gbm_simulate(_lib.ptr(cd), 6, T, P, 7, None, 3, scheme, 0 if dtype == "float32" else 1,
                                      _lib.ptr(paths), _lib.ptr(rowsum), None))
     torch.cuda.synchronize()
@@ -125,7 +126,7 @@ def test_zero_vol_and_zero_maturity_exact() -> None:
     c = torch.tensor([[100.0, 95.0, 2.0, 0.05, 0.01, 0.0], [50.0, 40.0, 0.0, 0.1, 0.0, 0.7]],
                      dtype=torch.float64, device=DEV)
     T, P = 8, 256
-    paths = torch.empty((2, T, P), dtype=torch.float64, device=DEV)
+    paths = poisoned((2, T, P), torch.float64, DEV)
     _lib.check(_L().smc_gbm_simulate(_lib.ptr(c), 2, T, P, 7, None, 0, 0, 1, _lib.ptr(paths), None, None))
     torch.cuda.synchronize()
     p = paths.cpu().numpy()
@@ -157,9 +158,9 @@ def _run_targets(c: np.ndarray, T: int, N: int, M: int, scheme: int, normalize: 
     chunk = chunk or B
     pitch = pitch or P
     shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
-    paths = torch.empty(shape, dtype=tdt, device=DEV)
-    rowsum = torch.empty((B, T), dtype=torch.float64, device=DEV)
-    tg = torch.empty((B, N), dtype=cdt, device=DEV)
+    paths = poisoned(shape, tdt, DEV)
+    rowsum = poisoned((B, T), torch.float64, DEV)
+    tg = poisoned((B, N), cdt, DEV)
     wsb = int(_L().smc_engine_workspace_bytes(chunk, T, P, int(with_rowsum))) if sliced else 0
     if sliced and workspace is None:
         workspace = torch.zeros(max(wsb, 8), dtype=torch.uint8, device=DEV)
@@ -330,7 +331,7 @@ def test_cf_targets_from_stored_paths_equal_fused(oracle, golden) -> None:
     fused, rowsum, paths = _run_targets(c, T, N, M, 0, 1, "float32", _lib.STORE_ALL)
     cd = torch.from_numpy(c).to(DEV)
     rs = torch.from_numpy(rowsum).to(DEV)
-    tg = torch.empty((7, N), dtype=torch.complex64, device=DEV)
+    tg = poisoned((7, N), torch.complex64, DEV)
     _lib.check(_L().smc_cf_targets(_lib.ptr(cd), 7, T, N, M, 1, 0, _lib.ptr(paths), _lib.ptr(rs), _lib.ptr(tg), None))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(tg.cpu().numpy(), fused)
@@ -371,7 +372,7 @@ def test_hw_math_mode_within_fp32_tolerance(oracle, golden, scheme) -> None:
     got, _, _ = _run_targets(c, 16, 256, 4, scheme, 1, "float32", _lib.STORE_ALL, flags=_lib.MATH_HW)
     want = oracle.training_targets(c, 16, 256, 4, seed=7, scheme=scheme)
     assert _norm_rel(got, want) < 1e-5
-    z = torch.empty((16, 4096), dtype=torch.float32, device=DEV)
+    z = poisoned((16, 4096), torch.float32, DEV)
     _lib.check(_L().smc_normals(7, 3, 16, 4096, _lib.DTYPE_F32 | _lib.MATH_HW, _lib.ptr(z), None))
     torch.cuda.synchronize()
     np.testing.assert_allclose(z.cpu().numpy(), oracle.normals(7, 3, 16, 4096), rtol=0, atol=2e-5)
@@ -441,7 +442,7 @@ def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store, ch
     hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
     pitch = int(L.smc_path_pitch(P, 0))
     shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
-    paths = torch.empty(shape, dtype=torch.float32, device=DEV)
+    paths = poisoned(shape, torch.float32, DEV)
     scheme = _lib.SCHEME_LOG_EULER | math
     offset, adv = B, 2 * B  # rank 1 of 2
     cur_a = torch.tensor([100, 50], dtype=torch.int64, device=DEV)
@@ -449,16 +450,16 @@ def test_train_step_equals_draw_then_targets(golden, B, T, N, M, math, store, ch
     sync, nsync = _sync(L, T, N, M, pitch)
     assert nsync == 128  # whole-contract shapes: done counter, status word, contract queue
     for _ in range(3):
-        ca = torch.empty((B, 6), dtype=torch.float64, device=DEV)
-        fa = torch.empty((B, 6), dtype=torch.float32, device=DEV)
-        ta = torch.empty((B, N), dtype=torch.complex64, device=DEV)
+        ca = poisoned((B, 6), torch.float64, DEV)
+        fa = poisoned((B, 6), torch.float32, DEV)
+        ta = poisoned((B, N), torch.complex64, DEV)
         _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur_a), offset, adv,
                                     _lib.ptr(ca), _lib.ptr(fa), B, T, N, M, 7, scheme, _lib.NORM_NORMALIZE,
                                     _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, chunk, _lib.ptr(ta),
                                     _lib.ptr(sync), nsync, None))
-        cb = torch.empty_like(ca)
-        fb = torch.empty_like(fa)
-        tb = torch.empty_like(ta)
+        cb = poisoned_like(ca)
+        fb = poisoned_like(fa)
+        tb = poisoned_like(ta)
         draw_device(tables, 6, cur_b[0:1], offset, B, lo, hi, cb, fb)
         _lib.check(L.smc_train_targets(_lib.ptr(cb), B, T, N, M, 7, _lib.ptr(cur_b[1:2]), offset, scheme,
                                        _lib.NORM_NORMALIZE, _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, chunk,
@@ -498,21 +499,21 @@ def test_rows_train_step_equals_targets(golden, B, T, N, M, dtype, store, chunk)
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
     hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
     shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
-    paths = torch.empty(shape, dtype=torch.float64 if f64 else torch.float32, device=DEV)
+    paths = poisoned(shape, torch.float64 if f64 else torch.float32, DEV)
     ctype = torch.complex128 if f64 else torch.complex64
     cur_a = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
     cur_b = cur_a.clone()
     nsync = int(L.smc_train_step_sync_bytes(T, N, M, dtype, pitch))
     sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
     for _ in range(3):
-        ca = torch.empty((B, 6), dtype=torch.float64, device=DEV)
-        fa = torch.empty((B, 6), dtype=torch.float32, device=DEV)
-        ta = torch.empty((B, N), dtype=ctype, device=DEV)
+        ca = poisoned((B, 6), torch.float64, DEV)
+        fa = poisoned((B, 6), torch.float32, DEV)
+        ta = poisoned((B, N), ctype, DEV)
         _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur_a), 0, B,
                                     _lib.ptr(ca), _lib.ptr(fa), B, T, N, M, 7, _lib.SCHEME_LOG_EULER | _lib.MATH_HW,
                                     _lib.NORM_NORMALIZE, dtype, store, _lib.ptr(paths), pitch, chunk, _lib.ptr(ta),
                                     _lib.ptr(sync), nsync, None))
-        tb = torch.empty_like(ta)
+        tb = poisoned_like(ta)
         _lib.check(L.smc_train_targets(_lib.ptr(ca), B, T, N, M, 7, _lib.ptr(cur_b[1:2]), 0,
                                        _lib.SCHEME_LOG_EULER | _lib.MATH_HW, _lib.NORM_NORMALIZE, dtype, store,
                                        _lib.ptr(paths), pitch, chunk, None, _lib.ptr(tb), None, 0, None))
@@ -541,13 +542,13 @@ def test_c2_f64_timed_call_matches_oracle(oracle, golden) -> None:
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
     hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
-    paths = torch.empty((B, T, pitch), dtype=torch.float64, device=DEV)
+    paths = poisoned((B, T, pitch), torch.float64, DEV)
     cur = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
     nsync = int(L.smc_train_step_sync_bytes(T, N, M, dtype, pitch))
     sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
     for step in range(2):
-        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
-        t = torch.empty((B, N), dtype=torch.complex128, device=DEV)
+        c = poisoned((B, 6), torch.float64, DEV)
+        t = poisoned((B, N), torch.complex128, DEV)
         _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
                                     _lib.ptr(c), None, B, T, N, M, 7, _lib.SCHEME_LOG_EULER | _lib.MATH_HW,
                                     _lib.NORM_NORMALIZE, dtype, _lib.STORE_ALL, _lib.ptr(paths), pitch, B,
@@ -566,16 +567,17 @@ def test_c2_f64_timed_call_matches_oracle(oracle, golden) -> None:
             assert _norm_rel(got[k:k + 1], want) < 1e-10, (step, b)
 
 
-PACKED_CASES = [  # (B, T, N, M, normalize, store): P < 4096 -> packed_kernel, K = 4096 / P contracts per workgroup
-    (4096, 16, 128, 4, 1, _lib.STORE_ALL),       # the reference's e2e shape (P = 512, K = 8) at a full batch
-    (1001, 16, 64, 4, 1, _lib.STORE_ALL),        # P = 256 (K = 16, one wave per contract), ragged last group
-    (300, 5, 256, 8, 0, _lib.STORE_TERMINAL),    # P = 2048 (K = 2), odd T (rolled rows), RAW, terminal rows
-    (77, 1, 16, 64, 1, _lib.STORE_ALL),          # T = 1, N = 16, P = 1024
+PACKED_CASES = [  # (B, T, N, M, normalize, store, chunk): P < 4096 -> packed_kernel, K = 4096 / P per workgroup
+    (4096, 16, 128, 4, 1, _lib.STORE_ALL, None),    # the reference's e2e shape (P = 512, K = 8) at a full batch
+    (1001, 16, 64, 4, 1, _lib.STORE_ALL, None),     # P = 256 (K = 16, one wave per contract), ragged last group
+    (300, 5, 256, 8, 0, _lib.STORE_TERMINAL, None),  # P = 2048 (K = 2), odd T (rolled rows), RAW, terminal rows
+    (77, 1, 16, 64, 1, _lib.STORE_ALL, None),       # T = 1, N = 16, P = 1024
+    (1000, 16, 128, 4, 1, _lib.STORE_ALL, 334),     # e2e shape in 3 chunk launches (ragged last: 332)
 ]
 
 
-@pytest.mark.parametrize("B,T,N,M,normalize,store", PACKED_CASES)
-def test_packed_train_step_matches_oracle(oracle, golden, B, T, N, M, normalize, store) -> None:
+@pytest.mark.parametrize("B,T,N,M,normalize,store,chunk", PACKED_CASES)
+def test_packed_train_step_matches_oracle(oracle, golden, B, T, N, M, normalize, store, chunk) -> None:
     """Small P: smc_train_step runs K = 4096 / P whole contracts per 1024-thread
     workgroup (packed_kernel, Sobol draw and cursor advance fused).  Portable math bit-exact with the
     kernel-mode oracle in the packed order (one chunk of P / 4 lanes per contract: oracle.engine_wg);
@@ -590,20 +592,21 @@ def test_packed_train_step_matches_oracle(oracle, golden, B, T, N, M, normalize,
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
     hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
-    shape = (B, T, pitch) if store == _lib.STORE_ALL else (B, pitch)
-    paths = torch.empty(shape, dtype=torch.float32, device=DEV)
+    chunk = chunk or B  # chunk < B: several launches (per-chunk Sobol index and ordinal, last one advances)
+    shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
+    paths = poisoned(shape, torch.float32, DEV)
     nsync = int(L.smc_train_step_sync_bytes(T, N, M, 0, pitch))
     sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
     norm = _lib.NORM_NORMALIZE if normalize else _lib.NORM_RAW
     for math in (0, _lib.MATH_HW):
         cur = torch.tensor([40, 9], dtype=torch.int64, device=DEV)
-        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
-        f = torch.empty((B, 6), dtype=torch.float32, device=DEV)
+        c = poisoned((B, 6), torch.float64, DEV)
+        f = poisoned((B, 6), torch.float32, DEV)
         t = torch.full((B, N), float("nan"), dtype=torch.complex64, device=DEV)
         _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
                                     _lib.ptr(c), _lib.ptr(f), B, T, N, M, 7, _lib.SCHEME_LOG_EULER | math, norm,
-                                    _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, B, _lib.ptr(t), _lib.ptr(sync),
-                                    nsync, None))
+                                    _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, chunk, _lib.ptr(t),
+                                    _lib.ptr(sync), nsync, None))
         torch.cuda.synchronize()
         assert cur.tolist() == [40 + B, 9 + B]
         assert not sync.view(torch.int32).any()
@@ -616,24 +619,28 @@ def test_packed_train_step_matches_oracle(oracle, golden, B, T, N, M, normalize,
             kt, _ = oracle.kernel_targets(contracts, T, N, M, seed=7, ordinal0=9, normalize=bool(normalize),
                                           wg=P // 4)
             np.testing.assert_array_equal(got, kt)
-            if store == _lib.STORE_ALL:  # the stored rows are the kernel-mode paths
-                kp, _, _ = oracle.kernel_paths(contracts[:3], T, P, 7, ordinal0=9, want_paths=True, wg=P // 4)
-                np.testing.assert_array_equal(paths[:3, :, :P].cpu().numpy(), kp)
+            if store == _lib.STORE_ALL:  # the stored rows (the last chunk's) are the kernel-mode paths
+                b0 = (B - 1) // chunk * chunk
+                kp, _, _ = oracle.kernel_paths(contracts[b0:b0 + 3], T, P, 7, ordinal0=9 + b0, want_paths=True,
+                                               wg=P // 4)
+                np.testing.assert_array_equal(paths[:len(kp), :, :P].cpu().numpy(), kp)
         else:
             want = oracle.training_targets(contracts[:24], T, N, M, seed=7, ordinal0=9, normalize=bool(normalize))
             assert _norm_rel(got[:24], want) < 1e-5
 
 
-WAVE_CASES = [  # (B, T, N, M, store): RAW, T <= 2 -> wave_kernel, one wave per contract
-    (4096, 1, 16, 4096, _lib.STORE_ALL),      # the reference's lock-step shape at C2's batch (bench "lockstep")
-    (333, 2, 64, 64, _lib.STORE_ALL),          # T = 2: 8 draws per group, 4 groups per stream span
-    (5000, 1, 256, 16, _lib.STORE_TERMINAL),   # more contracts than resident waves: two rounds; N = 256
-    (70, 2, 1024, 2, _lib.STORE_TERMINAL),     # N = 1024: one batch row per chunk
+WAVE_CASES = [  # (B, T, N, M, store, chunk): RAW, T <= 2 -> wave_kernel, one wave per contract
+    (4096, 1, 16, 4096, _lib.STORE_ALL, None),      # the reference's lock-step shape at C2's batch (bench "lockstep")
+    (333, 2, 64, 64, _lib.STORE_ALL, None),          # T = 2: 8 draws per group, 4 groups per stream span
+    (5000, 1, 256, 16, _lib.STORE_TERMINAL, None),   # more contracts than resident waves: two rounds; N = 256
+    (70, 2, 1024, 2, _lib.STORE_TERMINAL, None),     # N = 1024: one batch row per chunk
+    (333, 2, 64, 64, _lib.STORE_ALL, 130),           # three chunk launches (ragged last: 73)
+    (40, 1, 16, 8192, _lib.STORE_TERMINAL, None),    # P = 131,072 > 65,536: still one wave (not the sliced kernel)
 ]
 
 
-@pytest.mark.parametrize("B,T,N,M,store", WAVE_CASES)
-def test_wave_train_step_matches_oracle(oracle, golden, B, T, N, M, store) -> None:
+@pytest.mark.parametrize("B,T,N,M,store,chunk", WAVE_CASES)
+def test_wave_train_step_matches_oracle(oracle, golden, B, T, N, M, store, chunk) -> None:
     """RAW targets at T <= 2 (the reference's lock-step trainer shape, tests/test_gbm_trainer.py:122-142):
     smc_train_step runs one wave per contract (wave_kernel: 16 paths = one stream span per lane,
     payoffs added as the chunks finish, the M-mean and FFT by the wave alone).  Portable math bit-exact
@@ -649,18 +656,19 @@ def test_wave_train_step_matches_oracle(oracle, golden, B, T, N, M, store) -> No
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
     hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
-    shape = (B, T, pitch) if store == _lib.STORE_ALL else (B, pitch)
-    paths = torch.empty(shape, dtype=torch.float32, device=DEV)
+    chunk = chunk or B  # chunk < B: several launches (per-chunk Sobol index and ordinal, last one advances)
+    shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
+    paths = poisoned(shape, torch.float32, DEV)
     nsync = int(L.smc_train_step_sync_bytes(T, N, M, 0, pitch))
     sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
     for math in (0, _lib.MATH_HW):
         cur = torch.tensor([17, 3], dtype=torch.int64, device=DEV)
-        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
-        f = torch.empty((B, 6), dtype=torch.float32, device=DEV)
+        c = poisoned((B, 6), torch.float64, DEV)
+        f = poisoned((B, 6), torch.float32, DEV)
         t = torch.full((B, N), float("nan"), dtype=torch.complex64, device=DEV)
         _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
                                     _lib.ptr(c), _lib.ptr(f), B, T, N, M, 43, _lib.SCHEME_LOG_EULER | math,
-                                    _lib.NORM_RAW, _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, B, _lib.ptr(t),
+                                    _lib.NORM_RAW, _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, chunk, _lib.ptr(t),
                                     _lib.ptr(sync), nsync, None))
         torch.cuda.synchronize()
         assert cur.tolist() == [17 + B, 3 + B]
@@ -675,7 +683,8 @@ def test_wave_train_step_matches_oracle(oracle, golden, B, T, N, M, store) -> No
                 kt, _ = oracle.kernel_targets(contracts[b:b + 1], T, N, M, seed=43, ordinal0=3 + int(b),
                                               normalize=False, wg=256)
                 np.testing.assert_array_equal(got[b:b + 1], kt)
-            kp, _, _ = oracle.kernel_paths(contracts[:2], T, P, 43, ordinal0=3, want_paths=True, wg=256)
+            b0 = (B - 1) // chunk * chunk  # the scratch holds the last chunk's rows
+            kp, _, _ = oracle.kernel_paths(contracts[b0:b0 + 2], T, P, 43, ordinal0=3 + b0, want_paths=True, wg=256)
             if store == _lib.STORE_ALL:
                 np.testing.assert_array_equal(paths[:2, :, :P].cpu().numpy(), kp)
             else:
@@ -714,21 +723,21 @@ def test_sliced_train_step_bit_exact(oracle, golden, B, N, M, store, chunk) -> N
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
     hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
     shape = (chunk, T, pitch) if store == _lib.STORE_ALL else (chunk, pitch)
-    paths = torch.empty(shape, dtype=torch.float32, device=DEV)
+    paths = poisoned(shape, torch.float32, DEV)
     sync, nsync = _sync(L, T, N, M, pitch)
     assert nsync > 4
     start = [40, 9]
     for math in (0, _lib.MATH_HW):
         cur = torch.tensor(start, dtype=torch.int64, device=DEV)
-        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
-        f = torch.empty((B, 6), dtype=torch.float32, device=DEV)
+        c = poisoned((B, 6), torch.float64, DEV)
+        f = poisoned((B, 6), torch.float32, DEV)
         t = torch.full((B, N), float("nan"), dtype=torch.complex64, device=DEV)
         _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
                                     _lib.ptr(c), _lib.ptr(f), B, T, N, M, 7, _lib.SCHEME_LOG_EULER | math,
                                     _lib.NORM_NORMALIZE, _lib.DTYPE_F32, store, _lib.ptr(paths), pitch, chunk,
                                     _lib.ptr(t), _lib.ptr(sync), nsync, None))
-        cb = torch.empty_like(c)
-        fb = torch.empty_like(f)
+        cb = poisoned_like(c)
+        fb = poisoned_like(f)
         draw_device(tables, 6, torch.tensor(start[:1], dtype=torch.int64, device=DEV), 0, B, lo, hi, cb, fb)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(c.cpu().numpy(), cb.cpu().numpy())
@@ -769,11 +778,11 @@ def test_exchange_timeout_sets_status_not_silent_nan(oracle, golden) -> None:
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
     lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
     hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
-    paths = torch.empty((B, pitch), dtype=torch.float32, device=DEV)
+    paths = poisoned((B, pitch), torch.float32, DEV)
     sync, nsync = _sync(L, T, N, M, pitch)
 
     def step(cur):
-        c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
+        c = poisoned((B, 6), torch.float64, DEV)
         t = torch.zeros((B, N), dtype=torch.complex64, device=DEV)
         _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
                                     _lib.ptr(c), None, B, T, N, M, 7, _lib.SCHEME_LOG_EULER, _lib.NORM_NORMALIZE,

@@ -21,6 +21,7 @@ import pytest
 import torch
 
 from spectralmc_amd import _lib
+from tests.helpers import poisoned
 from tests.test_reference_fixtures import CASE_NAMES, per_contract_rel, unpack
 
 pytestmark = pytest.mark.gpu
@@ -45,8 +46,8 @@ def train_targets(contracts: np.ndarray, m: dict, *, hw: bool, padded: bool = Tr
     f32 = m["dtype"] == "float32"
     dcode = _lib.DTYPE_F32 if f32 else _lib.DTYPE_F64
     pitch = int(_lib.lib().smc_path_pitch(P, dcode)) if padded else P
-    paths = torch.empty((B, T, pitch), dtype=torch.float32 if f32 else torch.float64, device=DEV)
-    tg = torch.empty((B, N), dtype=torch.complex64 if f32 else torch.complex128, device=DEV)
+    paths = poisoned((B, T, pitch), torch.float32 if f32 else torch.float64, DEV)
+    tg = poisoned((B, N), torch.complex64 if f32 else torch.complex128, DEV)
     cd = torch.from_numpy(np.ascontiguousarray(contracts)).to(DEV)
     scheme = m["scheme"] | (_lib.MATH_HW if hw else 0)
     _lib.check(_lib.lib().smc_train_targets(
@@ -124,15 +125,15 @@ def test_c2_timed_call_train_step(oracle, gbm_golden) -> None:
     eng = SobolEngine(6, 7, 0)
     tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
     lo_d, hi_d = torch.from_numpy(lo).to(DEV), torch.from_numpy(hi).to(DEV)
-    paths = torch.empty((B, T, pitch), dtype=torch.float32, device=DEV)
+    paths = poisoned((B, T, pitch), torch.float32, DEV)
     nsync = int(L.smc_train_step_sync_bytes(T, N, M, 0, pitch))
     sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
     for math in (_lib.MATH_HW, 0):
         cur = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
         for step in range(2):
-            c = torch.empty((B, 6), dtype=torch.float64, device=DEV)
-            f = torch.empty((B, 6), dtype=torch.float32, device=DEV)
-            t = torch.empty((B, N), dtype=torch.complex64, device=DEV)
+            c = poisoned((B, 6), torch.float64, DEV)
+            f = poisoned((B, 6), torch.float32, DEV)
+            t = poisoned((B, N), torch.complex64, DEV)
             _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo_d), _lib.ptr(hi_d), _lib.ptr(cur), 0, B,
                                         _lib.ptr(c), _lib.ptr(f), B, T, N, M, 7, _lib.SCHEME_LOG_EULER | math,
                                         _lib.NORM_NORMALIZE, _lib.DTYPE_F32, _lib.STORE_ALL, _lib.ptr(paths), pitch,

@@ -571,3 +571,16 @@ def test_mc_lanes_must_divide_the_step_slots() -> None:
     p.mc_lanes = 3
     res = p.open_session(make_training_config(num_batches=2, batch_size=16))
     assert isinstance(res, Failure) and "mc_lanes" in res.error.message
+
+
+@pytest.mark.parametrize("field", ["mc_lanes", "mc_lanes_long"])
+def test_lane_counts_that_do_not_divide_the_slots_are_rejected(field) -> None:
+    """Both lane settings are validated when the session opens (mc_lanes_long was checked only by
+    an assert inside the step program)."""
+    from spectralmc.errors.trainer import InvalidTrainerConfig
+
+    p, _ = _pricer()
+    setattr(p, field, 3)
+    res = p.open_session(make_training_config(num_batches=1, batch_size=8))
+    assert isinstance(res, Failure) and isinstance(res.error, InvalidTrainerConfig)
+    assert field in res.error.message
