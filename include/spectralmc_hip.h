@@ -275,7 +275,9 @@ typedef struct smc_adam_args {
   void* exp_avg_sq;
   float* step;
   double lr, beta1, beta2, eps, weight_decay;
-  double* norm_partials;         /* [smc_adam_norm_partials(n_params)] scratch          */
+  double* norm_partials;         /* [smc_adam_norm_partials(n_params)] scratch, ZEROED before
+                                    the first call (its last slot is the fused finalize's
+                                    arrival counter; every call leaves it zero)            */
   void* grad_norm;               /* scalar out: ||grad||_2 (gbm_trainer.py:834)         */
   void* loss;                    /* scalar out: grads[n_params] (the loss slot)         */
 } smc_adam_args;
@@ -290,12 +292,14 @@ int32_t smc_cvnn_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers
                                   const void* input_im, const void* targets, int64_t batch,
                                   void* partials, int64_t partial_blocks, void* stream);
 /* grads[0..n_params] = fixed-order sum of the partials (last entry: loss).  With adam != NULL
- * the Adam update, grad norm, loss copy and step increment follow in the same call. */
+ * the Adam update, grad norm, loss copy and step increment follow in the same launch (the last
+ * workgroup to finish takes the grad norm, loss and step: one kernel, ABI 12). */
 int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t partial_blocks,
                               int64_t n_params, void* grads, const smc_adam_args* adam, void* stream);
 /* Adam update from an already reduced (e.g. all-reduced) grads[0..n_params]. */
 int32_t smc_adam_step(int32_t dtype, int64_t n_params, const void* grads, const smc_adam_args* adam,
                       void* stream);
+/* f64 entries of smc_adam_args.norm_partials: one per 64 gradient entries + the arrival counter. */
 int64_t smc_adam_norm_partials(int64_t n_params);
 
 /* ---- the same network step on the matrix cores (csrc/cvnn_mfma.hip) ---------

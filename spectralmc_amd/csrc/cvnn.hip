@@ -18,7 +18,8 @@
 //     gradient buffer [n_params + 1]; with SMC Adam arguments it also applies the Adam update
 //     (fused, single process) and per-block partial sums of g^2.
 //   * adam_kernel: the same update from an already reduced (all-reduced) gradient buffer.
-//   * finalize_kernel: grad norm from the block partials (fixed order), loss, step += 1.
+//   * the last workgroup of either (an arrival counter) takes the grad norm from the block partials (fixed
+//     order), the loss and step += 1 (round 4 and before: a separate finalize_kernel launch).
 // Weights stay in HBM/L2 (tens of KB for the benchmark network); parameters, gradients and
 // Adam moments are single flat buffers whose layout is the model's parameter order.
 
@@ -365,9 +366,12 @@ struct AdamArgs {
   void* params;
   void* exp_avg;
   void* exp_avg_sq;
-  const float* step;  // torch's capturable step counter before this update
+  float* step;  // torch's capturable step counter before this update (the last workgroup increments it)
   double lr, beta1, beta2, eps, weight_decay;
-  double* norm_partials;  // [gridDim] sums of g^2
+  double* norm_partials;  // [gridDim] sums of g^2, then (at norm_slots - 1) the arrival counter
+  int64_t norm_slots;     // smc_adam_norm_partials(n_params)
+  void* grad_norm;        // scalar out
+  void* loss;             // scalar out: grads[n_params]
 };
 
 template <typename Real>
@@ -393,6 +397,38 @@ __device__ __forceinline__ void adam_update(const AdamArgs& ad, int64_t p, Real 
 // so every load instruction reads 64 consecutive entries); slices are added in order.
 constexpr int kReduceCols = 64;
 constexpr int kReduceSlices = kNetThreads / kReduceCols;
+
+// The update's tail, fused (round 5: it was a separate one-workgroup finalize_kernel launch): every workgroup has
+// written its g^2 partial; the last one to arrive on the counter (the final slot of norm_partials, zero between
+// launches) adds the partials in index order (finalize_kernel's order: thread stride, then block_sum), writes the
+// grad norm and the loss, increments Adam's step and resets the counter.  Every workgroup read the step before
+// it arrived.  Release: each thread's agent-scope fence after its stores; acquire: after the counter.
+template <typename Real>
+__device__ __forceinline__ void adam_finalize_last(const AdamArgs& ad, int64_t n_partials, const Real* grads,
+                                                   int64_t n_params, double* red) {
+  __shared__ int last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(ad.norm_partials + (ad.norm_slots - 1));
+    last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  double sum = 0.0;
+  for (int64_t i = threadIdx.x; i < n_partials; i += kNetThreads)
+    sum += __hip_atomic_load(ad.norm_partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double t = block_sum<double>(sum, red);
+  if (threadIdx.x == 0) {
+    *static_cast<Real*>(ad.grad_norm) = static_cast<Real>(sqrt(t));
+    *static_cast<Real*>(ad.loss) =
+        __hip_atomic_load(const_cast<Real*>(grads) + n_params, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *ad.step = *ad.step + 1.0f;
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(ad.norm_partials + (ad.norm_slots - 1)), 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 template <typename Real, bool ADAM>
 __global__ __launch_bounds__(kNetThreads) void reduce_kernel(const Real* __restrict__ partials, int64_t blocks,
@@ -428,6 +464,7 @@ __global__ __launch_bounds__(kNetThreads) void reduce_kernel(const Real* __restr
   if (ADAM) {
     const double t = block_sum<double>(sq, red);
     if (threadIdx.x == 0) ad.norm_partials[blockIdx.x] = t;
+    adam_finalize_last<Real>(ad, gridDim.x, grads, n_params, red);
   }
 }
 
@@ -444,22 +481,7 @@ __global__ __launch_bounds__(kNetThreads) void adam_kernel(const Real* __restric
   }
   const double t = block_sum<double>(sq, red);
   if (threadIdx.x == 0) ad.norm_partials[blockIdx.x] = t;
-}
-
-template <typename Real>
-__global__ __launch_bounds__(kNetThreads) void finalize_kernel(const double* __restrict__ norm_partials,
-                                                               int64_t n_partials, const Real* __restrict__ grads,
-                                                               int64_t n_params, float* step, Real* grad_norm,
-                                                               Real* loss) {
-  __shared__ double red[kNetThreads / 64];
-  double s = 0.0;
-  for (int64_t i = threadIdx.x; i < n_partials; i += kNetThreads) s += norm_partials[i];
-  const double t = block_sum<double>(s, red);
-  if (threadIdx.x == 0) {
-    *grad_norm = static_cast<Real>(sqrt(t));
-    *loss = grads[n_params];
-    *step = *step + 1.0f;
-  }
+  adam_finalize_last<Real>(ad, gridDim.x, grads, n_params, red);
 }
 
 bool layers_valid(const smc_cvnn_layer* layers, int32_t n_layers, int64_t n_params) {
@@ -571,7 +593,7 @@ int32_t smc_cvnn_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers
   return check_launch("cvnn forward_backward_kernel");
 }
 
-static AdamArgs to_adam(const smc_adam_args* ad) {
+static AdamArgs to_adam(const smc_adam_args* ad, int64_t n_params) {
   AdamArgs a{};
   a.params = ad->params;
   a.exp_avg = ad->exp_avg;
@@ -583,6 +605,9 @@ static AdamArgs to_adam(const smc_adam_args* ad) {
   a.eps = ad->eps;
   a.weight_decay = ad->weight_decay;
   a.norm_partials = ad->norm_partials;
+  a.norm_slots = smc_adam_norm_partials(n_params);
+  a.grad_norm = ad->grad_norm;
+  a.loss = ad->loss;
   return a;
 }
 
@@ -591,7 +616,10 @@ static bool adam_valid(const smc_adam_args* ad) {
          ad->loss && ad->lr > 0.0 && ad->beta1 >= 0.0 && ad->beta1 < 1.0 && ad->beta2 >= 0.0 && ad->beta2 < 1.0;
 }
 
-int64_t smc_adam_norm_partials(int64_t n_params) { return (n_params + 1 + kReduceCols - 1) / kReduceCols; }
+// g^2 partials of reduce_kernel (one per 64 gradient entries; adam_kernel's fewer) + the arrival counter of the
+// fused finalize (zero before the first call; the last workgroup leaves it zero)
+static int64_t reduce_blocks(int64_t n_params) { return (n_params + 1 + kReduceCols - 1) / kReduceCols; }
+int64_t smc_adam_norm_partials(int64_t n_params) { return reduce_blocks(n_params) + 1; }
 
 int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t partial_blocks, int64_t n_params,
                               void* grads, const smc_adam_args* adam, void* stream) {
@@ -600,8 +628,8 @@ int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t parti
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_reduce_grads: bad argument");
   if (adam && !adam_valid(adam)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_reduce_grads: bad Adam arguments");
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  const unsigned grid = static_cast<unsigned>(smc_adam_norm_partials(n_params));  // 64 entries per block
-  const AdamArgs ad = adam ? to_adam(adam) : AdamArgs{};
+  const unsigned grid = static_cast<unsigned>(reduce_blocks(n_params));  // 64 entries per block
+  const AdamArgs ad = adam ? to_adam(adam, n_params) : AdamArgs{};
   if (dtype == SMC_DTYPE_F32) {
     if (adam)
       hipLaunchKernelGGL((reduce_kernel<float, true>), dim3(grid), dim3(kNetThreads), 0, s,
@@ -617,17 +645,7 @@ int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t parti
       hipLaunchKernelGGL((reduce_kernel<double, false>), dim3(grid), dim3(kNetThreads), 0, s,
                          static_cast<const double*>(partials), partial_blocks, n_params, static_cast<double*>(grads), ad);
   }
-  int32_t rc = check_launch("cvnn reduce_kernel");
-  if (rc != SMC_OK || !adam) return rc;
-  if (dtype == SMC_DTYPE_F32)
-    hipLaunchKernelGGL(finalize_kernel<float>, dim3(1), dim3(kNetThreads), 0, s, adam->norm_partials,
-                       static_cast<int64_t>(grid), static_cast<const float*>(grads), n_params, adam->step,
-                       static_cast<float*>(adam->grad_norm), static_cast<float*>(adam->loss));
-  else
-    hipLaunchKernelGGL(finalize_kernel<double>, dim3(1), dim3(kNetThreads), 0, s, adam->norm_partials,
-                       static_cast<int64_t>(grid), static_cast<const double*>(grads), n_params, adam->step,
-                       static_cast<double*>(adam->grad_norm), static_cast<double*>(adam->loss));
-  return check_launch("cvnn finalize_kernel");
+  return check_launch("cvnn reduce_kernel");
 }
 
 int32_t smc_adam_step(int32_t dtype, int64_t n_params, const void* grads, const smc_adam_args* adam, void* stream) {
@@ -636,25 +654,14 @@ int32_t smc_adam_step(int32_t dtype, int64_t n_params, const void* grads, const 
   if (!adam_valid(adam)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_adam_step: bad Adam arguments");
   const hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned grid = static_cast<unsigned>((n_params + kNetThreads - 1) / kNetThreads);
-  const AdamArgs ad = to_adam(adam);
-  if (dtype == SMC_DTYPE_F32) {
+  const AdamArgs ad = to_adam(adam, n_params);
+  if (dtype == SMC_DTYPE_F32)
     hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(kNetThreads), 0, s, static_cast<const float*>(grads),
                        n_params, ad);
-    int32_t rc = check_launch("adam_kernel");
-    if (rc != SMC_OK) return rc;
-    hipLaunchKernelGGL(finalize_kernel<float>, dim3(1), dim3(kNetThreads), 0, s, adam->norm_partials,
-                       static_cast<int64_t>(grid), static_cast<const float*>(grads), n_params, adam->step,
-                       static_cast<float*>(adam->grad_norm), static_cast<float*>(adam->loss));
-  } else {
+  else
     hipLaunchKernelGGL(adam_kernel<double>, dim3(grid), dim3(kNetThreads), 0, s, static_cast<const double*>(grads),
                        n_params, ad);
-    int32_t rc = check_launch("adam_kernel");
-    if (rc != SMC_OK) return rc;
-    hipLaunchKernelGGL(finalize_kernel<double>, dim3(1), dim3(kNetThreads), 0, s, adam->norm_partials,
-                       static_cast<int64_t>(grid), static_cast<const double*>(grads), n_params, adam->step,
-                       static_cast<double*>(adam->grad_norm), static_cast<double*>(adam->loss));
-  }
-  return check_launch("cvnn finalize_kernel");
+  return check_launch("adam_kernel");
 }
 
 }  // extern "C"

@@ -128,7 +128,8 @@ class FusedNetworkStep:
             self.workspace = None
         self.blocks = blocks.value
         self.partials = torch.empty((self.blocks, self.n + 1), dtype=dtype, device=dev)
-        self.norm_partials = torch.empty(int(L.smc_adam_norm_partials(self.n)), dtype=torch.float64, device=dev)
+        # (zeroed: its last slot is the fused finalize's arrival counter, which every update leaves at zero)
+        self.norm_partials = torch.zeros(int(L.smc_adam_norm_partials(self.n)), dtype=torch.float64, device=dev)
         self.grads = flat_grads
         # parameters and Adam moments -> flat buffers (views keep torch's objects valid)
         self.params_flat = torch.empty(self.n, dtype=dtype, device=dev)
