@@ -254,7 +254,12 @@ __device__ __forceinline__ void tile_gemm(f32x4* acc, const typename Op::T* ap, 
   }
 }
 
-constexpr int kFbThreads = 1024;
+// 512 threads (8 waves, two workgroups per CU at the 4-waves-per-SIMD register budget): beside the path kernel's
+// store stream each workgroup's chain of dependent global loads waits microseconds per load, and a second
+// workgroup per CU overlaps it (round 5, profiles/r05/bench_fb_threads.txt: lock-step 0.320 -> 0.305 ms/step;
+// the network alone on 32 CUs beside an HBM write storm 286 -> 211-236 us; a persistent form with biases and
+// weights staged in LDS measured 271 us alone and 0.313-0.315 ms/step and was not kept)
+constexpr int kFbThreads = 512;
 constexpr int kFbWaves = kFbThreads / 64;
 
 // K split of a layer GEMM with `ntile` output tiles: waves take (tile, K part) items when the

@@ -1623,17 +1623,6 @@ size_t lds_bytes(int T, int N, bool cf) {
 // Resident workgroups of a persistent kernel on the current device (occupancy x CUs, cached
 // per (device, kernel)); grid = min(work items, that).
 // CUs a stream may use: the popcount of its CU mask (hipExtStreamCreateWithCUMask), else the device's
-int stream_cus(hipStream_t stream, int cus) {
-  if (!stream) return cus;
-  uint32_t mask[16] = {};
-  if (hipExtStreamGetCUMask(stream, 16, mask) != hipSuccess) {
-    (void)hipGetLastError();
-    return cus;
-  }
-  int n = 0;
-  for (int i = 0; i < 16 && i * 32 < cus; ++i) n += __builtin_popcount(mask[i]);
-  return n > 0 && n < cus ? n : cus;
-}
 
 // Persistent grid: the kernel's resident slots on the CUs `stream` may use (a CU-masked stream's
 // launch is sized to its mask, so every workgroup is resident at once), at most `items`.

@@ -31,6 +31,20 @@ inline int32_t check_launch(const char* kernel) {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// CUs a (CU-masked) stream may use, out of `cus` (hipExtStreamCreateWithCUMask streams: the popcount of the
+// mask; other streams: all).  Persistent launches size their grids to it, so every workgroup is resident.
+inline int stream_cus(hipStream_t stream, int cus) {
+  if (!stream) return cus;
+  uint32_t mask[16] = {};
+  if (hipExtStreamGetCUMask(stream, 16, mask) != hipSuccess) {
+    (void)hipGetLastError();
+    return cus;
+  }
+  int n = 0;
+  for (int i = 0; i < 16 && i * 32 < cus; ++i) n += __builtin_popcount(mask[i]);
+  return n > 0 && n < cus ? n : cus;
+}
+
 // Polls of an inter-workgroup exchange before it gives up (~1 s of s_sleep(2) polling); the
 // exchange then sets SMC_SYNC_EXCHANGE_TIMEOUT in the sync area's status word and writes NaN
 // targets for the contracts it could not finish.

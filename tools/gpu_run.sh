@@ -73,6 +73,9 @@ for step in "$@"; do
     profbench:*)  # profbench:<config>[:steps] -> rocprofv3 kernel stats of bench.py (no CPU leg)
       IFS=: read -r _ cfg st <<< "$step"
       cd /tmp && run "prof_${cfg}" 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_${cfg}" -o run --output-format csv -- python "$ROOT/bench.py" --config "$cfg" --steps "${st:-5}" --warmup 2 --kernel-iters 2 --no-cpu-baseline; cd "$ROOT" ;;
+    profstep:*)  # profstep:<config>[:iters] -> rocprofv3 kernel stats of the MC launch alone (tools/kprof_step.py)
+      IFS=: read -r _ cfg its <<< "$step"
+      cd /tmp && run "profstep_${cfg}" 300 rocprofv3 --kernel-trace --stats -d "$OUT/profstep_${cfg}" -o run --output-format csv -- python "$ROOT/tools/kprof_step.py" --config "$cfg" --iters "${its:-10}"; cd "$ROOT" ;;
     benchcfg:*)  # benchcfg:<config>[:steps] -> bench.py line with the CPU baseline
       IFS=: read -r _ cfg st <<< "$step"
       run "bench_${cfg}" 900 python bench.py --config "$cfg" --steps "${st:-10}" --warmup 3 --kernel-iters 2 ;;

@@ -1,9 +1,11 @@
 """Shader clock and VALU issue rate per dispatch from a rocprofv3 --pmc run that collected GRBM_GUI_ACTIVE
 (GPU-clock cycles the graphics block was busy, one value per XCD) and optionally SQ_INSTS_VALU / SQ_BUSY_CYCLES.
-    clock_MHz  = GRBM_GUI_ACTIVE (mean over XCD instances) / dispatch duration
+    clock_MHz  = GRBM_GUI_ACTIVE per XCD / dispatch duration (rocprofv3 on this pool reports one instance, the
+                 SUM over the chip's XCDs: it is divided by --xcds; with per-XCD instances, their mean)
     valu_frac  = SQ_INSTS_VALU x 4 cycles / (SIMDs x GRBM cycles): VALU issue slots used at the clock the
                  kernel actually ran at (each wave64 VALU instruction holds its SIMD 4 cycles; 4 SIMDs per CU)
-Usage: python tools/pmc_clock.py DIR [--kernel SUBSTRING] [--cus 256]"""
+Usage: python tools/pmc_clock.py DIR [--kernel SUBSTRING] [--cus 256] [--xcds 8]
+(round 4 printed the aggregate as if it were one XCD: clocks 8x and issue fractions 1/8 of the true values)"""
 import argparse
 import csv
 import glob
@@ -15,6 +17,7 @@ def main() -> None:
     ap.add_argument("dir")
     ap.add_argument("--kernel", default="")
     ap.add_argument("--cus", type=int, default=256)
+    ap.add_argument("--xcds", type=int, default=8, help="XCDs summed into one aggregated GRBM_GUI_ACTIVE instance")
     a = ap.parse_args()
     per: dict[int, dict] = defaultdict(lambda: {"ctr": defaultdict(float), "inst": defaultdict(int)})
     for f in glob.glob(f"{a.dir}/**/*counter_collection.csv", recursive=True):
@@ -33,7 +36,7 @@ def main() -> None:
         g, n = d["ctr"].get("GRBM_GUI_ACTIVE"), d["inst"].get("GRBM_GUI_ACTIVE", 1)
         line = f"{disp:5d} {d['name']:40s} {d['dur'] * 1e3:8.3f} ms"
         if g:
-            cyc = g / n
+            cyc = g / n if n > 1 else g / a.xcds  # GPU-clock cycles of one XCD
             line += f"  clock {cyc / d['dur'] / 1e6:6.0f} MHz"
             v = d["ctr"].get("SQ_INSTS_VALU")
             if v:
