@@ -292,8 +292,9 @@ int32_t smc_cvnn_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers
                                   const void* input_im, const void* targets, int64_t batch,
                                   void* partials, int64_t partial_blocks, void* stream);
 /* grads[0..n_params] = fixed-order sum of the partials (last entry: loss).  With adam != NULL
- * the Adam update, grad norm, loss copy and step increment follow in the same launch (the last
- * workgroup to finish takes the grad norm, loss and step: one kernel, ABI 12). */
+ * the Adam update, grad norm, loss copy and step increment follow (ABI 12: for networks of up to
+ * 65,535 parameters in the same launch, whose last workgroup takes the grad norm, loss and step;
+ * larger ones in a second, one-workgroup launch). */
 int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t partial_blocks,
                               int64_t n_params, void* grads, const smc_adam_args* adam, void* stream);
 /* Adam update from an already reduced (e.g. all-reduced) grads[0..n_params]. */

@@ -19,12 +19,14 @@
 //     (fused, single process) and per-block partial sums of g^2.
 //   * adam_kernel: the same update from an already reduced (all-reduced) gradient buffer.
 //   * the last workgroup of either (an arrival counter) takes the grad norm from the block partials (fixed
-//     order), the loss and step += 1 (round 4 and before: a separate finalize_kernel launch).
+//     order), the loss and step += 1; reduce grids above kFuseFinalizeMaxBlocks workgroups (wide networks)
+//     leave that to finalize_kernel, a one-workgroup launch.
 // Weights stay in HBM/L2 (tens of KB for the benchmark network); parameters, gradients and
 // Adam moments are single flat buffers whose layout is the model's parameter order.
 
 #include <cmath>
 
+#include "smc_device.h"
 #include "smc_internal.h"
 
 namespace smc {
@@ -372,7 +374,14 @@ struct AdamArgs {
   int64_t norm_slots;     // smc_adam_norm_partials(n_params)
   void* grad_norm;        // scalar out
   void* loss;             // scalar out: grads[n_params]
+  int32_t fuse_final;     // the last workgroup finalizes (else finalize_kernel, a launch of its own)
 };
+
+// Reduce grids up to this many workgroups finalize in their last workgroup; larger ones in finalize_kernel:
+// every workgroup's drained sc1 hand-off and one counter atomic cost more than the launch they save (round 5:
+// the H = 256 network's 4,176-workgroup reduce alone 0.224 -> 0.266 ms fused; the narrow networks' <= 306
+// workgroups: e2e 0.108 -> 0.098 ms/step, lock-step 0.305 -> 0.295, profiles/r05/bench_finalize_sc1_vs_r4.txt)
+constexpr int64_t kFuseFinalizeMaxBlocks = 1024;
 
 template <typename Real>
 __device__ __forceinline__ void adam_update(const AdamArgs& ad, int64_t p, Real g) {
@@ -398,32 +407,33 @@ __device__ __forceinline__ void adam_update(const AdamArgs& ad, int64_t p, Real 
 constexpr int kReduceCols = 64;
 constexpr int kReduceSlices = kNetThreads / kReduceCols;
 
-// The update's tail, fused (round 5: it was a separate one-workgroup finalize_kernel launch): every workgroup has
-// written its g^2 partial; the last one to arrive on the counter (the final slot of norm_partials, zero between
+// The update's tail, fused (round 5: it was a separate one-workgroup finalize_kernel launch): every workgroup
+// publishes its g^2 partial; the last one to arrive on the counter (the final slot of norm_partials, zero between
 // launches) adds the partials in index order (finalize_kernel's order: thread stride, then block_sum), writes the
 // grad norm and the loss, increments Adam's step and resets the counter.  Every workgroup read the step before
-// it arrived.  Release: each thread's agent-scope fence after its stores; acquire: after the counter.
+// it arrived.  Hand-off without fences: the partial (and the loss slot, reduce_kernel) are write-through (sc1)
+// stores drained before the arrival and read with sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility).
+// An agent-scope release fence per thread would write back the XCD's whole L2 -- beside the path kernel, all of
+// its dirty path lines: the first fused form (__threadfence per thread) made the H = 256 network 0.22 -> 0.53 ms.
 template <typename Real>
 __device__ __forceinline__ void adam_finalize_last(const AdamArgs& ad, int64_t n_partials, const Real* grads,
-                                                   int64_t n_params, double* red) {
+                                                   int64_t n_params, double* red, double partial) {
   __shared__ int last;
-  __threadfence();
+  if (threadIdx.x == 0) put_sc1(ad.norm_partials + blockIdx.x, partial);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores (the partial, the loss slot) done
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t* cnt = reinterpret_cast<uint32_t*>(ad.norm_partials + (ad.norm_slots - 1));
-    last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   double sum = 0.0;
-  for (int64_t i = threadIdx.x; i < n_partials; i += kNetThreads)
-    sum += __hip_atomic_load(ad.norm_partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int64_t i = threadIdx.x; i < n_partials; i += kNetThreads) sum += get_sc1(ad.norm_partials + i);
   const double t = block_sum<double>(sum, red);
   if (threadIdx.x == 0) {
     *static_cast<Real*>(ad.grad_norm) = static_cast<Real>(sqrt(t));
-    *static_cast<Real*>(ad.loss) =
-        __hip_atomic_load(const_cast<Real*>(grads) + n_params, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *static_cast<Real*>(ad.loss) = get_sc1(grads + n_params);
     *ad.step = *ad.step + 1.0f;
     __hip_atomic_store(reinterpret_cast<uint32_t*>(ad.norm_partials + (ad.norm_slots - 1)), 0u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -455,7 +465,8 @@ __global__ __launch_bounds__(kNetThreads) void reduce_kernel(const Real* __restr
     double s = 0.0;
     for (int k = 0; k < kReduceSlices; ++k) s += slice_sum[k][col];
     const Real gr = static_cast<Real>(s);
-    grads[p] = gr;
+    if (ADAM && p == n_params) put_sc1(grads + p, gr);  // the loss slot: read by the last workgroup
+    else grads[p] = gr;
     if (ADAM && p < n_params) {
       sq = static_cast<double>(gr) * static_cast<double>(gr);
       adam_update<Real>(ad, p, gr);
@@ -463,8 +474,8 @@ __global__ __launch_bounds__(kNetThreads) void reduce_kernel(const Real* __restr
   }
   if (ADAM) {
     const double t = block_sum<double>(sq, red);
-    if (threadIdx.x == 0) ad.norm_partials[blockIdx.x] = t;
-    adam_finalize_last<Real>(ad, gridDim.x, grads, n_params, red);
+    if (ad.fuse_final) adam_finalize_last<Real>(ad, gridDim.x, grads, n_params, red, t);
+    else if (threadIdx.x == 0) ad.norm_partials[blockIdx.x] = t;
   }
 }
 
@@ -480,8 +491,35 @@ __global__ __launch_bounds__(kNetThreads) void adam_kernel(const Real* __restric
     adam_update<Real>(ad, p, g);
   }
   const double t = block_sum<double>(sq, red);
-  if (threadIdx.x == 0) ad.norm_partials[blockIdx.x] = t;
-  adam_finalize_last<Real>(ad, gridDim.x, grads, n_params, red);
+  if (ad.fuse_final) adam_finalize_last<Real>(ad, gridDim.x, grads, n_params, red, t);
+  else if (threadIdx.x == 0) ad.norm_partials[blockIdx.x] = t;
+}
+
+// The finalize of large reduce grids (!AdamArgs.fuse_final): grad norm from the block partials (fixed order),
+// loss, step += 1, one workgroup after the update launch.
+template <typename Real>
+__global__ __launch_bounds__(kNetThreads) void finalize_kernel(const double* __restrict__ norm_partials,
+                                                               int64_t n_partials, const Real* __restrict__ grads,
+                                                               int64_t n_params, float* step, Real* grad_norm,
+                                                               Real* loss) {
+  __shared__ double red[kNetThreads / 64];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n_partials; i += kNetThreads) s += norm_partials[i];
+  const double t = block_sum<double>(s, red);
+  if (threadIdx.x == 0) {
+    *grad_norm = static_cast<Real>(sqrt(t));
+    *loss = grads[n_params];
+    *step = *step + 1.0f;
+  }
+}
+
+template <typename Real>
+int32_t launch_finalize(const smc_adam_args* adam, unsigned grid, const void* grads, int64_t n_params,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(finalize_kernel<Real>, dim3(1), dim3(kNetThreads), 0, s, adam->norm_partials,
+                     static_cast<int64_t>(grid), static_cast<const Real*>(grads), n_params, adam->step,
+                     static_cast<Real*>(adam->grad_norm), static_cast<Real*>(adam->loss));
+  return check_launch("cvnn finalize_kernel");
 }
 
 bool layers_valid(const smc_cvnn_layer* layers, int32_t n_layers, int64_t n_params) {
@@ -593,7 +631,7 @@ int32_t smc_cvnn_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers
   return check_launch("cvnn forward_backward_kernel");
 }
 
-static AdamArgs to_adam(const smc_adam_args* ad, int64_t n_params) {
+static AdamArgs to_adam(const smc_adam_args* ad, int64_t n_params, unsigned grid) {
   AdamArgs a{};
   a.params = ad->params;
   a.exp_avg = ad->exp_avg;
@@ -608,6 +646,7 @@ static AdamArgs to_adam(const smc_adam_args* ad, int64_t n_params) {
   a.norm_slots = smc_adam_norm_partials(n_params);
   a.grad_norm = ad->grad_norm;
   a.loss = ad->loss;
+  a.fuse_final = grid <= kFuseFinalizeMaxBlocks ? 1 : 0;
   return a;
 }
 
@@ -629,7 +668,7 @@ int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t parti
   if (adam && !adam_valid(adam)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_reduce_grads: bad Adam arguments");
   const hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned grid = static_cast<unsigned>(reduce_blocks(n_params));  // 64 entries per block
-  const AdamArgs ad = adam ? to_adam(adam, n_params) : AdamArgs{};
+  const AdamArgs ad = adam ? to_adam(adam, n_params, grid) : AdamArgs{};
   if (dtype == SMC_DTYPE_F32) {
     if (adam)
       hipLaunchKernelGGL((reduce_kernel<float, true>), dim3(grid), dim3(kNetThreads), 0, s,
@@ -645,7 +684,10 @@ int32_t smc_cvnn_reduce_grads(int32_t dtype, const void* partials, int64_t parti
       hipLaunchKernelGGL((reduce_kernel<double, false>), dim3(grid), dim3(kNetThreads), 0, s,
                          static_cast<const double*>(partials), partial_blocks, n_params, static_cast<double*>(grads), ad);
   }
-  return check_launch("cvnn reduce_kernel");
+  const int32_t rc = check_launch("cvnn reduce_kernel");
+  if (rc != SMC_OK || !adam || ad.fuse_final) return rc;
+  return dtype == SMC_DTYPE_F32 ? launch_finalize<float>(adam, grid, grads, n_params, s)
+                                : launch_finalize<double>(adam, grid, grads, n_params, s);
 }
 
 int32_t smc_adam_step(int32_t dtype, int64_t n_params, const void* grads, const smc_adam_args* adam, void* stream) {
@@ -654,14 +696,17 @@ int32_t smc_adam_step(int32_t dtype, int64_t n_params, const void* grads, const 
   if (!adam_valid(adam)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_adam_step: bad Adam arguments");
   const hipStream_t s = static_cast<hipStream_t>(stream);
   const unsigned grid = static_cast<unsigned>((n_params + kNetThreads - 1) / kNetThreads);
-  const AdamArgs ad = to_adam(adam, n_params);
+  const AdamArgs ad = to_adam(adam, n_params, grid);
   if (dtype == SMC_DTYPE_F32)
     hipLaunchKernelGGL(adam_kernel<float>, dim3(grid), dim3(kNetThreads), 0, s, static_cast<const float*>(grads),
                        n_params, ad);
   else
     hipLaunchKernelGGL(adam_kernel<double>, dim3(grid), dim3(kNetThreads), 0, s, static_cast<const double*>(grads),
                        n_params, ad);
-  return check_launch("adam_kernel");
+  const int32_t rc = check_launch("adam_kernel");
+  if (rc != SMC_OK || ad.fuse_final) return rc;
+  return dtype == SMC_DTYPE_F32 ? launch_finalize<float>(adam, grid, grads, n_params, s)
+                                : launch_finalize<double>(adam, grid, grads, n_params, s);
 }
 
 }  // extern "C"
