@@ -13,8 +13,8 @@ every rank processes B contracts per step (contract-sharded data parallel, one R
 Rank 0 prints ONE JSON line.  `value` = contracts x paths per second over the whole job.
 The roofline object is for the dominant kernel (the MC part of the step: resident_kernel at C2,
 its sliced form at C3, basket_resident_kernel at C5): algorithmic bytes per launch over the
-average duration of the MC launches inside the timed region (HIP events on the MC stream);
-`kernel_ms_isolated` is the same launch alone after the timed region.  `cpu_baseline` is the
+launch's duration, timed with HIP events on its own stream right after the timed region (`kernel_ms`;
+`kernel_ms_live` / `kernel_ms_steady`: the launches inside the timed region).  `cpu_baseline` is the
 reference CPU path (torch-cpu + numpy.fft, oracle/torch_cpu.py) on a bounded sample, with the
 C/OpenMP oracle as a second leg and C1 timed over 10 whole steps.
 """
@@ -441,17 +441,21 @@ def main() -> None:
     # live: HIP events on the MC stream around each MC-part launch inside the timed region
     # (Sobol draw + path/CF kernel + cursor update; the path/CF kernel is >99 % of it)
     live = [a.elapsed_time(b_) for a, b_ in (session.mc_events or [])]
-    live_ms = (sum(live) / len(live) / launches_per_call) if live else kernel_ms
+    live_ms = (sum(live) / len(live) / launches_per_call) if live else None
     lanes = getattr(eng, "lanes", 1)
     steady_ms = None
     if lanes > 1 and live:
         # MC lanes: step s + 1's launch starts in step s's tail, so an event pair around one launch also
-        # spans its wait for CUs; the launch duration is the isolated one, and the MC part's steady
-        # rate is the span of all live launches over their number
+        # spans its wait for CUs (no launch duration); the MC part's steady rate is the span of all live
+        # launches over their number
         ev = session.mc_events
         steady_ms = ev[0][0].elapsed_time(ev[-1][1]) / len(ev) / launches_per_call
-        live_ms = kernel_ms
-    achieved = bytes_launch / (live_ms * 1e-3) / 1e9
+        live_ms = None
+    # roofline: the launch's own duration, the same definition for every config (round 5; before, configs without
+    # MC lanes used the live event pairs, which also hold launch gaps and the CUs the concurrent network takes):
+    # the dominant launch alone, repeated on its own stream after the timed region -- the figure a rocprofv3
+    # kernel trace of that launch shape reproduces (tools/kprof_step.py, profiles/r05)
+    achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
 
     # ---- network part alone (fused HIP kernels), HIP events on its own stream ------------
     network = None
@@ -567,8 +571,12 @@ def main() -> None:
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
                      # bytes the kernel actually moved (PMC) over its live time, against the same peak
-                     "frac_moved": (traffic / (live_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                     "kernel_ms": live_ms, "kernel_ms_isolated": kernel_ms, "live_launches": len(live),
+                     "frac_moved": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                     "kernel_ms": kernel_ms, "kernel_ms_isolated": kernel_ms, "live_launches": len(live),
+                     # one MC lane: the launch inside the timed region (HIP events on the MC stream), next to the
+                     # network kernels of the previous step
+                     "kernel_ms_live": live_ms,
+                     "frac_live": (bytes_launch / (live_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if live_ms else None,
                      "mc_lanes": lanes,
                      # lanes > 1: consecutive launches overlap; the MC part's steady
                      # time per launch and the fraction of peak it corresponds to

@@ -29,7 +29,8 @@ def main() -> None:
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--budget-gb", type=float, default=40.0, help="path scratch budget (engine default)")
+    ap.add_argument("--budget-gb", type=float, default=0.0,
+                    help="path scratch budget (0: the engine's, engine.path_buffer_budget: half the HBM)")
     ap.add_argument("--pitch", type=int, default=0, help="row pitch in elements (0: smc_path_pitch)")
     ap.add_argument("--lanes", type=int, default=1, help="launches alternate over this many streams, each with "
                     "its own cursor, sync area and path scratch (consecutive launches may overlap)")
@@ -48,7 +49,14 @@ def main() -> None:
     pitch = a.pitch or int(L.smc_path_pitch(P, dcode))
     esz = 8 if f64 else 4
     per = (T if store == _lib.STORE_ALL else 1) * pitch * esz
-    chunk = max(1, min(B, int(a.budget_gb * (1 << 30)) // per))
+    from spectralmc_amd.engine import path_buffer_budget
+
+    budget = int(a.budget_gb * (1 << 30)) if a.budget_gb else path_buffer_budget(dev)
+    chunk = max(1, min(B, budget // per))
+    if chunk < B:  # the engine's rounding: whole rounds of resident workgroups (2 per CU)
+        slots = 2 * torch.cuda.get_device_properties(dev).multi_processor_count
+        if chunk >= slots:
+            chunk -= chunk % slots
     launches = -(-B // chunk)
     chunk = -(-B // launches)
     lanes = a.lanes
