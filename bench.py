@@ -94,6 +94,8 @@ def parse(argv: list[str] | None = None) -> argparse.Namespace:
                     help="pricer.mc_lanes_long (MC lanes for long path launches beside a narrow network)")
     ap.add_argument("--lanes", type=int, default=2, choices=[1, 2, 4], help="MC lanes (pricer.mc_lanes): consecutive path launches "
                     "on alternating streams, each starting in the previous one's tail")
+    ap.add_argument("--lanes-short", type=int, default=None,
+                    help="pricer.mc_lanes_short (MC lanes for launches below --net-cu-min-path-steps)")
     ap.add_argument("--net-cus", type=int, default=32, help="CUs reserved for the network (pricer.network_cus)")
     ap.add_argument("--net-cus-small", type=int, default=None,
                     help="pricer.network_cus_small (network CUs beside launches below --net-cu-min-path-steps)")
@@ -270,6 +272,8 @@ def make_pricer(args: argparse.Namespace, dev):
     pricer.mc_lanes = args.lanes
     if args.lanes_long is not None:
         pricer.mc_lanes_long = args.lanes_long
+    if args.lanes_short is not None:
+        pricer.mc_lanes_short = args.lanes_short
     pricer.network_cus = args.net_cus
     pricer.network_cus_wide = args.net_cus_wide
     pricer.network_cu_pattern = args.net_cu_pattern

@@ -443,6 +443,10 @@ class GbmCVNNPricer:
     #: the wide C2/H=256 network (3.03 -> 3.07) (profiles/r04/mc_lanes.txt): the default stays 2
     mc_lanes_long: int = 2
     mc_lanes_long_path_steps: int = 1 << 30
+    #: ... and this many for launches below network_cu_min_path_steps path-steps, where the network chain, not the
+    #: path launch, sets the step time and a second launch in flight only slows it (the reference's e2e shape:
+    #: one lane 0.095-0.097 against two 0.100-0.101 ms/step; profiles/r05/netcus_short_shapes.txt)
+    mc_lanes_short: int = 1
     #: with engine lanes: CUs reserved for the network part (CU-masked HIP streams, the path kernels on
     #: the rest; 0: none) and their choice of CU ids ("low": the lowest logical ids, which measured
     #: best; "spread": evenly over the id range)
@@ -609,7 +613,7 @@ class GbmCVNNPricer:
         """Set up a device training session (engine buffers, Adam, step program) for ``config``."""
         if isinstance(self._sampler_result, Failure):
             return Failure(SamplerInitFailed(error=self._sampler_result.error))
-        for name in ("mc_lanes", "mc_lanes_long"):
+        for name in ("mc_lanes", "mc_lanes_long", "mc_lanes_short"):
             lanes = getattr(self, name) if self.overlap_mc else 1
             if not isinstance(lanes, int) or lanes < 1 or _StepProgram.SLOTS % lanes:
                 # a lane's device cursor assumes it runs every lanes-th step; the step slots (whose graphs
@@ -828,9 +832,12 @@ class TrainingSession:
             lanes = pricer.mc_lanes if pricer.overlap_mc else 1
             sp = pricer._cfg.sim_params
             widest_in = max((m.in_features for m in pricer._cvnn.modules() if isinstance(m, ComplexLinear)), default=0)
+            path_steps = config.batch_size * sp.total_paths() * sp.timesteps
             if (lanes > 1 and pricer.fused_network and 0 < widest_in < 128
-                    and config.batch_size * sp.total_paths() * sp.timesteps >= pricer.mc_lanes_long_path_steps):
+                    and path_steps >= pricer.mc_lanes_long_path_steps):
                 lanes = pricer.mc_lanes_long
+            if lanes > 1 and path_steps < pricer.network_cu_min_path_steps:
+                lanes = pricer.mc_lanes_short
             self.engine = TrainingEngine(pricer._cfg, sampler, config.batch_size, model_dtype=pricer._dtype.to_torch(),
                                          device=dev, rank=rank, world_size=world, store_paths=pricer.store_paths,
                                          math=pricer.math_mode, lanes=lanes)

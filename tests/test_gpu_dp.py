@@ -46,6 +46,8 @@ def _train(batch: int, outfile: str, basket: int = 0) -> None:
     cfg = make_gbm_cvnn_config(model, sim_params=sp, bs_config=make_black_scholes_config(sim_params=sp),
                                domain_bounds=make_domain_bounds())
     pricer = expect_success(GbmCVNNPricer.create(cfg))
+    if basket < 0:
+        pricer.mc_lanes_short = 2  # keep two MC lanes at this short launch (the policy would run one)
     if basket > 0:
         from spectralmc_amd.basket import BasketConfig, use_basket_engine
 

@@ -534,6 +534,7 @@ def test_mc_lanes_match_one_stream(lanes: int) -> None:
                                    domain_bounds=make_domain_bounds())
         p = expect_success(GbmCVNNPricer.create(cfg))
         p.overlap_mc, p.mc_lanes, p.math_mode = overlap, lanes, "hw"
+        p.mc_lanes_short = lanes  # (a short launch: the policy would run it on one lane)
         return p, model
 
     cfg = make_training_config(num_batches=9, batch_size=96)
@@ -573,7 +574,7 @@ def test_mc_lanes_must_divide_the_step_slots() -> None:
     assert isinstance(res, Failure) and "mc_lanes" in res.error.message
 
 
-@pytest.mark.parametrize("field", ["mc_lanes", "mc_lanes_long"])
+@pytest.mark.parametrize("field", ["mc_lanes", "mc_lanes_long", "mc_lanes_short"])
 def test_lane_counts_that_do_not_divide_the_slots_are_rejected(field) -> None:
     """Both lane settings are validated when the session opens (mc_lanes_long was checked only by
     an assert inside the step program)."""
