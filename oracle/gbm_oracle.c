@@ -183,41 +183,40 @@ static void twiddle(int64_t j, int64_t N, double* s_out, double* c_out) {
 static inline uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
 static inline double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
 
-/* -2 ln((a + 1/2) 2^-32) as smc_math.h m2log_u32 (round 4, v3): m = a + 1/2 = 2^e f exactly; table point
- * c = 1 + i/1024, i = (mh + 2^9) >> 10 from the top 20 mantissa bits mh; r' = -2 (f INV - 1) in one fma;
- * r' + r'^2 Q(r') (Q: D5 = 1/80, D4 = 1/32, D3 = 1/12, D2 = 1/4, Horner); then
- * (k (-2 LN2_HI) + (-2 T_HI)) + ((k (-2 LN2_LO) + (-2 T_LO)) + that), k = e - 32. */
+/* -2 ln((a + 1/2) 2^-32) as smc_math.h m2log_u32 (round 5, v4): m = a + 1/2 = fr 2^e exactly (frexp, fr in
+ * [1/2, 1)); table point c = 1 + i/1024 nearest f = 2 fr, i = (mh + 2^9) >> 10 from fr's top 20 mantissa bits
+ * mh (the device addresses row i as ((hw + 2^9) >> 5) & 0xFFE0 bytes, hw = fr's high word: the same i);
+ * r' = fr (-4 INV) + 2 in one fma; r' + r'^2 Q(r') (Q: D5 = 1/80, D4 = 1/32, D3 = 1/12, D2 = 1/4, Horner);
+ * then (e (-2 LN2_HI) + HI) + ((e (-2 LN2_LO) + LO) + that), HI / LO the row's -2 T + 33 (2 LN2) parts. */
 static double m2log_u32(uint32_t a) {
   const double m = (double)a + 0.5;
-  const uint64_t bits = d2u(m);
-  const uint32_t hw = (uint32_t)(bits >> 32);
-  const uint32_t mh = hw & 0xFFFFFu;
-  const uint32_t idx = (mh + 0x200u) >> 10;
-  const double f = u2d(((uint64_t)(mh | 0x3FF00000u) << 32) | (bits & 0xFFFFFFFFull));
-  const double k = (double)((int)(hw >> 20) - 1055);
+  int ei;
+  const double fr = frexp(m, &ei);
+  const double e = (double)ei;
+  const uint32_t hw = (uint32_t)(d2u(fr) >> 32);
+  const uint32_t idx = ((hw & 0xFFFFFu) + 0x200u) >> 10;
   const double* t = kF64LogTab[idx];
-  const double r = fma(f, t[0], 2.0);
+  const double r = fma(fr, t[0], 2.0);
   double q = 0.0125;
   q = fma(q, r, 0.03125);
   q = fma(q, r, 0.08333333333333333);
   q = fma(q, r, 0.25);
   const double p = fma(q, r * r, r);
-  return fma(k, kF64M2Ln2Hi, t[1]) + (fma(k, kF64M2Ln2Lo, t[2]) + p);
+  return fma(e, kF64M2Ln2Hi, t[1]) + (fma(e, kF64M2Ln2Lo, t[2]) + p);
 }
 
-/* (sin, cos)(2 pi b 2^-32) as smc_math.h (round 4): nearest of 1024 table angles j = round(b / 2^22)
- * (mod 1024), rem = b - j 2^22 in [-2^21, 2^21) exactly, x = rem (2 pi 2^-32) (|x| <= pi/1024), sin x to
- * x^5, cos x to x^4, then the rotation by the table's (sin, cos)(2 pi j / 1024). */
+/* (sin, cos) of the angle 2 pi (j / 1024 + y 2^-32) as smc_math.h sincos2pi_u32 (round 5, v4): j = b mod
+ * 1024, y = (int32) b >> 10 (arithmetic shift) in [-2^21, 2^21); sin x = y (S1 + u (S3 + u S5)), cos x =
+ * 1 + u (C2 + u C4), u = y^2 (exact), the K^k (K = 2 pi 2^-32) in the coefficients; then the rotation by
+ * the table's (sin, cos)(2 pi j / 1024). */
 static void sincos2pi_u32(uint32_t b, double* s_out, double* c_out) {
-  const uint32_t j = ((b + (1u << 21)) >> 22) & 1023u;
-  const int32_t rem = (int32_t)(b - (j << 22));
-  const double x = (double)rem * 1.4629180792671596e-09;
-  const double u = x * x;
-  const double sp = fma(u, 0.008333333333333333, -0.16666666666666666);
-  const double sx = fma(sp * u, x, x);
-  const double cp = fma(u, 0.041666666666666664, -0.5);
+  const double y = (double)((int32_t)b >> 10);
+  const double u = y * y;
+  const double sp = fma(u, kF64SinS5, kF64SinS3);
+  const double sx = fma(u, sp, kF64SinS1) * y;
+  const double cp = fma(u, kF64CosC4, kF64CosC2);
   const double cx = fma(cp, u, 1.0);
-  const double S = kF64SinCosTab[j][0], C = kF64SinCosTab[j][1];
+  const double S = kF64SinCosTab[b & 1023u][0], C = kF64SinCosTab[b & 1023u][1];
   *s_out = fma(S, cx, C * sx);
   *c_out = fma(C, cx, -(S * sx));
 }
@@ -289,7 +288,7 @@ void oracle_stream_u32(uint64_t seed, uint64_t ordinal, uint64_t group, int64_t 
 static void normal_pair(mwc64x* g, int is_f64, double* z0, double* z1) {
   const uint32_t a = mwc_next(g), b = mwc_next(g);
   if (is_f64) {
-    /* u1 = (a + 1/2) 2^-32, angle b 2^-32 revolutions: smc_math.h m2log_u32 / sincos2pi_u32 */
+    /* u1 = (a + 1/2) 2^-32, the angle of b (sincos2pi_u32): smc_math.h m2log_u32 / sincos2pi_u32 */
     const double r = sqrt(m2log_u32(a));
     double sn, cs;
     sincos2pi_u32(b, &sn, &cs);

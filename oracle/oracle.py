@@ -116,7 +116,8 @@ def m2log_u32(a: int) -> float:
 
 
 def sincos2pi_u32(b: int) -> tuple[float, float]:
-    """(sin, cos)(2 pi b 2^-32) (csrc/smc_math.h sincos2pi_u32)."""
+    """(sin, cos) of the f64 Box-Muller angle of the 32-bit uniform b, 2 pi ((b mod 1024) / 1024 + y 2^-32) with
+    y = b >> 10 as a signed 22-bit integer (csrc/smc_math.h sincos2pi_u32)."""
     s, c = ctypes.c_double(), ctypes.c_double()
     lib().oracle_sincos2pi_u32(b, ctypes.byref(s), ctypes.byref(c))
     return s.value, c.value

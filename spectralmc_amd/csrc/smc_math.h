@@ -152,22 +152,26 @@ __device__ __forceinline__ void twiddle(int64_t j, int64_t N, double& s_out, dou
 }
 
 // ---- f64 path engine: the Box-Muller transcendentals of 32-bit uniforms and exp ------------
-// Fixed IEEE-754 sequences (fma, +, -, *, exact scaling and integer bit manipulation) over tables
+// Fixed IEEE-754 sequences (fma, +, -, *, exact scaling, frexp and integer bit manipulation) over tables
 // (smc_f64_tables.h: generated in 60-digit decimal arithmetic, rounded to double), restated op for op by
 // oracle/gbm_oracle.c, so f64 normals are bit-identical on the CPU.  Accuracy against libm
 // (tests/test_oracle.py): -2 ln u within 2 ulp, (sin, cos) within 2^-52 absolute, 2^(y/256) within 2 ulp.
-// The f64 path kernel is VALU-issue-bound (PMC, round 4: VALU busy ~95 % of the launch, every VALU
-// instruction, integer or f64, 4 cycles per wave), so the forms minimise instructions per path step
-// (v3, round 4): -2 ln u directly (the -2 folded into the table and the polynomial as exact power-of-two
-// scalings), its table indexed by the top 10 mantissa bits with no range halving (the cancellation near
-// u = 1 is avoided by an exact k LN2_HI + T_HI instead), and the path exponent carried in units of
-// ln 2 / 256 (the scale folded into the step constants), so e^y needs no Cody-Waite reduction, a
-// degree-4 polynomial, a 256-point table and one ldexp.  The kernels that run this math copy the tables
+// The f64 path kernel is VALU-issue-bound (PMC: VALU busy ~88-95 % of the launch, every VALU instruction,
+// integer or f64, 4 cycles per wave), so the forms minimise instructions per path step.  v3 (round 4):
+// -2 ln u directly (the -2 folded into the table and the polynomial as exact power-of-two scalings), its
+// table indexed by the top 10 mantissa bits with no range halving (the cancellation near u = 1 is avoided
+// by an exact k LN2_HI + T_HI instead), and the path exponent carried in units of ln 2 / 256 (the scale
+// folded into the step constants), so e^y needs no Cody-Waite reduction, a degree-4 polynomial, a
+// 256-point table and one ldexp.  v4 (round 5, 6 fewer VALU instructions per Box-Muller pair): the log's
+// mantissa and exponent from v_frexp_mant / v_frexp_exp (the exponent offset folded into the table, whose
+// 32-byte rows are addressed by one add, shift and mask of the mantissa's high word); the angle's table
+// index from the uniform's low 10 bits and its offset from the high 22 (one shift), the offset's
+// polynomial in integer units (no conversion multiply).  The kernels that run this math copy the tables
 // into LDS first (f64_tables_load): a global load on the path loop would wait for the wave's outstanding
 // path stores (one vmcnt counter).
 struct alignas(16) F64Tables {
   double2 sc[1024];     // (sin, cos)(2 pi j / 1024)
-  double log[1025][3];  // -2 INV, -2 T_HI, -2 T_LO at c = 1 + i/1024
+  double log[1025][4];  // -4 INV, -2 T_HI + 66 LN2_HI, -2 T_LO + 66 LN2_LO, 0 at c = 1 + i/1024
   double ex[256];       // 2^(j / 256)
 };
 
@@ -180,35 +184,34 @@ __device__ __forceinline__ F64Tables& f64_lds() {
 __device__ inline void f64_tables_load() {
   F64Tables& t = f64_lds();
   for (int k = threadIdx.x; k < 1024; k += blockDim.x) t.sc[k] = double2{kF64SinCosTab[k][0], kF64SinCosTab[k][1]};
-  for (int k = threadIdx.x; k < 1025 * 3; k += blockDim.x) (&t.log[0][0])[k] = (&kF64LogTab[0][0])[k];
+  for (int k = threadIdx.x; k < 1025 * 4; k += blockDim.x) (&t.log[0][0])[k] = (&kF64LogTab[0][0])[k];
   for (int k = threadIdx.x; k < 256; k += blockDim.x) t.ex[k] = kF64Exp2Tab[k];
   __syncthreads();
 }
 
-// X = -2 ln((a + 1/2) 2^-32), the Box-Muller radius squared: m = a + 1/2 = 2^e f exactly (f in [1, 2),
-// <= 33 significant bits); table point c = 1 + i/1024 nearest f from the top 10 mantissa bits (round half
-// up: i = (mh + 2^9) >> 10, i = 1024 at f -> 2); r' = -2 (f INV - 1) in one fma (|r'| <= 2^-10);
-// -2 ln(1 + r) = r' + r'^2 Q(r') with Q the r^2..r^5 terms of ln(1 + r), exactly rescaled (D2..D5 =
-// 1/4, 1/12, 1/32, 1/80); then X = (k (-2 LN2_HI) + (-2 T_HI)) + ((k (-2 LN2_LO) + (-2 T_LO)) + that),
-// k = e - 32 in -33..-1, whose first sum is exact (both multiples of 2^-42): near u = 1 (f -> 2, k = -1,
-// c = 2) it is exactly 0 and X the small remainder, with no cancellation.
+// X = -2 ln((a + 1/2) 2^-32), the Box-Muller radius squared: m = a + 1/2 = fr 2^e exactly (frexp: fr in
+// [1/2, 1), e in 0..32, <= 33 significant bits); table point c = 1 + i/1024 nearest f = 2 fr from the top 10
+// mantissa bits (round half up: i = (mh + 2^9) >> 10, i = 1024 at f -> 2; the row's byte offset 32 i is
+// ((hw + 2^9) >> 5) & 0xFFE0 of fr's high word hw = 0x3FE00000 | mh); r' = -2 (f INV - 1) = fr (-4 INV) + 2
+// in one fma (|r'| <= 2^-10); -2 ln(1 + r) = r' + r'^2 Q(r') with Q the r^2..r^5 terms of ln(1 + r),
+// exactly rescaled (D2..D5 = 1/4, 1/12, 1/32, 1/80); then X = (e (-2 LN2_HI) + HI) + ((e (-2 LN2_LO) + LO) +
+// that) with HI = -2 T_HI - 33 (-2 LN2_HI), LO the same for T_LO (k = e - 33 in -33..-1 folded into the
+// row): the first sum is exact (multiples of 2^-42 below 2^6): near u = 1 (f -> 2, e = 32, c = 2) it is
+// exactly 0 and X the small remainder, with no cancellation.
 __device__ __forceinline__ double m2log_u32(uint32_t a) {
   const double m = static_cast<double>(a) + 0.5;  // exact
-  const uint64_t bits = __double_as_longlong(m);
-  const uint32_t hw = static_cast<uint32_t>(bits >> 32);
-  const uint32_t mh = hw & 0xFFFFFu;
-  const uint32_t idx = (mh + 0x200u) >> 10;
-  const double f = __longlong_as_double(static_cast<long long>(
-      (static_cast<uint64_t>(mh | 0x3FF00000u) << 32) | (bits & 0xFFFFFFFFull)));
-  const double k = static_cast<double>(static_cast<int>(hw >> 20) - 1055);
-  const double* t = f64_lds().log[idx];
-  const double r = fma(f, t[0], 2.0);
+  const double fr = __builtin_amdgcn_frexp_mant(m);
+  const double e = static_cast<double>(__builtin_amdgcn_frexp_exp(m));
+  const uint32_t hw = static_cast<uint32_t>(static_cast<uint64_t>(__double_as_longlong(fr)) >> 32);
+  const uint32_t off = ((hw + 0x200u) >> 5) & 0xFFE0u;  // 32 i
+  const double* t = reinterpret_cast<const double*>(reinterpret_cast<const char*>(f64_lds().log) + off);
+  const double r = fma(fr, t[0], 2.0);
   double q = 0.0125;
   q = fma(q, r, 0.03125);
   q = fma(q, r, 0.08333333333333333);
   q = fma(q, r, 0.25);
   const double p = fma(q, r * r, r);
-  return fma(k, kF64M2Ln2Hi, t[1]) + (fma(k, kF64M2Ln2Lo, t[2]) + p);
+  return fma(e, kF64M2Ln2Hi, t[1]) + (fma(e, kF64M2Ln2Lo, t[2]) + p);
 }
 
 // sqrt(x) for the Box-Muller radius x = -2 ln u in [2.3e-10, 46.1] (u never 0 or 1): the correctly
@@ -227,19 +230,19 @@ __device__ __forceinline__ double sqrt_radius(double x) {
   return fma(d, h, g);
 }
 
-// (sin, cos)(2 pi b 2^-32): nearest of 1024 table angles j = round(b / 2^22) (mod 1024), rem = b - j 2^22
-// in [-2^21, 2^21) exactly, x = rem (2 pi 2^-32) (|x| <= pi/1024), sin x to x^5, cos x to x^4, then the
-// rotation by the table's (sin, cos)(2 pi j / 1024).
+// (sin, cos) of the angle 2 pi (j / 1024 + y 2^-32) of the 32-bit uniform b (v4): j = b mod 1024 (the table
+// angle), y = b >> 10 as a signed 22-bit integer in [-2^21, 2^21) (the offset, |x| = |K y| <= pi/1024,
+// K = 2 pi 2^-32): every b maps to one of the 2^32 grid angles and each grid angle to one b, so the angle is
+// uniform as b is.  sin x = y (S1 + u (S3 + u S5)), cos x = 1 + u (C2 + u C4) with u = y^2 (exact) and the
+// K^k folded into the coefficients, then the rotation by the table's (sin, cos)(2 pi j / 1024).
 __device__ __forceinline__ void sincos2pi_u32(uint32_t b, double& s_out, double& c_out) {
-  const uint32_t j = ((b + (1u << 21)) >> 22) & 1023u;
-  const int32_t rem = static_cast<int32_t>(b - (j << 22));
-  const double x = static_cast<double>(rem) * 1.4629180792671596e-09;  // 2 pi 2^-32 (exact scaling of 2 pi)
-  const double u = x * x;
-  const double sp = fma(u, 0.008333333333333333, -0.16666666666666666);
-  const double sx = fma(sp * u, x, x);
-  const double cp = fma(u, 0.041666666666666664, -0.5);
+  const double y = static_cast<double>(static_cast<int32_t>(b) >> 10);
+  const double u = y * y;
+  const double sp = fma(u, kF64SinS5, kF64SinS3);
+  const double sx = fma(u, sp, kF64SinS1) * y;
+  const double cp = fma(u, kF64CosC4, kF64CosC2);
   const double cx = fma(cp, u, 1.0);
-  const double2 sc = f64_lds().sc[j];
+  const double2 sc = f64_lds().sc[b & 1023u];
   s_out = fma(sc.x, cx, sc.y * sx);
   c_out = fma(sc.y, cx, -(sc.x * sx));
 }

@@ -1,4 +1,4 @@
-"""The f64 path-math tables (round 3; round-4 v3 forms): the device header (spectralmc_amd/csrc/smc_f64_tables.h) and
+"""The f64 path-math tables (round 3; round-4 v3 forms; round-5 v4 forms): the device header (spectralmc_amd/csrc/smc_f64_tables.h) and
 the oracle's copy (oracle/f64_tables.h) hold the same bits, and both are what tools/gen_f64_tables.py
 generates (60-digit decimal arithmetic rounded to double), so a hand edit of either breaks parity here
 rather than as an unexplained f64 mismatch on the GPU."""
@@ -39,7 +39,7 @@ def test_device_and_oracle_tables_hold_the_same_bits() -> None:
     dev = _values(os.path.join(ROOT, "spectralmc_amd", "csrc", "smc_f64_tables.h"))
     orc = _values(os.path.join(ROOT, "oracle", "f64_tables.h"))
     assert dev == orc
-    assert [len(dev[k]) for k in ("kF64LogTab", "kF64SinCosTab", "kF64Exp2Tab")] == [1025 * 3, 1024 * 2, 256]
+    assert [len(dev[k]) for k in ("kF64LogTab", "kF64SinCosTab", "kF64Exp2Tab")] == [1025 * 4, 1024 * 2, 256]
     assert _consts(os.path.join(ROOT, "spectralmc_amd", "csrc", "smc_f64_tables.h")) == \
         _consts(os.path.join(ROOT, "oracle", "f64_tables.h")) == _gen().constants()
 
@@ -60,13 +60,21 @@ def test_table_entries_are_near_libm() -> None:
     consts = _gen().constants()
     l2hi, l2lo = -consts["kF64M2Ln2Hi"] / 2, -consts["kF64M2Ln2Lo"] / 2
     assert l2hi == round(l2hi * 2.0**43) / 2.0**43 and abs(l2hi + l2lo - math.log(2)) <= 2 * math.ulp(math.log(2))
-    for i, (m2inv, m2hi, m2lo) in zip(range(0, 1025), log):
-        inv, hi, lo = -m2inv / 2, -m2hi / 2, -m2lo / 2  # stored scaled by -2 (exact)
+    m2hi_c, m2lo_c = consts["kF64M2Ln2Hi"], consts["kF64M2Ln2Lo"]
+    for i, (m4inv, hi2, lo2, pad) in zip(range(0, 1025), log):
+        # v4 rows: -4 INV (exact scaling), -2 T_HI - 33 (-2 LN2_HI) (exact), -2 T_LO - 33 (-2 LN2_LO) (rounded)
+        assert pad == 0.0 and hi2 == round(hi2 * 2.0**42) / 2.0**42 and abs(hi2) < 64
+        m2hi = hi2 + 33 * m2hi_c
+        assert m2hi - 33 * m2hi_c == hi2  # exact both ways
+        m2lo = lo2 + 33 * m2lo_c
+        inv, hi, lo = -m4inv / 4, -m2hi / 2, -m2lo / 2
         assert inv == 1.0 / (1.0 + i / 1024.0)
         assert hi == round(hi * 2.0**43) / 2.0**43  # k LN2_HI + T_HI exact for |k| <= 33
-        assert abs((hi + lo) - (-math.log(inv))) <= 2 * math.ulp(max(abs(hi), 1e-300)) if hi else lo == 0.0
-        assert abs(lo) <= 2.0**-43
-    assert (-log[1024][1] / 2, -log[1024][2] / 2) == (l2hi, l2lo)  # c = 2: T = ln 2 exactly as LN2_HI + LN2_LO
+        # (i = 0: T = 0; the LO entry's one rounding leaves |lo| <= 2^-85)
+        assert abs((hi + lo) - (-math.log(inv))) <= 2 * math.ulp(max(abs(hi), 1e-300)) if hi else abs(lo) <= 2.0**-85
+        assert abs(lo) <= 2.0**-43 + 2.0**-80
+    # c = 2: T = ln 2 exactly as LN2_HI + LN2_LO, so at e = 32 both sums vanish exactly
+    assert log[1024][1] == -32 * m2hi_c and log[1024][2] == -32 * m2lo_c
     for j, (s, c) in enumerate(sc):
         assert abs(s - math.sin(2 * math.pi * j / 1024)) <= 2 ** -50
         assert abs(c - math.cos(2 * math.pi * j / 1024)) <= 2 ** -50
@@ -75,3 +83,7 @@ def test_table_entries_are_near_libm() -> None:
     for k in range(1, 5):  # (ln 2 / 256)^k / k!
         assert abs(consts[f"kF64ExpE{k}"] - (math.log(2) / 256) ** k / math.factorial(k)) <= \
             2 * math.ulp(consts[f"kF64ExpE{k}"])
+    K = 2 * math.pi / 2.0**32  # sin / cos coefficients in integer angle units
+    for name, want in (("kF64SinS1", K), ("kF64SinS3", -K**3 / 6), ("kF64SinS5", K**5 / 120),
+                       ("kF64CosC2", -K**2 / 2), ("kF64CosC4", K**4 / 24)):
+        assert abs(consts[name] - want) <= 4 * math.ulp(want), name

@@ -66,7 +66,7 @@ def test_oracle_stream_span_at_small_t(oracle, rows) -> None:
     """Stream span (smc_rng.h, round 4): at T <= 2 group g (paths 4g .. 4g + 3) takes the (g mod 4)-th run
     of 4 T draws of the stream of g / 4 (one Philox-10 seed per 16 paths); T >= 3: one stream per group.
     Restated here from the raw streams and the f64 Box-Muller pieces: pair k of a group is
-    (a, b) -> sqrt(-2 ln u(a)) (cos, sin)(2 pi b 2^-32); T = 1 takes pairs 0, 1 for paths (0, 1), (2, 3);
+    (a, b) -> sqrt(-2 ln u(a)) (cos, sin)(angle(b)); T = 1 takes pairs 0, 1 for paths (0, 1), (2, 3);
     T = 2 one pair per path (z0 -> row 0, z1 -> row 1)."""
     seed, ordinal, cols = 7, 3, 64
     z = oracle.normals(seed, ordinal, rows, cols, "float64")
@@ -107,10 +107,14 @@ def test_f64_uniform_transcendentals_are_accurate(oracle) -> None:
     """The f64 normals' ln / sin / cos of 32-bit uniforms and the f64 recursion's exp (csrc/smc_math.h,
     restated in the oracle) against numpy's libm at the edges of their domains and on random points:
     within 2 ulp (log, exp); sin / cos within 2^-52 absolute of an x87 long-double evaluation of the
-    exactly reduced angle (the integer b is reduced to the nearest quarter turn before any rounding)."""
+    exactly reduced angle.  The angle of b is 2 pi B 2^-32 with B = (b mod 1024) 2^22 + (b >> 10 as a signed
+    22-bit integer) mod 2^32 (smc_math.h v4: the low bits pick the table angle); the integer B is reduced to
+    the nearest quarter turn before any rounding."""
     two_pi = np.longdouble("6.283185307179586476925286766559005768")
 
     def sincos_ld(b: int) -> tuple[float, float]:
+        y = (b >> 10) - (2**22 if b >= 2**31 else 0)
+        b = ((b & 1023) * 2**22 + y) % 2**32
         k = (b + 2**29) // 2**30
         x = two_pi * np.longdouble(b - k * 2**30) / np.longdouble(2**32)
         s_, c_ = np.sin(x), np.cos(x)
