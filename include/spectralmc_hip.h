@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 12
+#define SMC_ABI_VERSION 13
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -89,11 +89,6 @@ const char* smc_last_error_string(void);
 /* Waits for `stream`, then copies the status word of sync_dev to *status_out (0: no failure) and,
  * if clear != 0, zeroes it.  The only call of this ABI that synchronises the host. */
 int32_t smc_sync_status(void* sync_dev, int32_t clear, int32_t* status_out, void* stream);
-/* Test hook (tests/test_gpu_engine.py): for the exchanging launches enqueued after this call,
- * withhold = 1 makes slice W-1 of group 0 skip its first arrival (its partners time out), and
- * spin_limit (> 0) replaces the ~1 s poll budget.  (0, 0) restores normal operation. */
-int32_t smc_test_exchange_fault(int32_t withhold, uint32_t spin_limit);
-
 /* ---- scrambled Sobol (SciPy-bit-exact) ---------------------------------- */
 /* Build the LMS+digital-shift scrambled generator SciPy builds for
  * Sobol(d=dim, scramble=True, seed=seed), then fast_forward(skip).

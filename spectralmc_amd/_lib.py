@@ -39,7 +39,7 @@ MATH_HW = 0x100
 TRAIN_DYNAMIC = 0x200
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 
@@ -48,7 +48,6 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_abi_version": (_c_i32, []),
     "smc_last_error_string": (ctypes.c_char_p, []),
     "smc_sync_status": (_c_i32, [_c_vp, _c_i32, ctypes.POINTER(_c_i32), _c_vp]),
-    "smc_test_exchange_fault": (_c_i32, [_c_i32, ctypes.c_uint32]),
     "smc_sobol_create": (_c_i32, [_c_i32, _c_u64, _c_u64, ctypes.POINTER(_c_vp)]),
     "smc_sobol_destroy": (None, [_c_vp]),
     "smc_sobol_state": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp]),
@@ -88,6 +87,11 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_basket_sync_bytes": (_c_i64, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i64]),
     "smc_basket_train_targets_kernel": (ctypes.c_char_p, [_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32]),
     "smc_basket_resident_slots": (_c_i64, [_c_i32, _c_i32, _c_i32]),
+}
+
+# include/spectralmc_hip_testing.h: test-only entry points, inert unless SMC_ENABLE_TEST_HOOKS=1
+TEST_SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
+    "smc_test_exchange_fault": (_c_i32, [_c_i32, ctypes.c_uint32]),
 }
 
 CVNN_MAX_LAYERS = 8
@@ -143,7 +147,7 @@ def lib() -> ctypes.CDLL:
                     f"{LIB_PATH} not found: build it with `python __graft_entry__.py` "
                     "(hipcc --offload-arch=gfx950); there is no CPU fallback")
             handle = ctypes.CDLL(LIB_PATH)
-            for name, (restype, argtypes) in SIGNATURES.items():
+            for name, (restype, argtypes) in {**SIGNATURES, **TEST_SIGNATURES}.items():
                 fn = getattr(handle, name)
                 fn.restype = restype
                 fn.argtypes = argtypes

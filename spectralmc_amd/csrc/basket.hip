@@ -41,9 +41,6 @@ constexpr int kBWaves = kBThreads / 64;
 constexpr int kBPaths = 4;                      // paths per lane
 constexpr int kBChunk = kBThreads * kBPaths;    // paths per workgroup pass
 constexpr int kMaxAssets = 8;
-#ifndef SMC_BASKET_MIN_BLOCKS
-#define SMC_BASKET_MIN_BLOCKS 1
-#endif
 constexpr double kBLog2e = 1.4426950408889634;
 
 struct BasketArgs {
@@ -167,7 +164,7 @@ __device__ void basket_cf(const BasketArgs& a, int64_t b, const double* tot, dou
 }
 
 template <int A, bool HW, int MODE>  // MODE 0: simulate + CF, 1: simulate only (terminal sums out)
-__global__ __launch_bounds__(kBThreads, SMC_BASKET_MIN_BLOCKS) void basket_kernel(BasketArgs a) {
+__global__ __launch_bounds__(kBThreads) void basket_kernel(BasketArgs a) {
   typedef float v4f __attribute__((ext_vector_type(4)));
   typedef float f2 __attribute__((ext_vector_type(2)));
   extern __shared__ double lds[];
@@ -412,10 +409,8 @@ __global__ __launch_bounds__(kRThreads) void basket_resident_kernel(BasketResArg
   // finish times differed by up to 15 % with a static split).  Slice 0 takes the contract of
   // iteration j + 2 while publishing iteration j's slice sums; the partners read it with those sums
   // in iteration j + 1 (no added wait).
-#ifndef SMC_BASKET_STATIC_QUARTERS
-#define SMC_BASKET_STATIC_QUARTERS 3  // statically assigned share of the iterations, in quarters
-#endif
-  const int64_t S = (a.B / groups) * SMC_BASKET_STATIC_QUARTERS / 4;
+  constexpr int64_t kStaticQuarters = 3;  // statically assigned share of the iterations, in quarters
+  const int64_t S = (a.B / groups) * kStaticQuarters / 4;
   const bool dyn = S >= 2;
   const int64_t n_static = dyn ? S * groups : a.B;
   uint32_t* queue = reinterpret_cast<uint32_t*>(ra.sync + 64);
@@ -669,14 +664,12 @@ size_t basket_cf_lds_bytes(int N) {
 
 // Split (basket_kernel<1> then basket_cf_kernel) when the caller keeps the terminal sums: the CF
 // re-read then streams at full read bandwidth instead of stalling each workgroup's store queue
-// (as the single-asset paths_kernel + cf_kernel pair; SMC_BASKET_SPLIT=0 builds keep the fused kernel)
-#ifndef SMC_BASKET_SPLIT
-#define SMC_BASKET_SPLIT 1
-#endif
+// (as the single-asset paths_kernel + cf_kernel pair; kBasketSplit = false keeps the fused kernel)
+constexpr bool kBasketSplit = true;
 
 template <int A, bool HW>
 const void* basket_kernel_ptr() {
-  return reinterpret_cast<const void*>(basket_kernel<A, HW, SMC_BASKET_SPLIT ? 1 : 0>);
+  return reinterpret_cast<const void*>(basket_kernel<A, HW, kBasketSplit ? 1 : 0>);
 }
 
 // Workgroups of the kernel launched for <A, HW, N> resident on the current device (occupancy x CUs).
@@ -711,7 +704,7 @@ int32_t launch_basket_mode(const BasketArgs& a, hipStream_t stream) {
 
 template <int A, bool HW>
 int32_t launch_basket_k(const BasketArgs& a, hipStream_t stream) {
-  if (!SMC_BASKET_SPLIT || !a.terminal_sum) return launch_basket_mode<A, HW, 0>(a, stream);
+  if (!kBasketSplit || !a.terminal_sum) return launch_basket_mode<A, HW, 0>(a, stream);
   if (int32_t st = launch_basket_mode<A, HW, 1>(a, stream)) return st;
   const size_t lds = basket_cf_lds_bytes(a.N);
   auto cf = basket_cf_kernel<A>;
@@ -894,7 +887,7 @@ const char* smc_basket_train_targets_kernel(int32_t n_assets, int32_t timesteps,
   if (with_sync && n_assets >= 1 && n_assets <= kMaxAssets && network_size > 0 && batches_per_mc_run > 0 &&
       basket_res_slices(n_assets, timesteps, network_size, batches_per_mc_run) > 0)
     return "basket_resident_kernel";
-  return keep_sums && SMC_BASKET_SPLIT ? "basket_kernel+basket_cf_kernel" : "basket_kernel";
+  return keep_sums && kBasketSplit ? "basket_kernel+basket_cf_kernel" : "basket_kernel";
 }
 
 int64_t smc_basket_resident_slots(int32_t n_assets, int32_t network_size, int32_t math) {

@@ -1,9 +1,11 @@
 // C-ABI housekeeping of libspectralmc_hip.so: ABI version, per-thread error text, the sync-area
-// status word of the exchanging launches, and the exchange-fault test hook.
+// status word of the exchanging launches, and the exchange-fault test hook (spectralmc_hip_testing.h).
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 
+#include "../../include/spectralmc_hip_testing.h"
 #include "smc_internal.h"
 
 namespace smc {
@@ -51,7 +53,14 @@ int32_t smc_sync_status(void* sync_dev, int32_t clear, int32_t* status_out, void
   return SMC_OK;
 }
 
+// spectralmc_hip_testing.h: inert unless SMC_ENABLE_TEST_HOOKS=1 (read once, at the first call)
 int32_t smc_test_exchange_fault(int32_t withhold, uint32_t spin_limit) {
+  static const bool enabled = [] {
+    const char* e = getenv("SMC_ENABLE_TEST_HOOKS");
+    return e != nullptr && e[0] == '1' && e[1] == '\0';
+  }();
+  if (!enabled)
+    return smc::fail(SMC_ERR_INVALID_ARGUMENT, "smc_test_exchange_fault: test hooks disabled (SMC_ENABLE_TEST_HOOKS=1)");
   if (withhold != 0 && withhold != 1) return smc::fail(SMC_ERR_INVALID_ARGUMENT, "smc_test_exchange_fault: withhold");
   smc::g_fault_withhold.store(withhold);
   smc::g_fault_spin_limit.store(spin_limit);

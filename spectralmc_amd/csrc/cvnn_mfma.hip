@@ -543,15 +543,12 @@ __device__ void wgrad_bookkeeping(const MArgs& a, int64_t item, int wave, int la
   }
 }
 
-#ifndef SMC_WGRAD_ROWMAJOR
-#define SMC_WGRAD_ROWMAJOR 1  // layered plans: wgrad reads Z_l / dU_l row-major, lgemm writes no ^T copies
-#endif
-#ifndef SMC_WGRAD_KS_F32
+// (settled values; tools/micro/make_variant.py edits these lines for A/B builds)
+constexpr bool kWgradRowMajor = true;  // layered plans: wgrad reads Z_l / dU_l row-major, lgemm writes no ^T copies
 // f32 batch rows per K stage: 16 (20 KiB of LDS, 8 workgroups per CU) runs C2/H = 256's 1216 weight-
 // gradient items in one round where 32 (36 KiB, 4 per CU) left a second round of 192 (round-4 A/B:
 // isolated H = 256 network 251-253 -> 243 us, profiles/r04/ab_wgrad_stage.txt)
-#define SMC_WGRAD_KS_F32 16
-#endif
+constexpr int kWgradKsF32 = 16;
 constexpr int kWgBlock = 64;  // output block edge
 constexpr int kWgStage = 64;  // batch rows per K stage (bf16; 32 for f32: the same 36 KiB of LDS)
 
@@ -594,7 +591,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(MArgs a) {
   using V = typename Op::V;
   constexpr int KB = Op::KB, KQ = KB / 4;
   constexpr int ES = static_cast<int>(sizeof(T));
-  constexpr int KS = ES == 2 ? kWgStage : SMC_WGRAD_KS_F32;  // batch rows per K stage
+  constexpr int KS = ES == 2 ? kWgStage : kWgradKsF32;  // batch rows per K stage
   constexpr int LD = KS + 16 / ES;                       // LDS row stride (elements): odd multiple of 16 B
   constexpr int PER = kWgBlock * KS / kThreads;          // elements each thread stages per operand
   constexpr int NV = PER * ES / 16;                   // 16-byte loads per operand per thread
@@ -772,27 +769,15 @@ __global__ __launch_bounds__(kThreads) void wgrad_rm_kernel(MArgs a) {
 //   kLLast (last layer): prediction, loss partial, output gradient -> dU_L (row-major and ^T)
 //   kLBwd  (layer l, l >= 1): dZ_l = dU_l Wc_l, layer l-1's activation backward -> dU_{l-1}
 // wgrad_kernel then reads the ^T copies exactly as after fb_kernel (same partials, same reduction).
-#ifndef SMC_LGEMM_K
-#define SMC_LGEMM_K 64
-#endif
-#ifndef SMC_LGEMM_M
-#define SMC_LGEMM_M 64
-#endif
-#ifndef SMC_LGEMM_N
-#define SMC_LGEMM_N 64
-#endif
 // LDS row stride kLK + 8 floats: a ds_read_b128 fragment (lane 16 g + c: row c, 16 B at 16 g) is serviced in
 // four 16-lane groups ({0-3, 12-15, 20-27}, ...; MI355X_MICROARCH.md, LDS), and at stride 68 every group
 // had two lanes on one bank quad (PMC: 1.4e6 conflict cycles per H = 256 GEMM); 72 is conflict-free
-constexpr int kLM = SMC_LGEMM_M, kLN = SMC_LGEMM_N, kLK = SMC_LGEMM_K, kLLd = kLK + 8;  // tile (features x batch rows), K stage, LDS stride
-#ifndef SMC_LGEMM_THREADS
-#define SMC_LGEMM_THREADS 512
-#endif
+constexpr int kLM = 64, kLN = 64, kLK = 64, kLLd = kLK + 8;  // tile (features x batch rows), K stage, LDS stride
 // waves: 4 along the features (kLM / 4 each) x kLWR along the batch rows (kLN / kLWR each); kLM = 64: 512
 // workgroups at H = 256 (263 vs 269 us per step with 128).  8 waves (2 row groups): 4 waves per SIMD at two
 // workgroups per CU, the isolated H = 256 network 237-240 -> 228-230 us against 4 waves
 // (profiles/r04/net/ab_lgemm_waves.txt)
-constexpr int kLThreads = SMC_LGEMM_THREADS;
+constexpr int kLThreads = 512;
 constexpr int kLWF = 4, kLWR = kLThreads / 64 / kLWF;
 constexpr int kLTM = kLM / kLWF / 16, kLTN = kLN / kLWR / 16;  // 16 x 16 tiles per wave
 enum { kLFwd = 0, kLLast = 1, kLBwd = 2 };
@@ -883,7 +868,7 @@ __device__ __forceinline__ void lgemm_prefetch(const MArgs& a, int l, int m0, in
 
 // ---- epilogue, from the [row][feature] tile of the accumulators in LDS (written and synchronised by
 // the caller): each thread takes 4 features of one batch row (row-major outputs, 16-B stores along the
-// features) and finally, without SMC_WGRAD_ROWMAJOR, whole 64-row feature lines (the ^T copies, 16-B
+// features) and finally, without kWgradRowMajor, whole 64-row feature lines (the ^T copies, 16-B
 // stores along the batch): every global store is a full 16-B piece of a contiguous line
 constexpr int kLTld = kLM + 4;  // tile row stride (floats): [row][feature], 16-B pieces conflict-free
 template <int MODE>
@@ -947,7 +932,7 @@ __device__ __forceinline__ void lgemm_epilogue(const MArgs& a, int l, int mb, in
       }
     }
     if (f0 < nvalid) *reinterpret_cast<f32x4*>(ws + rm_off + b * rm_ld + f0) = f32x4{o[0], o[1], o[2], o[3]};
-    if constexpr (!SMC_WGRAD_ROWMAJOR)
+    if constexpr (!kWgradRowMajor)
       *reinterpret_cast<f32x4*>(&tile[rr * kLTld + 4 * q]) = f32x4{o[0], o[1], o[2], o[3]};  // the ^T copy's values
   }
   if constexpr (MODE != kLFwd) {
@@ -978,7 +963,7 @@ __device__ __forceinline__ void lgemm_epilogue(const MArgs& a, int l, int mb, in
     __syncthreads();
   }
   // phase C: the ^T copy, whole 64-row lines of each feature (only for the transposed wgrad_kernel)
-  for (int e = tid; e < (SMC_WGRAD_ROWMAJOR ? 0 : kLM * (kLN / 4)); e += kLThreads) {
+  for (int e = tid; e < (kWgradRowMajor ? 0 : kLM * (kLN / 4)); e += kLThreads) {
     const int fr = e / (kLN / 4), q4 = e % (kLN / 4);
     if (m0 + fr < nvalid)
       *reinterpret_cast<f32x4*>(ws + tr_off + static_cast<int64_t>(m0 + fr) * bp + n0 + 4 * q4) =
@@ -993,7 +978,7 @@ __device__ __forceinline__ void lgemm_epilogue(const MArgs& a, int l, int mb, in
         const int64_t b = n0 + e % kLN;
         const float v = k == 2 * ly.no ? 1.0f : 0.0f;
         ws[nx.zr + b * nx.kx + k] = v;
-        if constexpr (!SMC_WGRAD_ROWMAJOR) ws[nx.zt + static_cast<int64_t>(k) * bp + b] = v;
+        if constexpr (!kWgradRowMajor) ws[nx.zt + static_cast<int64_t>(k) * bp + b] = v;
       }
     }
   }
@@ -1293,7 +1278,7 @@ int32_t launch_fb(const Plan& p, hipStream_t s) {
 int32_t launch_layered(const Plan& p, hipStream_t s) {
   const MArgs& a = p.a;
   // (row-major wgrad: no Z_0^T region)
-  hipLaunchKernelGGL(lpack_kernel, dim3(256, 2 * a.n_layers + (SMC_WGRAD_ROWMAJOR ? 1 : 2)), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(lpack_kernel, dim3(256, 2 * a.n_layers + (kWgradRowMajor ? 1 : 2)), dim3(kThreads), 0, s, a);
   if (int32_t rc = check_launch("cvnn lpack_kernel")) return rc;
   const unsigned by = static_cast<unsigned>(a.bp / kLN);
   const int L = a.n_layers;
@@ -1314,9 +1299,9 @@ int32_t launch_layered(const Plan& p, hipStream_t s) {
   }
   // weight gradients in wgrad_kernel's 64 x 64 blocks over batch segments (they measured faster here than
   // this file's GEMM tile: 70 vs 74-81 us at C2/H=256), from the row-major Z_l / dU_l (wgrad_rm_kernel,
-  // round 4) or, without SMC_WGRAD_ROWMAJOR, from ^T copies as after fb_kernel
-  if (SMC_WGRAD_ROWMAJOR)
-    hipLaunchKernelGGL(wgrad_rm_kernel<SMC_WGRAD_KS_F32>, dim3(p.wgrad_grid), dim3(kThreads), 0, s, a);
+  // round 4) or, without kWgradRowMajor, from ^T copies as after fb_kernel
+  if (kWgradRowMajor)
+    hipLaunchKernelGGL(wgrad_rm_kernel<kWgradKsF32>, dim3(p.wgrad_grid), dim3(kThreads), 0, s, a);
   else
     hipLaunchKernelGGL(wgrad_kernel<OpF32>, dim3(p.wgrad_grid), dim3(kThreads), 0, s, a);
   return check_launch("cvnn wgrad_kernel");

@@ -40,22 +40,10 @@ namespace {
 // f64: two 8-wave workgroups per CU (4 waves per SIMD) whatever the budget between 4 and 5 waves, and the
 // 4-wave budget (97 VGPRs) measured 8.27-8.28 against 8.34-8.35 ms for rows + cf at 5 (91 VGPRs)
 // (profiles/r04/ab_f64_waves4.txt)
-#ifndef SMC_ROWS_WAVES_F64
-#define SMC_ROWS_WAVES_F64 4
-#endif
-#ifndef SMC_ROWS_WAVES
-#define SMC_ROWS_WAVES 8
-#endif
-#ifndef SMC_WG_THREADS
-#define SMC_WG_THREADS 512
-#endif
-#ifndef SMC_MIN_LDS
-#define SMC_MIN_LDS 0
-#endif
-#ifndef SMC_MIN_BLOCKS
-#define SMC_MIN_BLOCKS 1
-#endif
-constexpr int kThreads = SMC_WG_THREADS;
+// (settled values; tools/micro/make_variant.py edits these lines for A/B builds)
+constexpr int kRowsWavesF64 = 4;
+constexpr int kRowsWaves = 8;
+constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
 constexpr int kPathsPerLane = 4;
 constexpr int kChunk = kThreads * kPathsPerLane;
@@ -126,10 +114,7 @@ struct EngineArgs {
   int32_t withhold;
 };
 
-#ifndef SMC_SLICE_CHUNKS
-#define SMC_SLICE_CHUNKS 4
-#endif
-constexpr int kSliceChunks = SMC_SLICE_CHUNKS;  // chunks (of kChunk paths) per workgroup when sliced
+constexpr int kSliceChunks = 4;  // chunks (of kChunk paths) per workgroup when sliced
 
 
 
@@ -652,10 +637,7 @@ __device__ void cf_targets_contract(const EngineArgs& a, const Contract& c, int6
   double* cs = avg + N;                                          // [N]
   double* sn = cs + N;                                           // [N]
 
-#ifndef SMC_CF_BATCH
-#define SMC_CF_BATCH 8
-#endif
-  constexpr int kBatch = SMC_CF_BATCH;  // loads in flight per thread; the sum keeps the m order
+  constexpr int kBatch = 8;  // loads in flight per thread; the sum keeps the m order
   if constexpr (sizeof(Real) == 4) {
     if (quad) quad_column_sums<kBatch>(row, pay, N, M, cols, G, part, tid, kThreads);
   }
@@ -747,7 +729,7 @@ __device__ void run_slice(const EngineArgs& a, int64_t b, int k, double* lds, in
 
 // One workgroup per contract (slices == 1).
 template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
-__global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void contract_kernel(EngineArgs a) {
+__global__ __launch_bounds__(kThreads) void contract_kernel(EngineArgs a) {
   extern __shared__ double lds[];
   __shared__ int flag;
   if constexpr (sizeof(Real) == 8) math::f64_tables_load();
@@ -830,14 +812,14 @@ __global__ __launch_bounds__(kThreads) void cf_kernel(EngineArgs a) {
 // counter, for workgroups that start late beside a network kernel) cost a store drain per contract at
 // its queue barrier, and rows shapes run the step on one stream anyway (round 4, C2-f64: rows_kernel
 // 7.64 ms with the queue against ~6.9 without).
-// f64 rows: SMC_ROWS_WAVES_F64 sets the register budget (round 4 A/Bs on MI355X, C2-f64: v2 math 9.01 ms
+// f64 rows: kRowsWavesF64 sets the register budget (round 4 A/Bs on MI355X, C2-f64: v2 math 9.01 ms
 // at 6 vs 9.20-9.28 ms at 8 waves, and 9.49-9.53 ms with the CF phase fused into this kernel, which then
 // re-read the terminal row while its own path math waited; v3 math 8.47-8.50 ms at 5 vs 8.65-8.67 ms at
 // 6, where the 80-VGPR budget spilled outside the path loop): the larger register budget is worth more
 // than the sixth wave.
 template <typename Real, bool LOG_EULER, bool HW, bool STORE_ALL>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof(Real) == 8 ? SMC_ROWS_WAVES_F64
-                                                                                              : SMC_ROWS_WAVES)))
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof(Real) == 8 ? kRowsWavesF64
+                                                                                              : kRowsWaves)))
 void rows_kernel(EngineArgs a) {
   extern __shared__ double lds[];
   if constexpr (sizeof(Real) == 8) math::f64_tables_load();
@@ -1526,7 +1508,7 @@ bool rows_ok(const EngineArgs& a, bool f32) {
 // runs whatever is left in any queue (an XCD without workgroups) before resetting the counters.
 // queues[0..7]: next item per queue, queues[8]: workgroups done; all zero between launches.
 template <typename Real, bool LOG_EULER, bool HW, bool ALLROWS>
-__global__ __launch_bounds__(kThreads, SMC_MIN_BLOCKS) void queue_kernel(EngineArgs a) {
+__global__ __launch_bounds__(kThreads) void queue_kernel(EngineArgs a) {
   extern __shared__ double lds[];
   __shared__ int flag;
   __shared__ int64_t next_item;
@@ -1617,7 +1599,7 @@ size_t lds_bytes(int T, int N, bool cf) {
     if (cfw > work) work = cfw;
   }
   const size_t bytes = (doubles + work) * sizeof(double);
-  return bytes < SMC_MIN_LDS ? SMC_MIN_LDS : bytes;
+  return bytes;
 }
 
 // Resident workgroups of a persistent kernel on the current device (occupancy x CUs, cached
@@ -1705,16 +1687,8 @@ size_t workspace_bytes(int64_t B, int32_t T, int64_t P, bool all_rows) {
   return static_cast<size_t>(B) * W * (all_rows ? T : 1) * sizeof(double) + static_cast<size_t>(B + 16) * sizeof(uint32_t);
 }
 
-// Resident paths_kernel workgroups per CU (its ~42 VGPRs allow 4 x 512 threads); the
-// SMC_PATHS_WGS_PER_CU environment variable overrides (tuning only: results do not depend on it).
-int paths_wgs_per_cu() {
-  static const int v = [] {
-    const char* e = getenv("SMC_PATHS_WGS_PER_CU");
-    const int x = e ? atoi(e) : 4;
-    return x >= 1 && x <= 8 ? x : 4;
-  }();
-  return v;
-}
+// Resident paths_kernel workgroups per CU (its ~42 VGPRs allow 4 x 512 threads)
+constexpr int kPathsWgsPerCu = 4;
 
 template <bool LOG_EULER, bool HW, bool STRAIGHT, bool STORE_ALL>
 int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
@@ -1731,14 +1705,14 @@ int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
     return fail(SMC_ERR_HIP, "paths_kernel / cf_kernel: cannot raise the dynamic LDS limit");
   }
   unsigned grid1 = static_cast<unsigned>(a.B);
-  if (STRAIGHT) {  // persistent: paths_wgs_per_cu() resident workgroups per CU
+  if (STRAIGHT) {  // persistent: kPathsWgsPerCu resident workgroups per CU
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
       (void)hipGetLastError();
       return fail(SMC_ERR_HIP, "paths_kernel: device query failed");
     }
-    const int64_t slots = static_cast<int64_t>(paths_wgs_per_cu()) * cus;
+    const int64_t slots = static_cast<int64_t>(kPathsWgsPerCu) * cus;
     if (slots < a.B) grid1 = static_cast<unsigned>(slots);
   }
   hipLaunchKernelGGL(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
@@ -1836,17 +1810,12 @@ int32_t launch_packed_k(const EngineArgs& a, hipStream_t stream) {
   return check_launch("packed_kernel");
 }
 
-// Training-shape kernel choice: 3 = resident_kernel where it applies (P <= 65,536), else the
-// paths_kernel + cf_kernel pair (2); 0 = the fused contract_kernel (tools/micro comparison builds)
-#ifndef SMC_TRAIN_MODE
-#define SMC_TRAIN_MODE 3
-#endif
 
 template <typename Real>
 int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   if (a.B == 0) return SMC_OK;
   if constexpr (sizeof(Real) == 4) {
-    if (SMC_TRAIN_MODE == 3 && wave_ok(a, true)) {  // RAW, T <= 2: one wave per contract
+    if (wave_ok(a, true)) {  // RAW, T <= 2: one wave per contract
       const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
       const bool hw = (a.scheme & SMC_MATH_HW) != 0;
       const bool sa = a.store == SMC_STORE_ALL;
@@ -1862,7 +1831,7 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
       SMC_WAVE(false, false, false)
 #undef SMC_WAVE
     }
-    if (SMC_TRAIN_MODE == 3 && resident_ok(a, true)) {
+    if (resident_ok(a, true)) {
       const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
       const bool hw = (a.scheme & SMC_MATH_HW) != 0;
       const bool sa = a.store == SMC_STORE_ALL;
@@ -1878,7 +1847,7 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
       SMC_RES(false, false, false)
 #undef SMC_RES
     }
-    if (SMC_TRAIN_MODE == 3 && packed_ok(a, true)) {  // small P: several contracts per workgroup
+    if (packed_ok(a, true)) {  // small P: several contracts per workgroup
       const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
       const bool hw = (a.scheme & SMC_MATH_HW) != 0;
       const bool sa = a.store == SMC_STORE_ALL;
@@ -1897,7 +1866,7 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
     // the split pair: the straight-line T = 16 paths_kernel, or (ragged chunks) simulate_contract;
     // other whole-chunk shapes take rows_kernel below
     const bool straight_split = a.T == kRowBlock && a.P % kChunk == 0;
-    if (SMC_TRAIN_MODE >= 2 && split_ok(a, true) && (straight_split || !rows_ok(a, true))) {
+    if (split_ok(a, true) && (straight_split || !rows_ok(a, true))) {
       const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
       const bool hw = (a.scheme & SMC_MATH_HW) != 0;
       const bool straight = straight_split;
@@ -1919,7 +1888,7 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
 #undef SMC_SPLIT
     }
   }
-  if (SMC_TRAIN_MODE >= 2 && rows_ok(a, sizeof(Real) == 4)) {
+  if (rows_ok(a, sizeof(Real) == 4)) {
     const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
     const bool hw = (a.scheme & SMC_MATH_HW) != 0 && sizeof(Real) == 4;
     const bool sa = a.store == SMC_STORE_ALL;
@@ -2156,7 +2125,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
     a.res_xsum = reinterpret_cast<double*>(sync + l.xsum_off);
     a.res_xcol = reinterpret_cast<double*>(sync + l.xcol_off);
   }
-  const bool fused = SMC_TRAIN_MODE == 3 && dtype == SMC_DTYPE_F32 && n_contracts > 0 && chunk_contracts > 0 &&
+  const bool fused = dtype == SMC_DTYPE_F32 && n_contracts > 0 && chunk_contracts > 0 &&
                      valid_scheme(scheme) && (store_mode == SMC_STORE_ALL || store_mode == SMC_STORE_TERMINAL) &&
                      paths_dev && targets_dev && (wave_ok(a, true) || resident_ok(a, true) || packed_ok(a, true));
   if (fused) {
@@ -2210,7 +2179,7 @@ int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32
   a.res_cnt = reinterpret_cast<uint32_t*>(&a);  // any non-null: the shape test only
   a.res_xsum = a.res_xcol = reinterpret_cast<double*>(&a);
   a.done = reinterpret_cast<uint32_t*>(&a);
-  if (!(SMC_TRAIN_MODE == 3 && resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))) return kStepSyncBytes;
+  if (!(resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))) return kStepSyncBytes;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0) {
@@ -2235,8 +2204,8 @@ const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32
   a.res_xsum = a.res_xcol = reinterpret_cast<double*>(&a);
   a.done = reinterpret_cast<uint32_t*>(&a);
   a.normalize = (dtype & SMC_QUERY_RAW) ? 0 : 1;
-  if (SMC_TRAIN_MODE == 3 && wave_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "wave_kernel";
-  if (SMC_TRAIN_MODE == 3 && resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))
+  if (wave_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "wave_kernel";
+  if (resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))
     return a.res_slices > 1 ? "resident_kernel(sliced)" : "resident_kernel";
   return smc_train_targets_kernel(timesteps, network_size, a.P, dtype, path_pitch, 0);
 }
@@ -2259,12 +2228,12 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.store = SMC_STORE_ALL;
   const bool f32 = (dtype & 0xff) == SMC_DTYPE_F32;
   a.normalize = (dtype & SMC_QUERY_RAW) ? 0 : 1;
-  if (SMC_TRAIN_MODE == 3 && wave_ok(a, f32)) return "wave_kernel";
-  if (SMC_TRAIN_MODE == 3 && resident_ok(a, f32)) return "resident_kernel";
-  if (SMC_TRAIN_MODE == 3 && packed_ok(a, f32)) return "packed_kernel";
-  if (SMC_TRAIN_MODE >= 2 && split_ok(a, f32) && a.T == kRowBlock && a.P % kChunk == 0) return "paths_kernel+cf_kernel";
-  if (SMC_TRAIN_MODE >= 2 && rows_ok(a, f32)) return "rows_kernel+cf_kernel";
-  if (SMC_TRAIN_MODE >= 2 && split_ok(a, f32)) return "paths_kernel+cf_kernel";
+  if (wave_ok(a, f32)) return "wave_kernel";
+  if (resident_ok(a, f32)) return "resident_kernel";
+  if (packed_ok(a, f32)) return "packed_kernel";
+  if (split_ok(a, f32) && a.T == kRowBlock && a.P % kChunk == 0) return "paths_kernel+cf_kernel";
+  if (rows_ok(a, f32)) return "rows_kernel+cf_kernel";
+  if (split_ok(a, f32)) return "paths_kernel+cf_kernel";
   return a.slices > 1 ? "queue_kernel" : "contract_kernel";
 }
 

@@ -19,6 +19,8 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the exchange-fault hook of include/spectralmc_hip_testing.h is inert without this (read at its first call)
+os.environ.setdefault("SMC_ENABLE_TEST_HOOKS", "1")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 

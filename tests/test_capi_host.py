@@ -7,6 +7,8 @@ from __future__ import annotations
 import ctypes
 import os
 import re
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -16,10 +18,11 @@ from spectralmc_amd import _lib
 from spectralmc_amd.sobol_sampler import SobolEngine
 
 HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "spectralmc_hip.h")
+TESTING_HEADER = os.path.join(os.path.dirname(HEADER), "spectralmc_hip_testing.h")
 
 
-def declared_symbols() -> list[str]:
-    text = open(HEADER).read()
+def declared_symbols(header: str = HEADER) -> list[str]:
+    text = open(header).read()
     return sorted(set(re.findall(r"\b(smc_[a-z0-9_]+)\s*\(", text)))
 
 
@@ -31,6 +34,22 @@ def test_library_exports_every_declared_symbol() -> None:
         assert hasattr(L, name), name
     assert set(names) == set(_lib.SIGNATURES), "ctypes signature table out of sync with the header"
     assert L.smc_abi_version() == _lib.ABI_VERSION
+    # the test-only entry points live in their own header and signature table, none in the product ABI
+    testing = declared_symbols(TESTING_HEADER)
+    assert testing == sorted(_lib.TEST_SIGNATURES) and not set(testing) & set(names)
+    for name in testing:
+        assert hasattr(L, name), name
+
+
+def test_test_hooks_are_inert_without_the_environment_switch() -> None:
+    """smc_test_exchange_fault does nothing and fails unless SMC_ENABLE_TEST_HOOKS=1 (a fresh process
+    without it; no GPU call)."""
+    code = ("import ctypes, sys; sys.path.insert(0, %r); from spectralmc_amd import _lib; L = _lib.lib(); "
+            "print(L.smc_test_exchange_fault(1, 5), _lib.last_error())" % os.path.dirname(os.path.dirname(HEADER)))
+    env = {k: v for k, v in os.environ.items() if k != "SMC_ENABLE_TEST_HOOKS"}
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split()[0] == str(_lib.SMC_ERR_INVALID_ARGUMENT) and "disabled" in out.stdout
 
 
 INTEGRATION = os.path.join(os.path.dirname(HEADER), "..", "INTEGRATION.md")
