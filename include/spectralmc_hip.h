@@ -60,6 +60,12 @@ extern "C" {
 #define SMC_MATH_HW          0x100  /* flag, OR into `scheme` (engine calls) or `dtype` (smc_normals):
                                       f32 hardware transcendentals (v_exp/v_log/v_sin/v_cos/v_sqrt)
                                       instead of the portable, CPU-reproducible kernels */
+#define SMC_MATH_REF         0x400  /* flag, OR into smc_train_targets' / smc_train_step's `scheme` (f32
+                                      only, not with SMC_MATH_HW): the reference kernel's own typing
+                                      (gbm.py:224-257 under Numba: f64 state and step of the f32 normals,
+                                      f32 stores): portable normals, the f64 engine's step, rounded f32
+                                      paths (rows_ref_kernel + cf_kernel); in the kernel queries' dtype:
+                                      that kernel's name */
 #define SMC_TRAIN_DYNAMIC    0x200  /* flag, OR into smc_train_step's `scheme`: the whole-contract resident
                                       launch hands out every contract from its contract queue (default:
                                       the first three quarters of the rounds statically), for launches that
@@ -182,7 +188,7 @@ int64_t smc_train_step_sync_bytes(int32_t timesteps, int32_t network_size, int32
 /* Name of the kernel smc_train_step launches for this shape ("resident_kernel",
  * "resident_kernel(sliced)", or smc_train_targets_kernel's name).  Static string.  dtype may carry
  * SMC_QUERY_RAW: the shape's targets use RAW normalisation (one-wave-per-contract shapes); a bit of its
- * own (ABI 12: it was 0x100, SMC_MATH_HW's bit in smc_normals' dtype). */
+ * own (ABI 12: it was 0x100, SMC_MATH_HW's bit in smc_normals' dtype); and SMC_MATH_REF (ABI 13). */
 #define SMC_QUERY_RAW 0x1000
 const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32_t batches_per_mc_run,
                                   int32_t dtype, int64_t path_pitch);
@@ -190,8 +196,9 @@ const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32
 int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, int64_t n_paths,
                                    int32_t all_rows);
 /* Name of the kernel smc_train_targets launches for this shape ("wave_kernel", "resident_kernel",
- * "packed_kernel", the split pairs, "contract_kernel" or "queue_kernel"; sliced = a workspace is
- * passed; dtype | SMC_QUERY_RAW as for smc_train_step_kernel).  Static string. */
+ * "packed_kernel", the split pairs, "contract_kernel", "queue_kernel" or "rows_ref_kernel+cf_kernel";
+ * sliced = a workspace is passed; dtype | SMC_QUERY_RAW | SMC_MATH_REF as for smc_train_step_kernel).
+ * Static string. */
 const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, int64_t n_paths,
                                      int32_t dtype, int64_t path_pitch, int32_t sliced);
 /* Recommended row pitch (elements) for a path scratch buffer of n_paths columns: the row

@@ -457,6 +457,11 @@ int32_t oracle_num_threads(void) {
 void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t P, uint64_t seed, int64_t ordinal0,
                          int32_t scheme, int64_t slice_paths, int32_t wg, float* paths, float* terminal,
                          double* rowsum) {
+  /* scheme | 0x400 (SMC_MATH_REF, gbm.hip rows_ref_kernel): the reference kernel's typing -- the f64
+   * engine's step (Stepper<double>: a, b in f64, units of ln 2 / 256 for log-Euler, mul_exp2s_f64) of the
+   * portable f32 normals, the state kept in f64 and stored rounded to f32 */
+  const int step64 = (scheme & 0x400) != 0;
+  scheme &= 0xff;
   /* wg: lanes of the engine workgroup (512: contract/paths/queue kernels; 1024: resident_kernel) —
    * sets the chunk (4 wg paths) and the wave count of the row-sum order */
   const int lanes = wg > 0 ? wg : K_THREADS;
@@ -478,6 +483,15 @@ void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t 
       ca = (float)((c[3] - c[4]) * dt);
       cb = (float)(c[5] * sq);
     }
+    double ca64, cb64;
+    if (scheme == 0) {
+      const double drift = c[3] - c[4] - 0.5 * c[5] * c[5];
+      ca64 = drift * dt * 369.3299304675746; /* smc_math.h kExpUnit = 256 / ln 2 */
+      cb64 = c[5] * sq * 369.3299304675746;
+    } else {
+      ca64 = (c[3] - c[4]) * dt;
+      cb64 = c[5] * sq;
+    }
     const float x0 = (float)c[0];
     const uint64_t ordinal = (uint64_t)(ordinal0 + b);
     const int64_t groups = (P + GROUP - 1) / GROUP;
@@ -491,12 +505,18 @@ void oracle_kernel_paths(const double* contracts, int64_t B, int32_t T, int64_t 
           const int64_t p = gi * GROUP + j;
           if (p >= P) break;
           float x = x0;
+          double x64 = c[0];
           for (int t = 0; t < T; ++t) {
             const float zt = (float)z[(int64_t)t * GROUP + j];
-            if (scheme == 0)
+            if (step64) {
+              const double y = fma(cb64, (double)zt, ca64);
+              x64 = scheme == 0 ? oracle_mul_exp2s_f64(x64, y) : fabs(fma(x64, y, x64));
+              x = (float)x64;
+            } else if (scheme == 0) {
               x = x * exp2_any(fmaf(cb, zt, ca));
-            else
+            } else {
               x = fabsf(fmaf(x, fmaf(cb, zt, ca), x));
+            }
             X[(int64_t)t * P + p] = x;
           }
         }

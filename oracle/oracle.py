@@ -231,6 +231,9 @@ def training_targets(contracts: np.ndarray, timesteps: int, network_size: int, b
 # --------------------------------------------------------------------------- kernel mode
 # paths per workgroup slice when smc_train_targets gets a workspace (gbm.hip kSliceChunks * kChunk)
 SLICE_PATHS = 8192
+# scheme flag (spectralmc_hip.h SMC_MATH_REF): kernel mode of rows_ref_kernel -- the reference kernel's
+# typing, f64 state and step (the f64 engine's exp) of the portable f32 normals, f32 stores
+MATH_REF = 0x400
 
 
 def kernel_paths(contracts: np.ndarray, timesteps: int, n_paths: int, seed: int, ordinal0: int = 0,

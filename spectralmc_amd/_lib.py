@@ -37,6 +37,7 @@ QUERY_RAW = 0x1000  # smc_train_step_kernel / smc_train_targets_kernel: the targ
 STORE_TERMINAL = 1
 MATH_HW = 0x100
 TRAIN_DYNAMIC = 0x200
+MATH_REF = 0x400  # the reference kernel's typing: f64 state and step, f32 normals and stores
 STORE_ALL = 2
 SOBOL_BITS = 30
 ABI_VERSION = 13

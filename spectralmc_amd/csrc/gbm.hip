@@ -851,6 +851,98 @@ void rows_kernel(EngineArgs a) {
   }
 }
 
+// ---- reference arithmetic (SMC_MATH_REF): the reference kernel's own f32 typing --------------------
+// The reference's SimulateBlackScholes (gbm.py:224-257) is a Numba kernel whose scalar arguments are
+// Python floats: X, dt, sqrt_dt, the drift and the exponent are f64, only the io matrix (normals in,
+// paths out) is f32 -- per step dW = z sqrt_dt (z widened), X *= exp(drift dt + v dW) (log-Euler) or
+// X += drift X dt + v X dW, X = |X| (simple Euler), io = (float) X.  rows_ref_kernel computes that: the
+// portable f32 normals (bit-identical to the oracle), the f64 engine's step (Stepper<double>; e^y by
+// smc_math.h mul_exp2s_f64, within 2 ulp of libm), f32 stores of the rounded state, and the f32
+// pipeline's terminal sum and CF phase (cf_kernel<float>).  Any P: a lane past P draws and stores
+// nothing (stream positions never depend on P), a lane straddling P stores its valid paths one by one.
+// Terminal-sum order of rows_kernel (oracle kernel mode with step64, wg = 512).
+template <bool LOG_EULER, bool STORE_ALL>
+__device__ __forceinline__ void lane_rows_ref(const EngineArgs& a, const Stepper<double, LOG_EULER, false>& step,
+                                              double x0, uint64_t ordinal, int64_t chunk, float* contract_base,
+                                              int T, int64_t pitch, double& acc) {
+  const int lane_id = static_cast<int>(threadIdx.x);
+  const int64_t p0 = chunk + kPathsPerLane * static_cast<int64_t>(lane_id);
+  const int nvalid = a.P - p0 >= kPathsPerLane ? kPathsPerLane : (a.P > p0 ? static_cast<int>(a.P - p0) : 0);
+  PathStream s(a.seed, ordinal, static_cast<uint64_t>(p0 / kPathsPerLane), T);
+  double x[kPathsPerLane];
+  float zl[kPathsPerLane], zh[kPathsPerLane];
+#pragma unroll
+  for (int j = 0; j < kPathsPerLane; ++j) x[j] = x0;
+  const uint32_t lane_off = static_cast<uint32_t>(kPathsPerLane * sizeof(float)) * static_cast<uint32_t>(lane_id);
+  const char* row = reinterpret_cast<const char*>(contract_base + chunk);
+  const int64_t rstride = STORE_ALL ? pitch * static_cast<int64_t>(sizeof(float)) : 0;
+  auto advance = [&](const float (&z)[kPathsPerLane]) {
+#pragma unroll
+    for (int j = 0; j < kPathsPerLane; ++j) x[j] = step(x[j], static_cast<double>(z[j]));
+  };
+  auto store = [&] {
+    const float4 v = {static_cast<float>(x[0]), static_cast<float>(x[1]), static_cast<float>(x[2]),
+                      static_cast<float>(x[3])};
+    if (nvalid == kPathsPerLane) {
+      store_row(row, lane_off, v);
+    } else if (nvalid > 0) {
+      float* r = reinterpret_cast<float*>(const_cast<char*>(row) + lane_off);
+      const float w[kPathsPerLane] = {v.x, v.y, v.z, v.w};
+      for (int j = 0; j < nvalid; ++j) r[j] = w[j];
+    }
+  };
+#pragma unroll 1
+  for (int t = 0; t + 1 < T; t += 2) {
+#pragma unroll
+    for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<false>(zl[j], zh[j]);
+    advance(zl);
+    if constexpr (STORE_ALL) store();
+    row += rstride;
+    advance(zh);
+    if constexpr (STORE_ALL) store();
+    row += rstride;
+  }
+  if (T & 1) {  // the last step of an odd T: two Box-Muller pairs for the 4 paths
+    s.template normal_tail<false>(zl);
+    advance(zl);
+    if constexpr (STORE_ALL) store();
+  }
+  if constexpr (!STORE_ALL) store();
+  float part = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kPathsPerLane; ++j) part += j < nvalid ? static_cast<float>(x[j]) : 0.0f;
+  acc += static_cast<double>(part);
+}
+
+// rows_kernel's persistent contract loop over lane_rows_ref (the f64 step's tables in LDS)
+template <bool LOG_EULER, bool STORE_ALL>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kRowsWavesF64)))
+void rows_ref_kernel(EngineArgs a) {
+  extern __shared__ double lds[];
+  math::f64_tables_load();
+  const int64_t ord0 = (a.ordinal_dev ? *a.ordinal_dev : 0) + a.ordinal0;
+  const int64_t pitch = a.pitch ? a.pitch : a.P;
+  const int T = a.T;
+  int parity = 0;
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x, parity ^= 1) {
+    const Contract c = load_contract(a.contracts + b * 6);
+    const Stepper<double, LOG_EULER, false> step(c, T);
+    float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * T * pitch : b * pitch);
+    double acc = 0.0;
+    for (int64_t chunk = 0; chunk < a.P; chunk += kChunk)
+      lane_rows_ref<LOG_EULER, STORE_ALL>(a, step, c.X0, static_cast<uint64_t>(ord0 + b), chunk, base, T, pitch, acc);
+    const double w = wave_sum(acc);
+    double* ws = lds + parity * kWaves;
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = w;
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      double tot = 0.0;
+      for (int k = 0; k < kWaves; ++k) tot += ws[k];
+      *pad_sum<float>(a, b) = tot;
+    }
+  }
+}
+
 // ---- resident_kernel: the terminal row never leaves the chip -----------------------------------
 // For P <= 65,536 a 1024-thread workgroup (4 paths per lane, 4096-path chunks, <= 16 chunks) keeps
 // the contract's whole terminal row on chip next to its stores: chunks 0..7 in LDS (128 KiB, one
@@ -1500,6 +1592,13 @@ bool rows_ok(const EngineArgs& a, bool f32) {
          pitch >= a.P + (f32 ? (a.P & 1) + 2 : 1) && (a.store == SMC_STORE_ALL || a.store == SMC_STORE_TERMINAL);
 }
 
+// rows_ref_kernel + cf_kernel (SMC_MATH_REF): any P, the f32 terminal-sum padding
+bool ref_ok(const EngineArgs& a) {
+  const int64_t pitch = a.pitch ? a.pitch : a.P;
+  return a.simulate && a.targets && !a.all_rows && a.slices <= 1 && a.T >= 1 && pitch >= a.P + (a.P & 1) + 2 &&
+         (a.store == SMC_STORE_ALL || a.store == SMC_STORE_TERMINAL);
+}
+
 // Sliced contracts on persistent workgroups.  Contract b belongs to queue b mod 8; a workgroup
 // takes items (slice k of a contract) from the queue of the XCD it runs on (s_getreg XCC_ID), so
 // the slices of a contract run side by side on one XCD, finish within a few tens of microseconds
@@ -1741,6 +1840,26 @@ int32_t launch_rows_k(const EngineArgs& a, hipStream_t stream) {
   return check_launch("cf_kernel");
 }
 
+template <bool LOG_EULER, bool STORE_ALL>
+int32_t launch_rows_ref_k(const EngineArgs& a, hipStream_t stream) {
+  const size_t lds1 = 2 * kWaves * sizeof(double), lds2 = lds_bytes(a.T, a.N, true);
+  auto k1 = rows_ref_kernel<LOG_EULER, STORE_ALL>;
+  auto k2 = cf_kernel<float>;
+  if (lds2 > kMaxLds) return fail(SMC_ERR_INVALID_SHAPE, "engine: network_size exceeds the LDS budget");
+  if (lds2 > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(k2),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               static_cast<int>(lds2)) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(SMC_ERR_HIP, "cf_kernel: cannot raise the dynamic LDS limit");
+  }
+  unsigned grid1 = 0;
+  if (int32_t st = resident_grid(reinterpret_cast<const void*>(k1), kThreads, lds1, a.B, &grid1)) return st;
+  hipLaunchKernelGGL(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
+  if (int32_t st = check_launch("rows_ref_kernel")) return st;
+  hipLaunchKernelGGL(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
+  return check_launch("cf_kernel");
+}
+
 template <bool LOG_EULER, bool HW, bool STORE_ALL>
 int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
   const int W = a.res_slices > 1 ? a.res_slices : 1;
@@ -1814,6 +1933,16 @@ int32_t launch_packed_k(const EngineArgs& a, hipStream_t stream) {
 template <typename Real>
 int32_t launch_engine(EngineArgs a, hipStream_t stream) {
   if (a.B == 0) return SMC_OK;
+  if ((a.scheme & SMC_MATH_REF) != 0) {
+    if (sizeof(Real) != 4) return fail(SMC_ERR_INVALID_ARGUMENT, "engine: SMC_MATH_REF is an f32 mode");
+    if (!ref_ok(a))
+      return fail(SMC_ERR_INVALID_SHAPE, "engine: SMC_MATH_REF needs targets, whole contracts per workgroup and "
+                                         "a padded pitch (smc_path_pitch)");
+    const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
+    const bool sa = a.store == SMC_STORE_ALL;
+    if (log_euler) return sa ? launch_rows_ref_k<true, true>(a, stream) : launch_rows_ref_k<true, false>(a, stream);
+    return sa ? launch_rows_ref_k<false, true>(a, stream) : launch_rows_ref_k<false, false>(a, stream);
+  }
   if constexpr (sizeof(Real) == 4) {
     if (wave_ok(a, true)) {  // RAW, T <= 2: one wave per contract
       const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
@@ -1950,7 +2079,8 @@ int32_t dispatch_engine(const EngineArgs& a, int32_t dtype, hipStream_t stream) 
 
 bool valid_scheme(int32_t scheme) {
   const int32_t base = scheme & 0xff, flags = scheme & ~0xff;
-  return (base == SMC_SCHEME_LOG_EULER || base == SMC_SCHEME_SIMPLE_EULER) && (flags & ~SMC_MATH_HW) == 0;
+  return (base == SMC_SCHEME_LOG_EULER || base == SMC_SCHEME_SIMPLE_EULER) &&
+         (flags & ~(SMC_MATH_HW | SMC_MATH_REF)) == 0 && (flags & (SMC_MATH_HW | SMC_MATH_REF)) != (SMC_MATH_HW | SMC_MATH_REF);
 }
 
 int32_t validate_common(const double* contracts, int64_t B, int32_t T, int64_t P, int32_t dtype) {
@@ -1977,6 +2107,8 @@ int32_t smc_gbm_simulate(const double* contracts_dev, int64_t n_contracts, int32
   if (int32_t st = validate_common(contracts_dev, n_contracts, timesteps, n_paths, dtype)) return st;
   if (!paths_dev) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_gbm_simulate: paths_dev is NULL");
   if (!valid_scheme(scheme)) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_gbm_simulate: bad scheme");
+  if (scheme & SMC_MATH_REF)
+    return fail(SMC_ERR_INVALID_ARGUMENT, "smc_gbm_simulate: SMC_MATH_REF is for smc_train_targets / smc_train_step");
   EngineArgs a{contracts_dev, n_contracts, timesteps, n_paths, 1, 1, mc_seed, ordinal_dev, ordinal0,
                scheme, 0, SMC_STORE_ALL, 1, 1, paths_dev, rowsum_dev, nullptr};
   return dispatch_engine(a, dtype, as_stream(stream));
@@ -2126,7 +2258,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
     a.res_xcol = reinterpret_cast<double*>(sync + l.xcol_off);
   }
   const bool fused = dtype == SMC_DTYPE_F32 && n_contracts > 0 && chunk_contracts > 0 &&
-                     valid_scheme(scheme) && (store_mode == SMC_STORE_ALL || store_mode == SMC_STORE_TERMINAL) &&
+                     valid_scheme(scheme) && (scheme & SMC_MATH_REF) == 0 && (store_mode == SMC_STORE_ALL || store_mode == SMC_STORE_TERMINAL) &&
                      paths_dev && targets_dev && (wave_ok(a, true) || resident_ok(a, true) || packed_ok(a, true));
   if (fused) {
     // one resident launch per chunk of contracts; each draws its own contracts, the last advances
@@ -2204,6 +2336,7 @@ const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32
   a.res_xsum = a.res_xcol = reinterpret_cast<double*>(&a);
   a.done = reinterpret_cast<uint32_t*>(&a);
   a.normalize = (dtype & SMC_QUERY_RAW) ? 0 : 1;
+  if (dtype & SMC_MATH_REF) return "rows_ref_kernel+cf_kernel";
   if (wave_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "wave_kernel";
   if (resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))
     return a.res_slices > 1 ? "resident_kernel(sliced)" : "resident_kernel";
@@ -2228,6 +2361,7 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.store = SMC_STORE_ALL;
   const bool f32 = (dtype & 0xff) == SMC_DTYPE_F32;
   a.normalize = (dtype & SMC_QUERY_RAW) ? 0 : 1;
+  if (dtype & SMC_MATH_REF) return "rows_ref_kernel+cf_kernel";
   if (wave_ok(a, f32)) return "wave_kernel";
   if (resident_ok(a, f32)) return "resident_kernel";
   if (packed_ok(a, f32)) return "packed_kernel";

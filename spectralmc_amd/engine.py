@@ -80,11 +80,14 @@ class TrainingEngine:
         self.device = device
         self.sim_dtype = sp.dtype
         self._dtype_code = dtype_code(sp.dtype)
-        if math not in ("portable", "hw"):
-            raise ValueError(f"math must be 'portable' or 'hw', got {math!r}")
+        if math not in ("portable", "hw", "reference"):
+            raise ValueError(f"math must be 'portable', 'hw' or 'reference', got {math!r}")
+        if math == "reference" and sp.dtype != Precision.float32:
+            raise ValueError("math='reference' is the reference kernel's f32 typing (float32 simulations only)")
         self.math = math
-        # "hw": f32 hardware transcendentals in the path kernel (faster, ~1 ulp, not CPU-reproducible)
-        self._scheme = scheme_code(cfg.path_scheme) | (_lib.MATH_HW if math == "hw" else 0)
+        # "hw": f32 hardware transcendentals in the path kernel (faster, ~1 ulp, not CPU-reproducible);
+        # "reference": the reference kernel's typing (f64 state and step, f32 normals and stores: rows_ref_kernel)
+        self._scheme = scheme_code(cfg.path_scheme) | {"hw": _lib.MATH_HW, "reference": _lib.MATH_REF}.get(math, 0)
         self._norm = normalization_code(cfg.normalization)
         self.store_mode = _lib.STORE_ALL if store_paths else _lib.STORE_TERMINAL
         sim_torch = sp.dtype.to_torch()
@@ -126,7 +129,8 @@ class TrainingEngine:
         # zero-filled once; every step leaves its counters zeroed
         self._uses_train_step = self._f32_in and self.dim == 6 and self._workspace is None
         # the path/CF kernel the step runs for this shape (bench labels, rocprof cross-check)
-        query = self._dtype_code | (_lib.QUERY_RAW if self._norm == _lib.NORM_RAW else 0)
+        query = self._dtype_code | (_lib.QUERY_RAW if self._norm == _lib.NORM_RAW else 0) | \
+            (_lib.MATH_REF if math == "reference" else 0)
         if self._uses_train_step:
             self.kernel_name = _lib.lib().smc_train_step_kernel(self.T, self.N, self.M, query, self.pitch).decode()
         else:

@@ -4,6 +4,7 @@ known-answer vectors and closed-form cases.  CPU only."""
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import pytest
@@ -188,3 +189,23 @@ def test_black_formula_put_call_parity(oracle) -> None:
     # call by parity must be positive and above intrinsic
     call = put + X0 * math.exp(-d * T) - K * math.exp(-r * T)
     assert call > max(X0 * math.exp(-d * T) - K * math.exp(-r * T), 0.0)
+
+
+@pytest.mark.parametrize("scheme", [0, 1])
+@pytest.mark.parametrize("T", [1, 5, 16, 33])
+def test_reference_math_mode_reproduces_the_reference_arithmetic(oracle, T, scheme) -> None:
+    """Kernel mode with MATH_REF (gbm.hip rows_ref_kernel: the f64 engine's step of the portable f32
+    normals, state in f64, stores rounded to f32) against the reference mode (gbm.py:224-257's own typing
+    under Numba: f64 state, libm exp, f32 stores; pinned to the reference's output by gbm_golden.npz): the
+    stored f32 paths agree to the bit except where the two f64 exps (within 2 ulp of each other) round to
+    different floats -- none in these 32 x 2048 x T values -- while the f32 recursion differs in most."""
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden.npz"), allow_pickle=False)
+    c = oracle.sobol_contracts(7, 0, 32, g["bounds_lower"], g["bounds_upper"])
+    P = 2048
+    ref, _, _ = oracle.gbm_paths(c, T, P, 7, 3, scheme, "float32", want_paths=True)
+    k64, term, rowsum = oracle.kernel_paths(c, T, P, 7, 3, scheme | oracle.MATH_REF, want_paths=True)
+    k32, _, _ = oracle.kernel_paths(c, T, P, 7, 3, scheme, want_paths=True)
+    fin = np.isfinite(ref)
+    assert int(((k64 != ref) & fin).sum()) == 0
+    assert ((k32 != ref) & fin).mean() > 0.3
+    np.testing.assert_array_equal(term, k64[:, -1])
