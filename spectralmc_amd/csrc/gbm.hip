@@ -914,9 +914,12 @@ __device__ __forceinline__ void lane_rows_ref(const EngineArgs& a, const Stepper
   acc += static_cast<double>(part);
 }
 
-// rows_kernel's persistent contract loop over lane_rows_ref (the f64 step's tables in LDS)
+// rows_kernel's persistent contract loop over lane_rows_ref (the f64 step's tables in LDS).  Register budget:
+// 6 waves per SIMD (three 8-wave workgroups per CU with the 51 KB table image each): C2 6.59 ms against 6.65
+// at 4 and 6.69 at 8 waves (profiles/r05/ab_ref_waves.txt)
+constexpr int kRowsRefWaves = 6;
 template <bool LOG_EULER, bool STORE_ALL>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kRowsWavesF64)))
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kRowsRefWaves)))
 void rows_ref_kernel(EngineArgs a) {
   extern __shared__ double lds[];
   math::f64_tables_load();

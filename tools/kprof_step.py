@@ -25,7 +25,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=sorted(SHAPES))
     ap.add_argument("--B", type=int, default=0, help="contracts per step (default: the config's)")
-    ap.add_argument("--math", default="hw", choices=["hw", "portable"])
+    ap.add_argument("--math", default="hw", choices=["hw", "portable", "reference"])
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--iters", type=int, default=5)
@@ -73,7 +73,8 @@ def main() -> None:
     nsync = int(L.smc_train_step_sync_bytes(T, N, M, dcode, pitch))
     syncs = [torch.zeros(max(nsync, 8), dtype=torch.uint8, device=dev) for _ in range(lanes)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(lanes - 1)]
-    scheme = _lib.SCHEME_LOG_EULER | (_lib.MATH_HW if a.math == "hw" else 0) | (_lib.TRAIN_DYNAMIC if a.dynamic else 0)
+    scheme = _lib.SCHEME_LOG_EULER | {"hw": _lib.MATH_HW, "reference": _lib.MATH_REF}.get(a.math, 0) | \
+        (_lib.TRAIN_DYNAMIC if a.dynamic else 0)
     n_launched = [0]
     raw = a.norm == "raw" or (a.norm == "" and a.config == "lockstep")
     norm = _lib.NORM_RAW if raw else _lib.NORM_NORMALIZE
@@ -100,7 +101,8 @@ def main() -> None:
     e1.record()
     torch.cuda.synchronize()
     assert all(_lib.sync_status(sy) == 0 for sy in syncs)
-    name = L.smc_train_step_kernel(T, N, M, dcode | (_lib.QUERY_RAW if raw else 0), pitch).decode()
+    name = L.smc_train_step_kernel(T, N, M, dcode | (_lib.QUERY_RAW if raw else 0) |
+                                   (_lib.MATH_REF if a.math == "reference" else 0), pitch).decode()
     ms = e0.elapsed_time(e1) / a.iters
     print(f"{a.config} {'raw' if raw else 'normalize'} pitch={pitch} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
           f"({launches} launch(es) of {chunk}), checksum {float(t.abs().double().mean()):.6g}")
