@@ -196,12 +196,13 @@ class TrainingEngine:
         return StepBuffers(contracts=torch.empty_like(b.contracts), real_in=torch.empty_like(b.real_in),
                            imag_in=b.imag_in, targets=torch.empty_like(b.targets))
 
-    def enqueue_step(self, out: StepBuffers | None = None, lane: int | None = None) -> StepBuffers:
-        """Launch contracts + targets of the next step on the current stream into ``out`` (default:
-        the engine's own buffers), advance the cursor.  ``lane``: the lane of this step (default: the
-        next in turn); steps must use the lanes in turn, 0, 1, ..., so a lane's cursor stays the
+    def enqueue_step(self, out: StepBuffers | None = None, lane: int | None = None,
+                     stream: int | None = None) -> StepBuffers:
+        """Launch contracts + targets of the next step on the current stream (or the hipStream_t ``stream``)
+        into ``out`` (default: the engine's own buffers), advance the cursor.  ``lane``: the lane of this step
+        (default: the next in turn); steps must use the lanes in turn, 0, 1, ..., so a lane's cursor stays the
         position of its next step."""
-        stream = _lib.stream_handle()
+        stream = stream if stream is not None else _lib.stream_handle()
         b = out if out is not None else self.buffers
         offset = self.rank * self.B
         k = self._next_lane if lane is None else lane % self.lanes

@@ -283,7 +283,8 @@ class _StepProgram:
                 self.fused = None
 
     # -- pieces -------------------------------------------------------------------------
-    def mc(self, slot: int) -> None:
+    def mc(self, slot: int, stream: int | None = None) -> None:
+        """stream: the hipStream_t to launch on (None: the current stream)."""
         out = self.slots[slot] if self.direct else None
         lanes = getattr(self.engine, "lanes", 1)
         if lanes > 1:
@@ -291,9 +292,9 @@ class _StepProgram:
             # SLOTS (GbmCVNNPricer.open_session rejects other values)
             if self.SLOTS % lanes:
                 raise ValueError(f"{lanes} MC lanes do not divide the {self.SLOTS} step slots")
-            self.engine.enqueue_step(out, lane=slot)
+            self.engine.enqueue_step(out, lane=slot, **({} if stream is None else {"stream": stream}))
         else:
-            self.engine.enqueue_step(out)
+            self.engine.enqueue_step(out, **({} if stream is None else {"stream": stream}))
 
     def handoff(self, slot: int) -> None:
         if self.direct:
@@ -302,9 +303,9 @@ class _StepProgram:
         self.real_in[slot].copy_(eb.real_in)
         self.targets[slot].copy_(eb.targets)
 
-    def fwd_bwd(self, slot: int) -> None:
+    def fwd_bwd(self, slot: int, stream: int | None = None) -> None:
         if self.fused is not None:
-            self.fused.fwd_bwd(self.real_in[slot], self.imag_in, self.targets[slot])
+            self.fused.fwd_bwd(self.real_in[slot], self.imag_in, self.targets[slot], stream=stream)
             return
         self.flat.zero_()
         targets = self.targets[slot]
@@ -314,10 +315,10 @@ class _StepProgram:
         loss.backward()
         self.loss_slot.copy_(loss.detach().reshape(1))
 
-    def update(self) -> None:
+    def update(self, stream: int | None = None) -> None:
         if self.fused is not None:
             if not self.fused.fuse_adam:  # data-parallel: Adam after the all-reduce
-                self.fused.adam()
+                self.fused.adam(stream=stream)
             return
         self.adam.step()
         grads = [p.grad for p in self.params]
@@ -394,17 +395,26 @@ class _StepProgram:
         self.handoff(slot)
         self.run_nn(slot)
 
-    def run_mc(self, slot: int) -> None:
+    def run_mc(self, slot: int, stream: int | None = None) -> None:
+        """stream: eager launches on this hipStream_t (replays use the current stream)."""
         if self.mc_graphs:
             self.mc_graphs[slot].replay()
         else:
-            self.mc(slot)
+            self.mc(slot, stream)
 
-    def run_nn(self, slot: int) -> None:
+    @property
+    def explicit_streams(self) -> bool:
+        """The eager step takes explicit stream handles (no torch op in it: direct slots, the one-call
+        smc_train_step MC part, fused network, no all-reduce), so it needs no torch stream contexts (their host
+        cost bounds short steps)."""
+        return (self.direct and getattr(self.engine, "_uses_train_step", False) and self.fused is not None and
+                self.dp is None and not self.captured)
+
+    def run_nn(self, slot: int, stream: int | None = None) -> None:
         if not self.nn_graphs:
-            self.fwd_bwd(slot)
+            self.fwd_bwd(slot, stream)
             self.reduce()
-            self.update()
+            self.update(stream)
             return
         graphs = self.nn_graphs[slot]
         graphs[0].replay()
@@ -414,11 +424,19 @@ class _StepProgram:
 
 
 # ============================================================================ trainer
+GRAPH_MIN_PATH_STEPS = 1 << 27  # GbmCVNNPricer.graph_min_path_steps
+
+
 class GbmCVNNPricer:
     """Coordinates the MC engine, the CF targets and CVNN optimisation on one GPU (per process)."""
 
     #: eager steps before the step is captured as a hipGraph (0 disables capture)
     warmup_steps: int = 2
+    #: capture only steps of at least this many path-steps (contracts x paths x timesteps): below it every
+    #: hipGraph launch cost the GPU more than the eager launches it replaces (the reference's e2e shape, 33.6 M
+    #: path-steps: 0.092 ms/step replayed against 0.079-0.082 eager; the lock-step shape, 268 M, equal;
+    #: profiles/r05/ab_graphs_short.txt)
+    graph_min_path_steps: int = GRAPH_MIN_PATH_STEPS
     #: materialise the full [B][T][P] path matrix each step (the reference kernel's output contract)
     store_paths: bool = True
     #: "hw": hardware f32 transcendentals in the path kernel (throughput mode; parity with the
@@ -907,6 +925,9 @@ class TrainingSession:
         self._nn_done = [torch.cuda.Event() for _ in range(K)]  # network finished reading slot k
         self._slot_used = [False] * K
         self._mc_pending = False             # the MC part of the next step is already enqueued
+        eng = self.engine
+        self.capture_graphs = (getattr(eng, "B", 0) * getattr(eng, "P", 0) * getattr(eng, "T", 0) >=
+                               pricer.graph_min_path_steps)
         self.mc_events: list[tuple[torch.cuda.Event, torch.cuda.Event]] | None = None
         self._closed = False
         # exchanging path launches wait for the previous step's network part (pricer.exchange_after_network)
@@ -927,7 +948,7 @@ class TrainingSession:
             return Failure(SamplerInitFailed(error=SequenceExhausted(requested_end=self.sobol_skip + self.global_batch)))
         prog = self.program
         warm = self.pricer.warmup_steps
-        if warm > 0 and self.steps >= warm and not prog.captured:
+        if warm > 0 and self.steps >= warm and not prog.captured and self.capture_graphs:
             if self._mc_pending:  # the pending eager MC launch must finish before capture
                 for ms in self.mc_streams:
                     ms.synchronize()
@@ -942,6 +963,8 @@ class TrainingSession:
             self.global_step += 1
             self.pricer._mc_engine.advance(self.global_batch)
             return Success(self.global_step)
+        if prog.explicit_streams:
+            return self._step_explicit(slot, prefetch_next)
         ms = self._lane_stream(slot)
         with torch.cuda.stream(ms):
             if not self._mc_pending:
@@ -973,24 +996,56 @@ class TrainingSession:
         self.pricer._mc_engine.advance(self.global_batch)
         return Success(self.global_step)
 
+    def _step_explicit(self, slot: int, prefetch_next: bool) -> Result[int, TrainerError]:
+        """step() for an eager step of fused HIP launches only: the same launches and events in the same
+        order, on explicit stream handles instead of inside torch stream contexts (e2e: 0.078 ms of host
+        time per step, the bound of that shape, before; profiles/r05/)."""
+        K = _StepProgram.SLOTS
+        ms = self._lane_stream(slot)
+        if not self._mc_pending:
+            self._enqueue_mc(slot, explicit=True)
+        self._mc_done[slot].record(ms)
+        self._mc_pending = False
+        prefetch = prefetch_next and self.sobol_skip + 2 * self.global_batch <= MAX_POINTS
+        nxt = (self.steps + 1) % K
+        if prefetch and not self._mc_after_nn:
+            self._enqueue_mc(nxt, explicit=True)
+            self._mc_pending = True
+        self.stream.wait_event(self._mc_done[slot])
+        self.program.run_nn(slot, self.stream.cuda_stream)
+        self._nn_done[slot].record(self.stream)
+        self._slot_used[slot] = True
+        if prefetch and self._mc_after_nn:
+            ns = self._lane_stream(nxt)
+            ns.wait_event(self._nn_done[slot])
+            self._enqueue_mc(nxt, explicit=True)
+            self._mc_pending = True
+        self.steps += 1
+        self.sobol_skip += self.global_batch
+        self.global_step += 1
+        self.pricer._mc_engine.advance(self.global_batch)
+        return Success(self.global_step)
+
     def _lane_stream(self, slot: int) -> torch.cuda.Stream:
         """The MC stream of step slot ``slot`` (slot k runs on engine lane k % lanes)."""
         return self.mc_streams[slot % len(self.mc_streams)]
 
-    def _enqueue_mc(self, slot: int) -> None:
+    def _enqueue_mc(self, slot: int, explicit: bool = False) -> None:
         """MC part of a step into ``slot`` on its lane's MC stream, once the network part that last
-        read the slot (SLOTS steps back) is done with it."""
+        read the slot (SLOTS steps back) is done with it.  explicit: eager launches on the lane's stream
+        handle (else the caller's current stream is the lane's)."""
         ms = self._lane_stream(slot)
+        handle = ms.cuda_stream if explicit else None
         if self._slot_used[slot]:
             ms.wait_event(self._nn_done[slot])
         if self.mc_events is not None:  # live timing of the MC part on its own stream
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(ms)
-            self.program.run_mc(slot)
+            self.program.run_mc(slot, handle)
             e1.record(ms)
             self.mc_events.append((e0, e1))
         else:
-            self.program.run_mc(slot)
+            self.program.run_mc(slot, handle)
 
     def sync(self) -> None:
         """Wait for the enqueued steps; raises SmcError (SMC_ERR_EXCHANGE_TIMEOUT) if an exchanging

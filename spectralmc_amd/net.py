@@ -164,10 +164,12 @@ class FusedNetworkStep:
                                        loss=_lib.ptr(loss_out))
         self.fuse_adam = fuse_adam
 
-    def fwd_bwd(self, real_in: torch.Tensor, imag_in: torch.Tensor | None, targets: torch.Tensor) -> None:
-        """Gradients + loss into the flat buffer (and, fused, the Adam step) on the current stream."""
+    def fwd_bwd(self, real_in: torch.Tensor, imag_in: torch.Tensor | None, targets: torch.Tensor,
+                stream: int | None = None) -> None:
+        """Gradients + loss into the flat buffer (and, fused, the Adam step) on the current stream (or the
+        hipStream_t ``stream``)."""
         L = _lib.lib()
-        stream = _lib.stream_handle()
+        stream = stream if stream is not None else _lib.stream_handle()
         if self.mode:
             _lib.check(L.smc_cvnn_mfma_forward_backward(
                 self._layers, len(self.table), self.mode, _lib.ptr(self.params_flat), self.n, _lib.ptr(real_in),
@@ -187,10 +189,11 @@ class FusedNetworkStep:
     def kernels(self) -> str:
         return {0: "valu", _lib.CVNN_MFMA_F32: "mfma_f32", _lib.CVNN_MFMA_BF16: "mfma_bf16"}[self.mode]
 
-    def adam(self) -> None:
+    def adam(self, stream: int | None = None) -> None:
         """Adam + grad norm + loss copy from the (all-reduced) flat buffer."""
         _lib.check(_lib.lib().smc_adam_step(self.dtype_code, self.n, _lib.ptr(self.grads),
-                                            ctypes.byref(self.adam_args), _lib.stream_handle()))
+                                            ctypes.byref(self.adam_args),
+                                            stream if stream is not None else _lib.stream_handle()))
 
 
 __all__ = ["FusedNetworkStep", "UnsupportedNetwork", "lower"]

@@ -91,3 +91,12 @@ def async_store(tmp_path):
     from spectralmc_amd.storage import AsyncBlockchainModelStore
 
     return AsyncBlockchainModelStore(tmp_path / "store")
+
+
+@pytest.fixture(autouse=True)
+def _graphs_at_every_shape(monkeypatch):
+    """The suite exercises hipGraph capture and replay at its small shapes too: the product captures only
+    steps of at least GbmCVNNPricer.graph_min_path_steps path-steps (test_gpu_trainer checks that default)."""
+    from spectralmc_amd.gbm_trainer import GbmCVNNPricer
+
+    monkeypatch.setattr(GbmCVNNPricer, "graph_min_path_steps", 0)

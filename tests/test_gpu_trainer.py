@@ -88,6 +88,23 @@ def test_portable_math_trainer_loss_within_tolerance(oracle) -> None:
     assert res.final_loss == pytest.approx(ref.loss, rel=1e-4)
 
 
+def test_short_steps_run_eager_and_long_steps_capture(monkeypatch) -> None:
+    """graph_min_path_steps (the product default, 2^27 path-steps): a step below it stays eager after the
+    warm-up steps, one at or above it is captured (here by lowering the threshold to the step's own size)."""
+    from spectralmc_amd.gbm_trainer import GRAPH_MIN_PATH_STEPS
+
+    monkeypatch.setattr(GbmCVNNPricer, "graph_min_path_steps", GRAPH_MIN_PATH_STEPS)
+    B = 16
+    for threshold, captured in ((GRAPH_MIN_PATH_STEPS, False), (B * N * M * T, True)):
+        p, _ = _pricer(warmup=1)
+        p.graph_min_path_steps = threshold
+        session = expect_success(p.open_session(make_training_config(num_batches=3, batch_size=B)))
+        for _ in range(3):
+            expect_success(session.step())
+        assert session.program.captured is captured
+        session.close()
+
+
 def test_graph_replay_matches_eager() -> None:
     eager, m_e = _pricer(warmup=0)
     graph, m_g = _pricer(warmup=1)
