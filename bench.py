@@ -358,7 +358,14 @@ def main() -> None:
     if ctx:
         dist.barrier()
     torch.cuda.synchronize()
-    session.mc_events = []  # HIP events around each MC-part launch on its stream (timed region)
+    # HIP events around each MC-part launch on its stream (timed region), created and recorded once beforehand
+    pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps + 2)]
+    for e0, e1 in pool:
+        e0.record()
+        e1.record()
+    torch.cuda.synchronize()
+    session.mc_event_pool = pool[::-1]
+    session.mc_events = []
     if ctx:
         session.program.ar_events = []  # ... and around each step's all-reduce on the network stream
     t0 = time.perf_counter()

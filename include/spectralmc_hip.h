@@ -269,6 +269,23 @@ typedef struct smc_cvnn_layer {
   int64_t act_bias;              /* [out] modReLU bias offset or -1                    */
 } smc_cvnn_layer;
 
+/* Where an Adam update also writes the matrix-core (MFMA) operand copies of the weights it changes, so the
+ * next smc_cvnn_mfma_forward_backward skips its pack launch (mode | SMC_CVNN_MFMA_PACKED): each complex
+ * weight w = a + i b of layer l lands at Wc[2j][2k] = Wc[2j+1][2k+1] = a, Wc[2j][2k+1] = -b, Wc[2j+1][2k] = b
+ * and at the same places of Wc^T (smc_cvnn_mfma_pack_plan fills it from the forward_backward plan). */
+typedef struct smc_cvnn_pack_layer {
+  int64_t w_re, w_im;            /* the layer's weight offsets in params (as smc_cvnn_layer)   */
+  int32_t ni, no;                /* complex in / out features                                  */
+  int32_t win, wout;             /* packed widths (2 ni, 2 no rounded up to the K block)       */
+  int64_t wc, wct;               /* element offsets of Wc [wout][win] and Wc^T [win][wout]     */
+} smc_cvnn_pack_layer;
+typedef struct smc_cvnn_pack {
+  void* ws;                      /* the forward_backward workspace                             */
+  int32_t bf16;                  /* operands are bf16 (SMC_CVNN_MFMA_BF16), else f32           */
+  int32_t n_layers;              /* 0: nothing to write                                        */
+  smc_cvnn_pack_layer layer[SMC_CVNN_MAX_LAYERS];
+} smc_cvnn_pack;
+
 /* torch.optim.Adam (defaults of gbm_trainer.py:1513) on flat buffers; `step` is torch's
  * capturable f32 step counter, read before and incremented after the update. */
 typedef struct smc_adam_args {
@@ -282,6 +299,7 @@ typedef struct smc_adam_args {
                                     arrival counter; every call leaves it zero)            */
   void* grad_norm;               /* scalar out: ||grad||_2 (gbm_trainer.py:834)         */
   void* loss;                    /* scalar out: grads[n_params] (the loss slot)         */
+  const smc_cvnn_pack* pack;     /* or NULL: the update also writes these packed copies (ABI 13) */
 } smc_adam_args;
 
 /* Number of per-workgroup gradient partials ([blocks][n_params + 1]) for this batch. */
@@ -317,6 +335,8 @@ int64_t smc_adam_norm_partials(int64_t n_params);
  * kernels' LDS plan return SMC_ERR_INVALID_SHAPE from the plan (callers keep the VALU kernels). */
 #define SMC_CVNN_MFMA_F32   1
 #define SMC_CVNN_MFMA_BF16  2
+#define SMC_CVNN_MFMA_PACKED 0x100  /* flag, OR into forward_backward's mode: the workspace already holds
+                                       the packed weights of params (the last Adam update wrote them) */
 int32_t smc_cvnn_mfma_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, int64_t batch,
                            int64_t* partial_blocks, int64_t* workspace_bytes);
 int32_t smc_cvnn_mfma_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode,
@@ -324,6 +344,10 @@ int32_t smc_cvnn_mfma_forward_backward(const smc_cvnn_layer* layers, int32_t n_l
                                        const float* input_im, const void* targets, int64_t batch,
                                        float* partials, int64_t partial_blocks, void* workspace,
                                        int64_t workspace_bytes, void* stream);
+/* The packed-weight layout of that plan for Adam (smc_adam_args.pack); out->n_layers = 0 for plans whose
+ * wide layers keep their own pack launch (the layered GEMM path). */
+int32_t smc_cvnn_mfma_pack_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, int64_t batch,
+                                void* workspace, smc_cvnn_pack* out);
 
 #ifdef __cplusplus
 }

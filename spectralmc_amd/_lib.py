@@ -82,6 +82,7 @@ SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_cvnn_mfma_plan": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_i64, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "smc_cvnn_mfma_forward_backward": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64,
                                                 _c_vp, _c_i64, _c_vp, _c_i64, _c_vp]),
+    "smc_cvnn_mfma_pack_plan": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_i64, _c_vp, _c_vp]),
     "smc_basket_train_targets": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_i32, _c_u64, _c_vp, _c_i64,
                                           _c_i32, _c_i32, _c_i32, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp,
                                           _c_i64, _c_vp]),
@@ -98,6 +99,7 @@ TEST_SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
 CVNN_MAX_LAYERS = 8
 ACT_NONE, ACT_MODRELU, ACT_ZRELU = 0, 1, 2
 CVNN_MFMA_F32, CVNN_MFMA_BF16 = 1, 2
+CVNN_MFMA_PACKED = 0x100  # forward_backward mode flag: the last Adam update wrote the packed weights
 
 
 class CvnnLayer(ctypes.Structure):
@@ -113,7 +115,20 @@ class AdamArgs(ctypes.Structure):
     _fields_ = [("params", _c_vp), ("exp_avg", _c_vp), ("exp_avg_sq", _c_vp), ("step", _c_vp),
                 ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
                 ("eps", ctypes.c_double), ("weight_decay", ctypes.c_double), ("norm_partials", _c_vp),
-                ("grad_norm", _c_vp), ("loss", _c_vp)]
+                ("grad_norm", _c_vp), ("loss", _c_vp), ("pack", _c_vp)]
+
+
+class CvnnPackLayer(ctypes.Structure):
+    """smc_cvnn_pack_layer (include/spectralmc_hip.h)."""
+
+    _fields_ = [("w_re", _c_i64), ("w_im", _c_i64), ("ni", _c_i32), ("no", _c_i32), ("win", _c_i32),
+                ("wout", _c_i32), ("wc", _c_i64), ("wct", _c_i64)]
+
+
+class CvnnPack(ctypes.Structure):
+    """smc_cvnn_pack (include/spectralmc_hip.h): where Adam writes the MFMA operand copies."""
+
+    _fields_ = [("ws", _c_vp), ("bf16", _c_i32), ("n_layers", _c_i32), ("layer", CvnnPackLayer * CVNN_MAX_LAYERS)]
 
 
 class HipExtensionMissing(ImportError):

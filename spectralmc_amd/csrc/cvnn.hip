@@ -375,6 +375,7 @@ struct AdamArgs {
   void* grad_norm;        // scalar out
   void* loss;             // scalar out: grads[n_params]
   int32_t fuse_final;     // the last workgroup finalizes (else finalize_kernel, a launch of its own)
+  smc_cvnn_pack pack;     // packed MFMA operand copies the update also writes (n_layers = 0: none)
 };
 
 // Reduce grids up to this many workgroups finalize in their last workgroup; larger ones in finalize_kernel:
@@ -382,6 +383,35 @@ struct AdamArgs {
 // the H = 256 network's 4,176-workgroup reduce alone 0.224 -> 0.266 ms fused; the narrow networks' <= 306
 // workgroups: e2e 0.108 -> 0.098 ms/step, lock-step 0.305 -> 0.295, profiles/r05/bench_finalize_sc1_vs_r4.txt)
 constexpr int64_t kFuseFinalizeMaxBlocks = 1024;
+
+// The MFMA operand copies of parameter p (smc_cvnn_pack, spectralmc_hip.h): cvnn_mfma.hip pack_kernel's
+// layout, element for element -- w = a + i b of layer l at (j, k) is Wc[2j][2k] = Wc[2j+1][2k+1] = a,
+// Wc[2j][2k+1] = -b, Wc[2j+1][2k] = b and the same entries of Wc^T; biases are not packed.
+__device__ __forceinline__ void pack_weight(const smc_cvnn_pack& pk, int64_t p, float v) {
+  for (int l = 0; l < pk.n_layers; ++l) {
+    const smc_cvnn_pack_layer& L = pk.layer[l];
+    const int64_t w = static_cast<int64_t>(L.ni) * L.no;
+    const bool re = p >= L.w_re && p < L.w_re + w, im = p >= L.w_im && p < L.w_im + w;
+    if (!re && !im) continue;
+    const int64_t r = p - (re ? L.w_re : L.w_im);
+    const int f = 2 * static_cast<int>(r / L.ni), k = 2 * static_cast<int>(r % L.ni);
+    // (row f + df, column k + dk) of Wc: re at (0, 0) and (1, 1); im at (0, 1) negated and (1, 0)
+    const int f0 = f, k0 = re ? k : k + 1, f1 = f + 1, k1 = re ? k + 1 : k;
+    const float v0 = re ? v : -v;
+    const int64_t c0 = L.wc + static_cast<int64_t>(f0) * L.win + k0, c1 = L.wc + static_cast<int64_t>(f1) * L.win + k1;
+    const int64_t t0 = L.wct + static_cast<int64_t>(k0) * L.wout + f0, t1 = L.wct + static_cast<int64_t>(k1) * L.wout + f1;
+    if (pk.bf16) {
+      uint16_t* ws = static_cast<uint16_t*>(pk.ws);
+      ws[c0] = ws[t0] = bf16_bits(v0);
+      ws[c1] = ws[t1] = bf16_bits(v);
+    } else {
+      float* ws = static_cast<float*>(pk.ws);
+      ws[c0] = ws[t0] = v0;
+      ws[c1] = ws[t1] = v;
+    }
+    return;
+  }
+}
 
 template <typename Real>
 __device__ __forceinline__ void adam_update(const AdamArgs& ad, int64_t p, Real g) {
@@ -399,7 +429,11 @@ __device__ __forceinline__ void adam_update(const AdamArgs& ad, int64_t p, Real 
   const Real bc2 = Real(1) - pow(b2, t);
   const Real step_size = static_cast<Real>(ad.lr) / bc1;
   const Real denom = sqrt(vv) / sqrt(bc2) + static_cast<Real>(ad.eps);
-  prm[p] = prm[p] - step_size * (mm / denom);
+  const Real np = prm[p] - step_size * (mm / denom);
+  prm[p] = np;
+  if constexpr (sizeof(Real) == 4) {
+    if (ad.pack.n_layers > 0) pack_weight(ad.pack, p, np);
+  }
 }
 
 // One block = 64 consecutive gradient entries x 4 slices of the G partials (a wave per slice,
@@ -643,6 +677,7 @@ static AdamArgs to_adam(const smc_adam_args* ad, int64_t n_params, unsigned grid
   a.eps = ad->eps;
   a.weight_decay = ad->weight_decay;
   a.norm_partials = ad->norm_partials;
+  if (ad->pack) a.pack = *ad->pack;  // else n_layers = 0
   a.norm_slots = smc_adam_norm_partials(n_params);
   a.grad_norm = ad->grad_norm;
   a.loss = ad->loss;

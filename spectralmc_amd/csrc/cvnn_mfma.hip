@@ -31,6 +31,7 @@
 // covers k = kb + 4 g + i for g, i in 0..3 on A and B alike.
 #include <cmath>
 
+#include "smc_device.h"
 #include "smc_internal.h"
 
 namespace smc {
@@ -49,21 +50,6 @@ constexpr int64_t kWgradBlocks = 2048;  // segments are added until the workgrou
 constexpr size_t kLdsCap = 156 * 1024;   // dynamic LDS of fb_kernel (160 KiB per CU, less its static LDS)
 constexpr size_t kLdsPair = 80 * 1024;   // two row tiles per workgroup only within this
 
-__host__ __device__ inline float bf16_round(float x) {
-  uint32_t u;
-  __builtin_memcpy(&u, &x, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) {
-    u |= 0x00400000u;  // quiet NaN
-  } else {
-    u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (torch's float -> bfloat16)
-  }
-  u &= 0xffff0000u;
-  float y;
-  __builtin_memcpy(&y, &u, 4);
-  return y;
-}
-
-__device__ __forceinline__ uint16_t bf16_bits(float x) { return static_cast<uint16_t>(__float_as_uint(bf16_round(x)) >> 16); }
 
 struct OpBf16 {
   using T = uint16_t;
@@ -1308,10 +1294,12 @@ int32_t launch_layered(const Plan& p, hipStream_t s) {
 }
 
 template <class Op>
-int32_t launch_all(const Plan& p, hipStream_t s) {
+int32_t launch_all(const Plan& p, hipStream_t s, bool packed) {
   if (p.a.layered) return launch_layered(p, s);
-  hipLaunchKernelGGL(pack_kernel<Op>, dim3(p.pack_grid), dim3(kThreads), 0, s, p.a);
-  if (int32_t rc = check_launch("cvnn pack_kernel")) return rc;
+  if (!packed) {  // (packed: the last Adam update wrote the operand copies, smc_cvnn_pack)
+    hipLaunchKernelGGL(pack_kernel<Op>, dim3(p.pack_grid), dim3(kThreads), 0, s, p.a);
+    if (int32_t rc = check_launch("cvnn pack_kernel")) return rc;
+  }
   if (int32_t rc = p.rt == 2 ? launch_fb<Op, 2>(p, s) : launch_fb<Op, 1>(p, s)) return rc;
   if (int32_t rc = check_launch("cvnn fb_kernel")) return rc;
   hipLaunchKernelGGL(wgrad_kernel<Op>, dim3(p.wgrad_grid), dim3(kThreads), 0, s, p.a);
@@ -1353,6 +1341,8 @@ int32_t smc_cvnn_mfma_forward_backward(const smc_cvnn_layer* layers, int32_t n_l
     if (s.activation == SMC_ACT_MODRELU) ok = ok && s.act_bias >= 0 && s.act_bias + s.out_features <= n_params;
     if (!ok) return fail(SMC_ERR_INVALID_SHAPE, "smc_cvnn_mfma_forward_backward: inconsistent layer table");
   }
+  const bool packed = (mode & SMC_CVNN_MFMA_PACKED) != 0;
+  mode &= ~SMC_CVNN_MFMA_PACKED;
   Plan p;
   const int32_t rc = make_plan(layers, n_layers, mode, batch, n_params, &p);
   if (rc != SMC_OK) return rc;
@@ -1368,7 +1358,25 @@ int32_t smc_cvnn_mfma_forward_backward(const smc_cvnn_layer* layers, int32_t n_l
   a.lossp = reinterpret_cast<double*>(static_cast<char*>(workspace) + p.f64_off);
   a.partials = partials;
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  return mode == SMC_CVNN_MFMA_BF16 ? launch_all<OpBf16>(p, s) : launch_all<OpF32>(p, s);
+  return mode == SMC_CVNN_MFMA_BF16 ? launch_all<OpBf16>(p, s, packed) : launch_all<OpF32>(p, s, packed);
+}
+
+int32_t smc_cvnn_mfma_pack_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, int64_t batch,
+                                void* workspace, smc_cvnn_pack* out) {
+  if (!out || !workspace) return fail(SMC_ERR_INVALID_ARGUMENT, "smc_cvnn_mfma_pack_plan: null argument");
+  Plan p;
+  const int32_t rc = make_plan(layers, n_layers, mode, batch, 0, &p);
+  if (rc != SMC_OK) return rc;
+  *out = smc_cvnn_pack{};
+  out->ws = workspace;
+  out->bf16 = mode == SMC_CVNN_MFMA_BF16 ? 1 : 0;
+  if (p.a.layered) return SMC_OK;  // the layered GEMM path packs Wc with its bias column itself
+  out->n_layers = n_layers;
+  for (int l = 0; l < n_layers; ++l) {
+    const MLayer& m = p.a.layer[l];
+    out->layer[l] = smc_cvnn_pack_layer{layers[l].w_re, layers[l].w_im, m.ni, m.no, m.win, m.wout, m.wc, m.wct};
+  }
+  return SMC_OK;
 }
 
 }  // extern "C"

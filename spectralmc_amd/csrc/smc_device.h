@@ -211,4 +211,21 @@ __device__ void fft_row(const double* avg, const double* cs, const double* sn, i
 }
 
 }  // namespace
+// bf16 rounding (round to nearest even, torch's float -> bfloat16; NaN kept quiet) of the MFMA operands
+__host__ __device__ inline float bf16_round(float x) {
+  uint32_t u;
+  __builtin_memcpy(&u, &x, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) {
+    u |= 0x00400000u;  // quiet NaN
+  } else {
+    u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (torch's float -> bfloat16)
+  }
+  u &= 0xffff0000u;
+  float y;
+  __builtin_memcpy(&y, &u, 4);
+  return y;
+}
+
+__device__ __forceinline__ uint16_t bf16_bits(float x) { return static_cast<uint16_t>(__float_as_uint(bf16_round(x)) >> 16); }
+
 }  // namespace smc

@@ -929,6 +929,9 @@ class TrainingSession:
         self.capture_graphs = (getattr(eng, "B", 0) * getattr(eng, "P", 0) * getattr(eng, "T", 0) >=
                                pricer.graph_min_path_steps)
         self.mc_events: list[tuple[torch.cuda.Event, torch.cuda.Event]] | None = None
+        #: timing-event pairs the live MC timing takes before creating new ones (created and recorded once
+        #: beforehand, so a timed loop pays no event creation)
+        self.mc_event_pool: list[tuple[torch.cuda.Event, torch.cuda.Event]] = []
         self._closed = False
         # exchanging path launches wait for the previous step's network part (pricer.exchange_after_network)
         order = pricer.exchange_after_network
@@ -1039,7 +1042,8 @@ class TrainingSession:
         if self._slot_used[slot]:
             ms.wait_event(self._nn_done[slot])
         if self.mc_events is not None:  # live timing of the MC part on its own stream
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, e1 = (self.mc_event_pool.pop() if self.mc_event_pool else
+                      (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
             e0.record(ms)
             self.program.run_mc(slot, handle)
             e1.record(ms)

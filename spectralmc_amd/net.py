@@ -163,6 +163,18 @@ class FusedNetworkStep:
                                        norm_partials=_lib.ptr(self.norm_partials), grad_norm=_lib.ptr(grad_norm_out),
                                        loss=_lib.ptr(loss_out))
         self.fuse_adam = fuse_adam
+        # MFMA (non-layered plans): Adam also writes the packed operand copies of the weights it updates, so
+        # every fwd_bwd after the first skips its pack launch (SMC_CVNN_MFMA_PACKED; the e2e network chain's
+        # 9 us pack_kernel, profiles/r05/)
+        self._pack = None
+        self._packed = False
+        if self.mode:
+            pk = _lib.CvnnPack()
+            _lib.check(L.smc_cvnn_mfma_pack_plan(self._layers, len(self.table), self.mode, batch,
+                                                 _lib.ptr(self.workspace), ctypes.byref(pk)))
+            if pk.n_layers > 0:
+                self._pack = pk
+                self.adam_args.pack = ctypes.addressof(pk)
 
     def fwd_bwd(self, real_in: torch.Tensor, imag_in: torch.Tensor | None, targets: torch.Tensor,
                 stream: int | None = None) -> None:
@@ -171,8 +183,9 @@ class FusedNetworkStep:
         L = _lib.lib()
         stream = stream if stream is not None else _lib.stream_handle()
         if self.mode:
+            mode = self.mode | (_lib.CVNN_MFMA_PACKED if self._packed else 0)
             _lib.check(L.smc_cvnn_mfma_forward_backward(
-                self._layers, len(self.table), self.mode, _lib.ptr(self.params_flat), self.n, _lib.ptr(real_in),
+                self._layers, len(self.table), mode, _lib.ptr(self.params_flat), self.n, _lib.ptr(real_in),
                 _lib.ptr(imag_in) if imag_in is not None else None, _lib.ptr(targets), self.batch,
                 _lib.ptr(self.partials), self.blocks, _lib.ptr(self.workspace), self.workspace.numel(), stream))
         else:
@@ -184,6 +197,8 @@ class FusedNetworkStep:
         _lib.check(L.smc_cvnn_reduce_grads(self.dtype_code, _lib.ptr(self.partials), self.blocks, self.n,
                                            _lib.ptr(self.grads),
                                            ctypes.byref(self.adam_args) if self.fuse_adam else None, stream))
+        if self.fuse_adam and self._pack is not None:
+            self._packed = True  # this update wrote the operand copies the next forward_backward reads
 
     @property
     def kernels(self) -> str:
@@ -194,6 +209,8 @@ class FusedNetworkStep:
         _lib.check(_lib.lib().smc_adam_step(self.dtype_code, self.n, _lib.ptr(self.grads),
                                             ctypes.byref(self.adam_args),
                                             stream if stream is not None else _lib.stream_handle()))
+        if self._pack is not None:
+            self._packed = True
 
 
 __all__ = ["FusedNetworkStep", "UnsupportedNetwork", "lower"]

@@ -119,6 +119,44 @@ def test_mfma_step_bit_reproducible(compute, arch) -> None:
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("compute,arch,n_out,B", [("mfma", "c2", 256, 1000), ("bf16", "zrelu", 64, 333),
+                                                  ("mfma", "lastact", 96, 4096), ("mfma", "h128", 64, 500)])
+@pytest.mark.parametrize("dp", [False, True])
+def test_adam_written_packed_weights_equal_the_pack_launch(compute, arch, n_out, B, dp) -> None:
+    """Adam writes the MFMA operand copies of the weights it updates (smc_cvnn_pack), so every fwd_bwd after
+    the first skips pack_kernel (SMC_CVNN_MFMA_PACKED): four steps equal, bit for bit (parameters, Adam
+    moments, loss, grad norm), four steps that run the pack launch every time; fused Adam and the separate
+    data-parallel update alike; the layered GEMM path (h128) keeps its own pack launch."""
+    runs = []
+    for packed in (True, False):
+        model = build(arch, n_out)
+        params = list(model.parameters())
+        adam = torch.optim.Adam(params, lr=1e-2)
+        n = sum(p.numel() for p in params)
+        flat = torch.zeros(n + 1, dtype=torch.float32, device=DEV)
+        loss = torch.zeros((), dtype=torch.float32, device=DEV)
+        gn = torch.zeros((), dtype=torch.float32, device=DEV)
+        step = FusedNetworkStep(model, adam, params, flat, loss, gn, B, fuse_adam=not dp, compute=compute)
+        assert (step._pack is not None) == (arch != "h128")
+        if not packed:
+            step._pack = None
+            step.adam_args.pack = None
+        losses = []
+        for k in range(4):
+            x, t = data(B, n_out, seed=20 + k)
+            xd = x.to(DEV)
+            step.fwd_bwd(xd, torch.zeros_like(xd), t.to(DEV))
+            if dp:
+                step.adam()
+            losses.append((float(loss), float(gn)))
+        torch.cuda.synchronize()
+        assert step._packed == (packed and arch != "h128")
+        runs.append((step.params_flat.cpu(), step.exp_avg.cpu(), step.exp_avg_sq.cpu(), losses))
+    (pa, ma, va, la), (pb, mb, vb, lb) = runs
+    assert torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(va, vb)
+    assert la == lb
+
+
 def test_auto_uses_mfma_for_f32_and_valu_for_f64() -> None:
     m32 = build("c2", 256)
     s32, _ = gpu_grads(m32, "auto", *data(64, 256))
