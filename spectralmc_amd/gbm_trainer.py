@@ -458,10 +458,11 @@ class GbmCVNNPricer:
     mc_lanes: int = 2
     #: ... and this many when the fused network is narrow (every layer input < 128 complex features: the
     #: fb_kernel path on network_cus CUs) and one path launch does at least mc_lanes_long_path_steps
-    #: path-steps.  4 lanes at C2 measured 2.855-2.888 against 2.957 ms/step on one box and 2.970-2.974
-    #: against 2.958 on another; slower at the lock-step (0.30 -> 0.36-0.38) and e2e shapes and beside
-    #: the wide C2/H=256 network (3.03 -> 3.07) (profiles/r04/mc_lanes.txt): the default stays 2
-    mc_lanes_long: int = 2
+    #: path-steps.  Round 5, three boxes: C2 2.69-2.79 / 2.94-2.95 / 2.69-2.79 ms/step with 4 lanes against
+    #: 2.95-3.00 with 2 (profiles/r05/ab_c2_lanes4.txt; round 4 had measured one box better, one equal): four
+    #: launches in flight keep more write streams open.  Not taken at the lock-step and e2e shapes (slower
+    #: there, profiles/r04/mc_lanes.txt) nor beside the wide C2/H=256 network (3.03 -> 3.07)
+    mc_lanes_long: int = 4
     mc_lanes_long_path_steps: int = 1 << 30
     #: ... and this many for launches below network_cu_min_path_steps path-steps, where the network chain, not the
     #: path launch, sets the step time and a second launch in flight only slows it (the reference's e2e shape:

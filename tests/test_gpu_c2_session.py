@@ -1,10 +1,10 @@
 """The timed C2 session end to end (BASELINE configs[1], north_star's own acceptance criterion):
 ``GbmCVNNPricer`` built and configured exactly as ``bench.py`` builds it for the driver's default run
 (``bench.make_pricer(bench.parse([]))``: B = 4096 contracts x 65,536 paths, T = 16, N = M = 256,
-6 -> 32 -> 32 -> 256 CVNN, hw math, full path store, 2 MC lanes, the network on a 32-CU masked stream,
+6 -> 32 -> 32 -> 256 CVNN, hw math, full path store, 4 MC lanes (mc_lanes_long), the network on a 32-CU masked stream,
 per-slot hipGraphs after 2 eager steps, next step's MC part prefetched beside the network part).
 
-* three steps (the third a graph replay on lane 0) bit-identical to the same pricer with
+* three steps (the third a graph replay) bit-identical to the same pricer with
   ``overlap_mc = False`` (one stream, one graph per step);
 * every step's targets (all 4096 contracts of step 1, a strided sample of steps 2 and 3, which ran on
   lane 1 and as a graph replay) within 1e-5 per contract of the reference-mode oracle
@@ -75,7 +75,7 @@ def overlapped():
 def test_c2_session_uses_the_bench_policy(overlapped) -> None:
     facts = overlapped[4]
     assert facts["kernel"] == "resident_kernel"
-    assert facts["lanes"] == 2 and facts["network_cus"] == 32 and facts["captured"]
+    assert facts["lanes"] == 4 and facts["network_cus"] == 32 and facts["captured"]
 
 
 def test_c2_session_equals_one_stream_run(overlapped) -> None:
