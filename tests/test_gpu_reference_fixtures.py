@@ -37,7 +37,7 @@ def gbm_golden() -> dict[str, np.ndarray]:
 
 
 def train_targets(contracts: np.ndarray, m: dict, *, hw: bool, padded: bool = True, seed: int | None = None,
-                  ordinal0: int | None = None) -> np.ndarray:
+                  ordinal0: int | None = None, ref: bool = False) -> np.ndarray:
     """smc_train_targets as the trainer calls it: STORE_ALL, no row-sum buffer (terminal sum on
     chip), padded scratch pitch, one launch."""
     B = contracts.shape[0]
@@ -49,7 +49,7 @@ def train_targets(contracts: np.ndarray, m: dict, *, hw: bool, padded: bool = Tr
     paths = poisoned((B, T, pitch), torch.float32 if f32 else torch.float64, DEV)
     tg = poisoned((B, N), torch.complex64 if f32 else torch.complex128, DEV)
     cd = torch.from_numpy(np.ascontiguousarray(contracts)).to(DEV)
-    scheme = m["scheme"] | (_lib.MATH_HW if hw else 0)
+    scheme = m["scheme"] | (_lib.MATH_HW if hw else 0) | (_lib.MATH_REF if ref else 0)
     _lib.check(_lib.lib().smc_train_targets(
         _lib.ptr(cd), B, T, N, M, m["seed"] if seed is None else seed, None,
         m["ordinal0"] if ordinal0 is None else ordinal0, scheme, _lib.NORM_NORMALIZE if m["normalize"] else
@@ -78,6 +78,20 @@ def test_portable_math_targets_bit_exact_and_match_reference(oracle, gbm_golden,
         assert per_contract_rel(got, want).max() < 5e-6
     else:
         assert per_contract_rel(got, want).max() < 1e-10
+
+
+@pytest.mark.parametrize("name", [n for n in CASE_NAMES if "f64" not in n])
+def test_reference_math_targets_bit_exact_and_match_reference(oracle, gbm_golden, name) -> None:
+    """SMC_MATH_REF (the reference kernel's own typing, rows_ref_kernel) on every f32 fixture case: bit-exact
+    with its kernel-mode restatement and within 4e-6 per contract of the reference's own targets (the paths
+    agree with the reference arithmetic to the bit, tests/test_oracle.py; what is left is the CF phase's f64
+    sums against the reference's f32 normalisation)."""
+    contracts, want, m = unpack(gbm_golden, name)
+    got = train_targets(contracts, m, hw=False, ref=True)
+    kt, _ = oracle.kernel_targets(contracts, m["T"], m["N"], m["M"], seed=m["seed"], ordinal0=m["ordinal0"],
+                                  scheme=m["scheme"] | oracle.MATH_REF, normalize=m["normalize"])
+    np.testing.assert_array_equal(got, kt)
+    assert per_contract_rel(got, want).max() < 4e-6
 
 
 def test_c2_bench_instantiation_whole_rounds(oracle, gbm_golden) -> None:
