@@ -107,7 +107,9 @@ class TrainingEngine:
                                    imag_in=torch.zeros_like(real_in),
                                    targets=torch.empty((B, self.N), dtype=cplx, device=device))
         # scratch rows at a padded pitch: a power-of-two row stride aliases in HBM
-        self.pitch = int(_lib.lib().smc_path_pitch(self.P, self._dtype_code))
+        # (math="reference": rows_ref_kernel keeps the terminal sum in the row padding, so the pitch must leave
+        # room after column P even where P is itself an odd multiple of 4 KiB)
+        self.pitch = int(_lib.lib().smc_path_pitch(self.P + (4 if math == "reference" else 0), self._dtype_code))
         per_contract = (self.T * self.pitch if store_paths else self.pitch) * torch.finfo(sim_torch).bits // 8
         budget = path_buffer_bytes if path_buffer_bytes is not None else path_buffer_budget(device)
         max_chunk = max(1, min(B, budget // per_contract))

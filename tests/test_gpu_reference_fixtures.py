@@ -45,7 +45,8 @@ def train_targets(contracts: np.ndarray, m: dict, *, hw: bool, padded: bool = Tr
     P = N * M
     f32 = m["dtype"] == "float32"
     dcode = _lib.DTYPE_F32 if f32 else _lib.DTYPE_F64
-    pitch = int(_lib.lib().smc_path_pitch(P, dcode)) if padded else P
+    # (reference math: room for the terminal sum after column P even where P is an odd multiple of 4 KiB)
+    pitch = int(_lib.lib().smc_path_pitch(P + (4 if ref else 0), dcode)) if padded else P
     paths = poisoned((B, T, pitch), torch.float32 if f32 else torch.float64, DEV)
     tg = poisoned((B, N), torch.complex64 if f32 else torch.complex128, DEV)
     cd = torch.from_numpy(np.ascontiguousarray(contracts)).to(DEV)
