@@ -606,9 +606,9 @@ def main() -> None:
                      "algorithmic_bytes_survey_per_launch": bytes_survey,
                      # the f64 rows kernel is bound by VALU issue at the clock the chip sustains under it, not
                      # by HBM (PMC): the HBM fraction above is not its ceiling
-                     "bound_note": ("rows_kernel (f64) is VALU-issue bound: 42 VALU instructions per path-step hold "
-                                    "the SIMDs ~88 % of the launch at the ~1.65 GHz it runs at "
-                                    "(profiles/r04/pmc/clock_valu.txt)" if eng.kernel_name.startswith("rows_")
+                     "bound_note": ("rows_kernel (f64) runs at the clock the power limiter allows (1.3-1.66 GHz): 38 VALU "
+                                    "instructions per path-step (math v4) hold the SIMDs 81-84 % of the launch "
+                                    "(profiles/r05/pmc_f64_v4.txt)" if eng.kernel_name.startswith("rows_")
                                    and f64 else None),
                      "bytes_note": ("the kernel keeps each contract's terminal row on chip: achieved counts the path "
                                     "store, targets and contract rows, not the terminal re-read of SURVEY 8(d)'s "

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: the --native-step option and smc_session_step were reverted after this measurement,
+#  profiles/r05/ab_native_session_step.txt; the script no longer runs against the current tree)
 # native steady-state step: trainer / session GPU tests, then bench lines with the native step on and off
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
