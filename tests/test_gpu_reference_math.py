@@ -141,3 +141,16 @@ def test_trainer_reference_math_one_step_matches_oracle(oracle) -> None:
     ref = oracle.torch_step(cpu_model, x, torch.zeros_like(x), torch.from_numpy(kt),
                             torch.optim.Adam(cpu_model.parameters(), lr=1e-2))
     assert res.final_loss == pytest.approx(ref.loss, rel=1e-4)
+
+
+def test_reference_math_chunked_launches_equal_one_launch(oracle, golden) -> None:
+    """smc_train_targets in reference math over chunked launches (three chunks, a ragged last one) gives the
+    one-launch targets bit for bit."""
+    B, T, N, M = 600, 5, 64, 32
+    c = _contracts(oracle, golden, B, seed=7)
+    pitch = int(_L().smc_path_pitch(N * M, 0))
+    one, _, _ = _run_targets(c, T, N, M, 1, 1, "float32", _lib.STORE_TERMINAL, ordinal0=3, with_rowsum=False,
+                             flags=_lib.MATH_REF, pitch=pitch)
+    chunked, _, _ = _run_targets(c, T, N, M, 1, 1, "float32", _lib.STORE_TERMINAL, ordinal0=3, with_rowsum=False,
+                                 flags=_lib.MATH_REF, pitch=pitch, chunk=250)
+    np.testing.assert_array_equal(chunked, one)
