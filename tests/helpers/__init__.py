@@ -141,3 +141,27 @@ def poisoned(shape, dtype: torch.dtype, device) -> torch.Tensor:
 
 def poisoned_like(x: torch.Tensor) -> torch.Tensor:
     return poisoned(x.shape, x.dtype, x.device)
+
+
+def assert_rows_equal(got, want, err_msg: str = "", chunk: int | None = None) -> None:
+    """``np.testing.assert_array_equal`` whose failure names the rows (the first axis: contracts, points) that
+    differ, with (row within its launch) mod 8: the XCD the dispatcher deals workgroup w of a launch to when
+    contract b runs on workgroup b (paths_kernel, cf_kernel, contract_kernel; ``chunk`` = contracts per
+    launch of a chunked step).  A recurrence of a one-XCD fault (DESIGN.md section 3.2b') then carries its
+    location."""
+    got, want = np.asarray(got), np.asarray(want)
+    if got.shape != want.shape or got.ndim == 0:
+        np.testing.assert_array_equal(got, want, err_msg=err_msg)
+        return
+    g, w = got.reshape(got.shape[0], -1), want.reshape(want.shape[0], -1)
+    same = (g == w) | (np.isnan(g) & np.isnan(w)) if np.issubdtype(g.dtype, np.inexact) else (g == w)
+    bad = np.flatnonzero(~same.all(axis=1))
+    if bad.size == 0:
+        return
+    local = bad % chunk if chunk else bad
+    xcd = np.bincount(local % 8, minlength=8)
+    cnt = (~same[bad]).sum(axis=1)
+    raise AssertionError(
+        f"{err_msg}: {bad.size} of {g.shape[0]} rows differ ({int(cnt.sum())} values); rows {bad[:24].tolist()}"
+        f"{' ...' if bad.size > 24 else ''}; row-in-launch mod 8 histogram {xcd.tolist()}"
+        + (f" (chunk {chunk})" if chunk else "") + f"; first row {int(bad[0])}: got {g[bad[0]][:4]} want {w[bad[0]][:4]}")

@@ -88,6 +88,9 @@ for step in "$@"; do
     benchx:*)  # benchx:<tag>:<bench args with , for spaces> (no CPU leg)
       IFS=: read -r _ tag args <<< "$step"
       run "benchx_$tag" 600 python bench.py --no-cpu-baseline ${args//,/ } ;;
+    tests:*)  # tests:<tag>:<limit s>:<pytest targets / args with , for spaces>
+      IFS=: read -r _ tag lim targets <<< "$step"
+      run "tests_$tag" "$lim" python -u -m pytest ${targets//,/ } -m gpu -v -x --timeout 300 --timeout-method thread -p no:cacheprovider -rf ;;
     testk:*)  # testk:<pytest -k expression with , for spaces>
       IFS=: read -r _ expr <<< "$step"
       run testk 600 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -rf -k "${expr//,/ }" ;;
