@@ -64,8 +64,11 @@ extern "C" {
                                       only, not with SMC_MATH_HW): the reference kernel's own typing
                                       (gbm.py:224-257 under Numba: f64 state and step of the f32 normals,
                                       f32 stores): portable normals, the f64 engine's step, rounded f32
-                                      paths (rows_ref_kernel + cf_kernel); in the kernel queries' dtype:
-                                      that kernel's name */
+                                      paths (rows_ref_kernel + cf_kernel).  The f64 step's exp is within
+                                      2 ulp of libm's, so a stored f32 value equals the reference
+                                      arithmetic's except where the two exps round to different floats
+                                      (C2 shape: <= 1e-6 of the values, 1 ulp; tests/test_oracle.py); in
+                                      the kernel queries' dtype: that kernel's name */
 #define SMC_TRAIN_DYNAMIC    0x200  /* flag, OR into smc_train_step's `scheme`: the whole-contract resident
                                       launch hands out every contract from its contract queue (default:
                                       the first three quarters of the rounds statically), for launches that
@@ -197,8 +200,9 @@ int64_t smc_engine_workspace_bytes(int64_t chunk_contracts, int32_t timesteps, i
                                    int32_t all_rows);
 /* Name of the kernel smc_train_targets launches for this shape ("wave_kernel", "resident_kernel",
  * "packed_kernel", the split pairs, "contract_kernel", "queue_kernel" or "rows_ref_kernel+cf_kernel";
- * sliced = a workspace is passed; dtype | SMC_QUERY_RAW | SMC_MATH_REF as for smc_train_step_kernel).
- * Static string. */
+ * sliced = a workspace is passed; dtype | SMC_QUERY_RAW | SMC_MATH_REF as for smc_train_step_kernel;
+ * "unsupported" for an SMC_MATH_REF shape the engine rejects: f64, a pitch without room for the terminal
+ * sum, sliced).  Static string. */
 const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, int64_t n_paths,
                                      int32_t dtype, int64_t path_pitch, int32_t sliced);
 /* Recommended row pitch (elements) for a path scratch buffer of n_paths columns: the row
@@ -296,7 +300,11 @@ typedef struct smc_adam_args {
   double lr, beta1, beta2, eps, weight_decay;
   double* norm_partials;         /* [smc_adam_norm_partials(n_params)] scratch, ZEROED before
                                     the first call (its last slot is the fused finalize's
-                                    arrival counter; every call leaves it zero)            */
+                                    arrival counter; every COMPLETED call leaves it zero:
+                                    a caller that allocates it without zeroing, or reuses
+                                    it after a launch that did not complete, must zero it
+                                    again, else no workgroup counts as last and grad_norm,
+                                    loss and step stop being written)                      */
   void* grad_norm;               /* scalar out: ||grad||_2 (gbm_trainer.py:834)         */
   void* loss;                    /* scalar out: grads[n_params] (the loss slot)         */
   const smc_cvnn_pack* pack;     /* or NULL: the update also writes these packed copies (ABI 13) */
@@ -336,7 +344,11 @@ int64_t smc_adam_norm_partials(int64_t n_params);
 #define SMC_CVNN_MFMA_F32   1
 #define SMC_CVNN_MFMA_BF16  2
 #define SMC_CVNN_MFMA_PACKED 0x100  /* flag, OR into forward_backward's mode: the workspace already holds
-                                       the packed weights of params (the last Adam update wrote them) */
+                                       the packed weights of params (the last Adam update wrote them).
+                                       Valid only while params change through those updates alone: a
+                                       caller that writes params any other way (a state_dict load, a
+                                       broadcast) must drop the flag for the next call (net.py
+                                       FusedNetworkStep.invalidate_pack) */
 int32_t smc_cvnn_mfma_plan(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode, int64_t batch,
                            int64_t* partial_blocks, int64_t* workspace_bytes);
 int32_t smc_cvnn_mfma_forward_backward(const smc_cvnn_layer* layers, int32_t n_layers, int32_t mode,

@@ -2339,7 +2339,9 @@ const char* smc_train_step_kernel(int32_t timesteps, int32_t network_size, int32
   a.res_xsum = a.res_xcol = reinterpret_cast<double*>(&a);
   a.done = reinterpret_cast<uint32_t*>(&a);
   a.normalize = (dtype & SMC_QUERY_RAW) ? 0 : 1;
-  if (dtype & SMC_MATH_REF) return "rows_ref_kernel+cf_kernel";
+  a.store = SMC_STORE_ALL;
+  if (dtype & SMC_MATH_REF)  // the checks launch_engine makes (f32, the padded pitch, whole contracts)
+    return (dtype & 0xff) == SMC_DTYPE_F32 && ref_ok(a) ? "rows_ref_kernel+cf_kernel" : "unsupported";
   if (wave_ok(a, (dtype & 0xff) == SMC_DTYPE_F32)) return "wave_kernel";
   if (resident_ok(a, (dtype & 0xff) == SMC_DTYPE_F32))
     return a.res_slices > 1 ? "resident_kernel(sliced)" : "resident_kernel";
@@ -2364,7 +2366,8 @@ const char* smc_train_targets_kernel(int32_t timesteps, int32_t network_size, in
   a.store = SMC_STORE_ALL;
   const bool f32 = (dtype & 0xff) == SMC_DTYPE_F32;
   a.normalize = (dtype & SMC_QUERY_RAW) ? 0 : 1;
-  if (dtype & SMC_MATH_REF) return "rows_ref_kernel+cf_kernel";
+  if (dtype & SMC_MATH_REF)  // the checks launch_engine makes (f32, the padded pitch, no slices)
+    return f32 && ref_ok(a) ? "rows_ref_kernel+cf_kernel" : "unsupported";
   if (wave_ok(a, f32)) return "wave_kernel";
   if (resident_ok(a, f32)) return "resident_kernel";
   if (packed_ok(a, f32)) return "packed_kernel";

@@ -66,7 +66,6 @@ class TrainingEngine:
                  device: torch.device, rank: int = 0, world_size: int = 1, store_paths: bool = True,
                  path_buffer_bytes: int | None = None, math: str = "portable",
                  sliced: bool = False, lanes: int = 1) -> None:
-        _lib.require_device()
         sp = cfg.sim_params
         self.cfg = cfg
         self.B = batch_size
@@ -84,6 +83,11 @@ class TrainingEngine:
             raise ValueError(f"math must be 'portable', 'hw' or 'reference', got {math!r}")
         if math == "reference" and sp.dtype != Precision.float32:
             raise ValueError("math='reference' is the reference kernel's f32 typing (float32 simulations only)")
+        if math == "reference" and sliced:
+            # rows_ref_kernel runs whole contracts per workgroup: every sliced launch would fail INVALID_SHAPE
+            raise ValueError("math='reference' runs whole contracts per workgroup (rows_ref_kernel); sliced=True "
+                             "is not supported")
+        _lib.require_device()
         self.math = math
         # "hw": f32 hardware transcendentals in the path kernel (faster, ~1 ulp, not CPU-reproducible);
         # "reference": the reference kernel's typing (f64 state and step, f32 normals and stores: rows_ref_kernel)

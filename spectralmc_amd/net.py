@@ -165,7 +165,8 @@ class FusedNetworkStep:
         self.fuse_adam = fuse_adam
         # MFMA (non-layered plans): Adam also writes the packed operand copies of the weights it updates, so
         # every fwd_bwd after the first skips its pack launch (SMC_CVNN_MFMA_PACKED; the e2e network chain's
-        # 9 us pack_kernel, profiles/r05/)
+        # 9 us pack_kernel, profiles/r05/).  The model's parameters are views of params_flat: any write to them
+        # other than Adam's must be followed by invalidate_pack()
         self._pack = None
         self._packed = False
         if self.mode:
@@ -199,6 +200,12 @@ class FusedNetworkStep:
                                            ctypes.byref(self.adam_args) if self.fuse_adam else None, stream))
         if self.fuse_adam and self._pack is not None:
             self._packed = True  # this update wrote the operand copies the next forward_backward reads
+
+    def invalidate_pack(self) -> None:
+        """The parameters changed other than through this step's Adam update (a state_dict load into the live
+        model, a broadcast into params_flat): the next fwd_bwd runs its pack launch again instead of reading
+        the packed operand copies the last update wrote (SMC_CVNN_MFMA_PACKED, include/spectralmc_hip.h)."""
+        self._packed = False
 
     @property
     def kernels(self) -> str:

@@ -217,6 +217,36 @@ def test_train_targets_kernel_choice() -> None:
     assert L.smc_train_targets_kernel(16, 256, 65536, 1, 0, 0) == b"contract_kernel"        # f64, no padding
     assert L.smc_train_targets_kernel(16, 6, 6144, 0, 6144, 0) == b"contract_kernel"        # pitch == P
     assert L.smc_train_targets_kernel(16, 6, 6144, 0, 7168, 0) == split                     # N not | 4096
+    # SMC_MATH_REF: the name only where launch_engine takes the shape
+    ref = _lib.MATH_REF
+    assert L.smc_train_targets_kernel(16, 256, 65536, ref, 66560, 0) == b"rows_ref_kernel+cf_kernel"
+    assert L.smc_train_step_kernel(16, 256, 256, ref, 66560) == b"rows_ref_kernel+cf_kernel"
+    assert L.smc_train_targets_kernel(16, 256, 65536, 1 | ref, 66560, 0) == b"unsupported"  # f64
+    assert L.smc_train_targets_kernel(16, 256, 65536, ref, 0, 0) == b"unsupported"          # no room for the sum
+    assert L.smc_train_step_kernel(16, 256, 256, ref, 65536) == b"unsupported"
+    assert L.smc_train_targets_kernel(16, 256, 65536, ref, 66560, 1) == b"unsupported"      # sliced
+
+
+def test_engine_rejects_reference_math_it_cannot_run() -> None:
+    """TrainingEngine(math="reference") fails at construction (before touching a device) for f64 and for
+    sliced engines, instead of on the first step's launch."""
+    import torch
+
+    from spectralmc_amd.engine import TrainingEngine
+    from spectralmc_amd.gbm import BlackScholes
+    from spectralmc_amd.models.numerical import Precision
+    from spectralmc_amd.sobol_sampler import SobolSampler, build_sobol_config
+    from tests.helpers import expect_success, make_black_scholes_config, make_domain_bounds, make_simulation_params
+
+    for dtype, sliced, msg in ((Precision.float32, True, "sliced"), (Precision.float64, False, "float32")):
+        sp = make_simulation_params(timesteps=16, network_size=64, batches_per_mc_run=8, threads_per_block=256,
+                                    mc_seed=7, buffer_size=4, dtype=dtype)
+        cfg = make_black_scholes_config(sim_params=sp)
+        sampler = expect_success(SobolSampler.create(BlackScholes.Inputs, make_domain_bounds(),
+                                                     config=build_sobol_config(seed=7, skip=0).unwrap()))
+        with pytest.raises(ValueError, match=msg):
+            TrainingEngine(cfg, sampler, 4, model_dtype=torch.float32, device=torch.device("cpu"), math="reference",
+                           sliced=sliced)
 
 
 def test_basket_entry_points_validate_before_any_device_work() -> None:

@@ -212,3 +212,38 @@ def test_c3_training_session_on_bf16_kernels(oracle) -> None:
     assert np.linalg.norm(got - g) / np.linalg.norm(g) < 2e-3
     res = expect_success(pricer.train(make_training_config(num_batches=2, batch_size=B, learning_rate=1e-2)))
     assert np.isfinite(res.final_loss)
+
+
+def test_invalidate_pack_after_an_in_place_parameter_write() -> None:
+    """The packed MFMA weight copies are written by Adam only: parameters written in place mid-session (here
+    halved through the model's views) followed by invalidate_pack() give the step a pack launch every time
+    gives, bit for bit; without invalidate_pack the next step would read the stale copies."""
+    B = 1000
+    runs = {}
+    for mode in ("packed", "always_pack", "stale"):
+        model = build("c2", 256)
+        params = list(model.parameters())
+        adam = torch.optim.Adam(params, lr=1e-2)
+        n = sum(p.numel() for p in params)
+        flat = torch.zeros(n + 1, dtype=torch.float32, device=DEV)
+        loss = torch.zeros((), dtype=torch.float32, device=DEV)
+        gn = torch.zeros((), dtype=torch.float32, device=DEV)
+        step = FusedNetworkStep(model, adam, params, flat, loss, gn, B, fuse_adam=True, compute="mfma")
+        if mode == "always_pack":
+            step._pack = None
+            step.adam_args.pack = None
+        for k in range(4):
+            if k == 2:
+                with torch.no_grad():
+                    for p in params:
+                        p.mul_(0.5)
+                if mode != "stale":
+                    step.invalidate_pack()
+            x, t = data(B, 256, seed=40 + k)
+            xd = x.to(DEV)
+            step.fwd_bwd(xd, torch.zeros_like(xd), t.to(DEV))
+        torch.cuda.synchronize()
+        runs[mode] = (step.params_flat.cpu(), float(loss), float(gn))
+    assert torch.equal(runs["packed"][0], runs["always_pack"][0])
+    assert runs["packed"][1:] == runs["always_pack"][1:]
+    assert not torch.equal(runs["stale"][0], runs["always_pack"][0])

@@ -35,6 +35,8 @@ def main() -> None:
     ap.add_argument("--lanes", type=int, default=1, help="launches alternate over this many streams, each with "
                     "its own cursor, sync area and path scratch (consecutive launches may overlap)")
     ap.add_argument("--dynamic", action="store_true", help="SMC_TRAIN_DYNAMIC: every contract from the queue")
+    ap.add_argument("--trace", default="", help="trace variant library (tools/micro/trace_variant.sh): after the timed "
+                    "loop run one launch alone and save its per-workgroup timestamps to this .npy file")
     ap.add_argument("--norm", default="", choices=["", "raw", "normalize"],
                     help="targets normalisation (default: RAW for the lock-step shape, else NORMALIZE)")
     a = ap.parse_args()
@@ -104,8 +106,44 @@ def main() -> None:
     name = L.smc_train_step_kernel(T, N, M, dcode | (_lib.QUERY_RAW if raw else 0) |
                                    (_lib.MATH_REF if a.math == "reference" else 0), pitch).decode()
     ms = e0.elapsed_time(e1) / a.iters
+    if a.trace:
+        import ctypes
+
+        buf = np.zeros((4096, 40), dtype=np.uint64)
+        L.smc_trace_copy.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        assert L.smc_trace_copy(buf.ctypes.data, 1) == 0
+        torch.cuda.synchronize()
+        step()
+        torch.cuda.synchronize()
+        assert L.smc_trace_copy(buf.ctypes.data, 0) == 0
+        np.save(a.trace, buf)
+        summarize(buf)
     print(f"{a.config} {'raw' if raw else 'normalize'} pitch={pitch} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
           f"({launches} launch(es) of {chunk}), checksum {float(t.abs().double().mean()):.6g}")
+
+
+def summarize(buf: np.ndarray) -> None:
+    """Per-workgroup timeline of one launch (trace variant): start spread, per-XCD end times, idle tail."""
+    used = buf[:, 39] > 0
+    t = buf[used].astype(np.int64)
+    us = 0.01  # s_memrealtime: 100 MHz
+    t0 = t[:, 0].min()
+    start, end = (t[:, 0] - t0) * us, (t[:, 39] - t0) * us
+    span = end.max()
+    print(f"trace: {used.sum()} workgroups, span {span:.1f} us, starts {start.min():.1f}..{start.max():.1f} us, "
+          f"ends {end.min():.1f}..{end.max():.1f} us, mean idle tail {np.mean(span - end):.1f} us "
+          f"({np.mean(span - end) / span:.2%} of the CU-time)")
+    rounds = t[:, 38]
+    print(f"  contracts per workgroup: min {rounds.min()} max {rounds.max()} mean {rounds.mean():.2f}")
+    for x in sorted(set(t[:, 1].tolist())):
+        m = t[:, 1] == x
+        per = (t[m, 39] - t[m, 0]) * us / np.maximum(rounds[m], 1)
+        print(f"  XCC {x}: {m.sum()} WGs, end {end[m].min():.1f}..{end[m].max():.1f} us, "
+              f"{per.mean():.1f} us per contract, contracts {rounds[m].min()}..{rounds[m].max()}")
+    first = (t[:, 2] - t[:, 0]) * us
+    print(f"  first contract {first.mean():.1f} us (min {first.min():.1f} max {first.max():.1f})")
+    last_start = np.array([(t[i, 2 + r - 2] if r >= 2 else t[i, 0]) for i, r in enumerate(rounds)], dtype=np.int64)
+    print(f"  last contract starts {((last_start - t0) * us).min():.1f}..{((last_start - t0) * us).max():.1f} us")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,37 @@
+#!/bin/bash
+# Builds tools/micro/v/libsmc_trace.so: resident_kernel with per-workgroup s_memrealtime stamps (kernel start, XCC id,
+# end of every contract round, kernel end) in a device array read back by smc_trace_copy (tools/kprof_step.py --trace).
+# No hooks in the product sources: make_variant.py applies literal edits to a scratch copy.
+set -e
+cd "$(dirname "$0")/../.."
+python tools/micro/make_variant.py trace${1:+_$1} \
+  gbm.hip 'constexpr int kResThreads = 1024;' '__device__ unsigned long long g_trace[4096 * 40];
+constexpr int kResThreads = 1024;' \
+  gbm.hip '  static_assert(!(ONTHEFLY && T16), "the on-the-fly CF phase is instantiated for the rolled row loop only");' '  static_assert(!(ONTHEFLY && T16), "the on-the-fly CF phase is instantiated for the rolled row loop only");
+  unsigned long long* tr = g_trace + (blockIdx.x & 4095) * 40;
+  if (threadIdx.x == 0) {
+    unsigned xcc_ = 0;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));
+    tr[0] = __builtin_amdgcn_s_memrealtime();
+    tr[1] = xcc_;
+  }' \
+  gbm.hip '    fft_row<float, kResThreads, true>(avg, cs, sn, N, part, part + N, static_cast<float2*>(a.targets) + b * N);
+    lds_barrier();  // part (= term_lds) / avg / wsum / row are reused by the next contract' '    fft_row<float, kResThreads, true>(avg, cs, sn, N, part, part + N, static_cast<float2*>(a.targets) + b * N);
+    lds_barrier();  // part (= term_lds) / avg / wsum / row are reused by the next contract
+    if (tid == 0 && round < 36) tr[2 + round] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) tr[38] = round + 1;' \
+  gbm.hip '  if (a.done && tid == 0) {
+    // every workgroup read the cursor (and made its last exchange)' '  if (tid == 0) tr[39] = __builtin_amdgcn_s_memrealtime();
+  if (a.done && tid == 0) {
+    // every workgroup read the cursor (and made its last exchange)' \
+  gbm.hip '#pragma GCC visibility pop
+}  // extern "C"' '__attribute__((visibility("default"))) int32_t smc_trace_copy(void* dst, int32_t clear) {
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(smc::g_trace), sizeof(smc::g_trace)) != hipSuccess) return 1;
+  if (clear) {
+    static unsigned long long zeros[4096 * 40];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(smc::g_trace), zeros, sizeof(zeros)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#pragma GCC visibility pop
+}  // extern "C"'
