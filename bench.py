@@ -208,6 +208,32 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
                    f"({t_nn * 1e3:.1f} ms)"),
         "cpu_model": cpu_model,
     }
+    # the same leg on every core of the process's affinity set (BASELINE.md section 2.2 plans
+    # torch.set_num_threads(len(os.sched_getaffinity(0)))): the GPU box shows the whole host there, while one
+    # GPU's job gets a 16-core share (OMP_NUM_THREADS), which the leg above uses
+    aff = len(os.sched_getaffinity(0))
+    if aff != threads and not n_assets:
+        torch.set_num_threads(aff)
+        try:
+            per_a, done_a, _ = sample(lambda c, o: cpu_path_targets(c, T, N, M, 7, o, dtype=dtype, normals="numpy",
+                                                                    normalize=normalize, workers=min(aff, 64)),
+                                      budget_s * 0.4, 2 * min(aff, 64))
+            oracle.torch_step(model, x, torch.zeros_like(x), tgt, adam)  # warm at this thread count
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                oracle.torch_step(model, x, torch.zeros_like(x), tgt, adam)
+            t_nn_a = (time.perf_counter() - t0) / reps
+        finally:
+            torch.set_num_threads(threads)
+        line["affinity_leg"] = {
+            "value": B * N * M / (per_a * B + t_nn_a), "unit": "contracts*paths/s", "cores": aff, "kind": "port",
+            "sample": (f"{path}, {aff} threads (torch.set_num_threads(len(os.sched_getaffinity(0)))), on "
+                       f"{done_a}/{B} contracts ({per_a * done_a:.1f}s), extrapolated x{B / done_a:.1f}, + full B={B} "
+                       f"CVNN/Adam step ({t_nn_a * 1e3:.1f} ms)")}
+    else:
+        line["affinity_leg"] = {"value": line["value"], "unit": "contracts*paths/s", "cores": aff, "kind": "port",
+                                "sample": "the affinity set is the leg above's thread count" if aff == threads else
+                                "basket: kernel-mode C oracle leg only"}
     if not n_assets:
         # second leg: the C/OpenMP oracle (f64 recursion, this build's normal streams)
         per_c2, done2, _ = sample(lambda c, o: oracle.training_targets(c, T, N, M, seed=7, ordinal0=o, dtype=dtype,
