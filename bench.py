@@ -433,6 +433,9 @@ def main() -> None:
                          "allreduce_per_step": 1,
                          "allreduce_ms_in_step": (sum(ar) / len(ar)) if ar else None,
                          "allreduce_ms_isolated": float(iso.item()),
+                         "collective_stream": ("the step's network stream (dp.RcclComm: ncclAllReduce on it, CU-masked "
+                                               "with the network)" if ctx.comm is not None else
+                                               "torch.distributed's internal stream"),
                          "note": "allreduce_ms_in_step: HIP events around each step's eager all-reduce (sum, then / "
                                  "world) on the network stream inside the timed region (rank 0); isolated: 20 "
                                  "back-to-back all-reduces of the same buffer after it, max over ranks"}
@@ -464,7 +467,30 @@ def main() -> None:
             run_kernel()
         ev1.record(stream)
     ev1.synchronize()
-    kernel_ms = ev0.elapsed_time(ev1) / (args.kernel_iters * launches_per_call)
+    kernel_ms_events = ev0.elapsed_time(ev1) / (args.kernel_iters * launches_per_call)
+    # the same launches again, each call's kernels timed by their own execution timestamps (smc_time_launches:
+    # hipExtLaunchKernel start / stop events, the figure a kernel trace gives, without the dispatch gap a pair
+    # of stream events around back-to-back launches also holds: round 5's e2e line was +3.4 % against rocprof)
+    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+             for _ in range(args.kernel_iters)]
+    with torch.cuda.stream(stream):
+        for t0_, t1_ in pairs:  # create the events (recorded once by torch), then arm them per call
+            t0_.record(stream)
+            t1_.record(stream)
+        for t0_, t1_ in pairs:
+            # each call alone (the stream drained first): a kernel queued behind the previous call's would take its
+            # start timestamp while it still waits for it
+            stream.synchronize()
+            _lib.check(L.smc_time_launches(t0_.cuda_event, t1_.cuda_event))
+            try:
+                run_kernel()
+            finally:
+                _lib.check(L.smc_time_launches(None, None))
+    stream.synchronize()
+    kernel_ms = sum(t0_.elapsed_time(t1_) for t0_, t1_ in pairs) / (args.kernel_iters * launches_per_call)
+    kernel_timing = (f"mean over {args.kernel_iters} calls, each alone on the drained stream, of the first kernel's "
+                     "start to the last kernel's end (smc_time_launches: hipExtLaunchKernel events); kernel_ms_events: "
+                     f"HIP events around the {args.kernel_iters} back-to-back calls")
     contracts_per_launch = min(eng.chunk, eng.B)
     if n_assets:
         bytes_survey = eng.algorithmic_bytes_per_contract() * contracts_per_launch
@@ -613,7 +639,9 @@ def main() -> None:
                      "traffic_source": traffic_src,
                      # bytes the kernel actually moved (PMC) over its live time, against the same peak
                      "frac_moved": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                     "kernel_ms": kernel_ms, "kernel_ms_isolated": kernel_ms, "live_launches": len(live),
+                     "kernel_ms": kernel_ms, "kernel_ms_isolated": kernel_ms, "kernel_timing": kernel_timing,
+                     "kernel_ms_events": kernel_ms_events,
+                     "live_launches": len(live),
                      # one MC lane: the launch inside the timed region (HIP events on the MC stream), next to the
                      # network kernels of the previous step
                      "kernel_ms_live": live_ms,
@@ -655,6 +683,7 @@ def main() -> None:
         print(json.dumps(line), flush=True)
     if ctx:
         dist.barrier()
+        dp.shutdown()
         dist.destroy_process_group()
 
 

@@ -40,7 +40,7 @@ TRAIN_DYNAMIC = 0x200
 MATH_REF = 0x400  # the reference kernel's typing: f64 state and step, f32 normals and stores
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 
@@ -48,6 +48,7 @@ _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
 SIGNATURES: dict[str, tuple[Any, list[Any]]] = {
     "smc_abi_version": (_c_i32, []),
     "smc_last_error_string": (ctypes.c_char_p, []),
+    "smc_time_launches": (_c_i32, [_c_vp, _c_vp]),
     "smc_sync_status": (_c_i32, [_c_vp, _c_i32, ctypes.POINTER(_c_i32), _c_vp]),
     "smc_sobol_create": (_c_i32, [_c_i32, _c_u64, _c_u64, ctypes.POINTER(_c_vp)]),
     "smc_sobol_destroy": (None, [_c_vp]),

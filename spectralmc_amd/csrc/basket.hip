@@ -698,7 +698,7 @@ int32_t launch_basket_mode(const BasketArgs& a, hipStream_t stream) {
     (void)hipGetLastError();
     return fail(SMC_ERR_HIP, "basket_kernel: cannot raise the dynamic LDS limit");
   }
-  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(kBThreads), lds, stream, a);
+  launch(kernel, dim3(static_cast<unsigned>(a.B)), dim3(kBThreads), lds, stream, a);
   return check_launch("basket_kernel");
 }
 
@@ -714,7 +714,7 @@ int32_t launch_basket_k(const BasketArgs& a, hipStream_t stream) {
     (void)hipGetLastError();
     return fail(SMC_ERR_HIP, "basket_cf_kernel: cannot raise the dynamic LDS limit");
   }
-  hipLaunchKernelGGL(cf, dim3(static_cast<unsigned>(a.B)), dim3(kBThreads), lds, stream, a);
+  launch(cf, dim3(static_cast<unsigned>(a.B)), dim3(kBThreads), lds, stream, a);
   return check_launch("basket_cf_kernel");
 }
 
@@ -749,7 +749,7 @@ int32_t launch_basket_resident_k(const BasketArgs& a, int W, int64_t groups, int
   const BasketSyncLayout l = basket_sync_layout(A, W, a.N, groups, chunk);
   const BasketResArgs ra{a, W, static_cast<int32_t>(groups), sync, l.xsum_off, l.xcol_off, exchange_spin_limit(),
                         exchange_fault().withhold};
-  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(groups * W)), dim3(kRThreads), lds, stream, ra);
+  launch(kernel, dim3(static_cast<unsigned>(groups * W)), dim3(kRThreads), lds, stream, ra);
   if (int32_t st = check_launch("basket_resident_kernel")) return st;
   const size_t flds = 5 * static_cast<size_t>(a.N) * sizeof(double);
   if (flds > 64 * 1024 &&
@@ -758,7 +758,7 @@ int32_t launch_basket_resident_k(const BasketArgs& a, int W, int64_t groups, int
     (void)hipGetLastError();
     return fail(SMC_ERR_HIP, "basket_mean_fft_kernel: cannot raise the dynamic LDS limit");
   }
-  hipLaunchKernelGGL(basket_mean_fft_kernel, dim3(static_cast<unsigned>(a.B)), dim3(kFThreads), flds, stream,
+  launch(basket_mean_fft_kernel, dim3(static_cast<unsigned>(a.B)), dim3(kFThreads), flds, stream,
                      reinterpret_cast<const double*>(sync + l.xcol_off), W, a.N, a.M, a.targets);
   return check_launch("basket_mean_fft_kernel");
 }
@@ -849,6 +849,14 @@ int32_t smc_basket_train_targets(const double* contracts_dev, int64_t n_contract
   if (W > 0) {
     groups = basket_res_groups(W);
     if (groups <= 0) return fail(SMC_ERR_HIP, "smc_basket_train_targets: device query failed");
+    // a CU-masked stream (the data-parallel step keeps its collective and network kernels on CUs of their own):
+    // only as many groups as the stream's CUs hold, so every workgroup of a group is resident at once
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return (void)hipGetLastError(), fail(SMC_ERR_HIP, "smc_basket_train_targets: device query failed");
+    const int64_t on_stream = stream_cus(as_stream(stream), cus) / W;
+    if (on_stream <= 0) return fail(SMC_ERR_INVALID_SHAPE, "smc_basket_train_targets: fewer CUs on the stream than slices");
+    if (on_stream < groups) groups = on_stream;
     if (sync_bytes < basket_sync_layout(n_assets, W, static_cast<int>(N), groups, chunk_contracts).bytes)
       return fail(SMC_ERR_INVALID_ARGUMENT, "smc_basket_train_targets: sync_bytes < smc_basket_sync_bytes(...)");
   }

@@ -1,4 +1,4 @@
-// C-ABI housekeeping of libspectralmc_hip.so: ABI version, per-thread error text, the sync-area
+// C-ABI housekeeping of libspectralmc_hip.so: ABI version, per-thread error text, launch timing, the sync-area
 // status word of the exchanging launches, and the exchange-fault test hook (spectralmc_hip_testing.h).
 #include <atomic>
 #include <cstdarg>
@@ -24,6 +24,11 @@ void set_error(const char* fmt, ...) {
 
 ExchangeFault exchange_fault() { return ExchangeFault{g_fault_withhold.load(), g_fault_spin_limit.load()}; }
 
+LaunchTiming& launch_timing() {
+  thread_local LaunchTiming t{nullptr, nullptr};
+  return t;
+}
+
 }  // namespace smc
 
 extern "C" {
@@ -32,6 +37,11 @@ extern "C" {
 int32_t smc_abi_version(void) { return SMC_ABI_VERSION; }
 
 const char* smc_last_error_string(void) { return smc::g_last_error; }
+
+int32_t smc_time_launches(void* start_event, void* stop_event) {
+  smc::launch_timing() = smc::LaunchTiming{static_cast<hipEvent_t>(start_event), static_cast<hipEvent_t>(stop_event)};
+  return SMC_OK;
+}
 
 int32_t smc_sync_status(void* sync_dev, int32_t clear, int32_t* status_out, void* stream) {
   if (!sync_dev || !status_out) return smc::fail(SMC_ERR_INVALID_ARGUMENT, "smc_sync_status: NULL pointer");

@@ -1761,7 +1761,7 @@ int32_t launch_engine_k(const EngineArgs& a, size_t lds, hipStream_t stream) {
     unsigned grid = 0;
     if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kThreads, lds, a.B * a.slices, &grid))
       return st;
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), lds, stream, a);
+    launch(kernel, dim3(grid), dim3(kThreads), lds, stream, a);
     return check_launch("queue_kernel");
   }
   auto kernel = contract_kernel<Real, LOG_EULER, HW, ALLROWS>;
@@ -1772,7 +1772,7 @@ int32_t launch_engine_k(const EngineArgs& a, size_t lds, hipStream_t stream) {
       return fail(SMC_ERR_HIP, "contract_kernel: cannot raise the dynamic LDS limit");
     }
   }
-  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds, stream, a);
+  launch(kernel, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds, stream, a);
   return check_launch("contract_kernel");
 }
 
@@ -1817,9 +1817,9 @@ int32_t launch_split_k(const EngineArgs& a, hipStream_t stream) {
     const int64_t slots = static_cast<int64_t>(kPathsWgsPerCu) * cus;
     if (slots < a.B) grid1 = static_cast<unsigned>(slots);
   }
-  hipLaunchKernelGGL(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
+  launch(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
   if (int32_t st = check_launch("paths_kernel")) return st;
-  hipLaunchKernelGGL(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
+  launch(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
   return check_launch("cf_kernel");
 }
 
@@ -1837,9 +1837,9 @@ int32_t launch_rows_k(const EngineArgs& a, hipStream_t stream) {
   }
   unsigned grid1 = 0;
   if (int32_t st = resident_grid(reinterpret_cast<const void*>(k1), kThreads, lds1, a.B, &grid1)) return st;
-  hipLaunchKernelGGL(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
+  launch(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
   if (int32_t st = check_launch("rows_kernel")) return st;
-  hipLaunchKernelGGL(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
+  launch(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
   return check_launch("cf_kernel");
 }
 
@@ -1857,9 +1857,9 @@ int32_t launch_rows_ref_k(const EngineArgs& a, hipStream_t stream) {
   }
   unsigned grid1 = 0;
   if (int32_t st = resident_grid(reinterpret_cast<const void*>(k1), kThreads, lds1, a.B, &grid1)) return st;
-  hipLaunchKernelGGL(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
+  launch(k1, dim3(grid1), dim3(kThreads), lds1, stream, a);
   if (int32_t st = check_launch("rows_ref_kernel")) return st;
-  hipLaunchKernelGGL(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
+  launch(k2, dim3(static_cast<unsigned>(a.B)), dim3(kThreads), lds2, stream, a);
   return check_launch("cf_kernel");
 }
 
@@ -1888,7 +1888,7 @@ int32_t launch_resident_k(const EngineArgs& a, hipStream_t stream) {
     if (groups == 0) return fail(SMC_ERR_INVALID_SHAPE, "resident_kernel: fewer resident slots than slices");
     grid = groups * W;
   }
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kResThreads), lds, stream, a);
+  launch(kernel, dim3(grid), dim3(kResThreads), lds, stream, a);
   return check_launch("resident_kernel");
 }
 
@@ -1907,7 +1907,7 @@ int32_t launch_wave_k(const EngineArgs& a, hipStream_t stream) {
   if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kWaveThreads, lds, (a.B + wpg - 1) / wpg, &grid,
                                  stream))
     return st;
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWaveThreads), lds, stream, a);
+  launch(kernel, dim3(grid), dim3(kWaveThreads), lds, stream, a);
   return check_launch("wave_kernel");
 }
 
@@ -1928,7 +1928,7 @@ int32_t launch_packed_k(const EngineArgs& a, hipStream_t stream) {
   if (int32_t st = resident_grid(reinterpret_cast<const void*>(kernel), kResThreads, lds, (a.B + K - 1) / K, &grid,
                                  stream))
     return st;
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kResThreads), lds, stream, a);
+  launch(kernel, dim3(grid), dim3(kResThreads), lds, stream, a);
   return check_launch("packed_kernel");
 }
 
@@ -2125,10 +2125,10 @@ int32_t smc_gbm_normalize(const double* contracts_dev, int64_t n_contracts, int3
   if (rows == 0) return SMC_OK;
   const unsigned blocks = static_cast<unsigned>(rows < 65536 ? rows : 65536);
   if (dtype == SMC_DTYPE_F32)
-    hipLaunchKernelGGL(normalize_kernel<float>, dim3(blocks), dim3(256), 0, as_stream(stream), contracts_dev,
+    launch(normalize_kernel<float>, dim3(blocks), dim3(256), 0, as_stream(stream), contracts_dev,
                        n_contracts, timesteps, n_paths, static_cast<float*>(paths_dev), rowsum_dev);
   else
-    hipLaunchKernelGGL(normalize_kernel<double>, dim3(blocks), dim3(256), 0, as_stream(stream), contracts_dev,
+    launch(normalize_kernel<double>, dim3(blocks), dim3(256), 0, as_stream(stream), contracts_dev,
                        n_contracts, timesteps, n_paths, static_cast<double*>(paths_dev), rowsum_dev);
   return check_launch("normalize_kernel");
 }
@@ -2294,7 +2294,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
                                  cursor_dev + 1, index_offset, scheme, normalization, dtype, store_mode, paths_dev,
                                  path_pitch, chunk_contracts, nullptr, targets_dev, nullptr, 0, stream))
     return st;
-  hipLaunchKernelGGL(advance_cursor_kernel, dim3(1), dim3(64), 0, s, cursor_dev, advance);
+  launch(advance_cursor_kernel, dim3(1), dim3(64), 0, s, cursor_dev, advance);
   return check_launch("advance_cursor_kernel");
 }
 
@@ -2398,13 +2398,13 @@ int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t col
   const bool hw = (dtype & SMC_MATH_HW) != 0;
   dtype &= 0xff;
   if (dtype == SMC_DTYPE_F32 && !hw)
-    hipLaunchKernelGGL((normals_kernel<float, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
+    launch((normals_kernel<float, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
                        static_cast<uint64_t>(ordinal), rows, cols, static_cast<float*>(out_dev));
   else if (dtype == SMC_DTYPE_F32)
-    hipLaunchKernelGGL((normals_kernel<float, true>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
+    launch((normals_kernel<float, true>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
                        static_cast<uint64_t>(ordinal), rows, cols, static_cast<float*>(out_dev));
   else if (dtype == SMC_DTYPE_F64)
-    hipLaunchKernelGGL((normals_kernel<double, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
+    launch((normals_kernel<double, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
                        static_cast<uint64_t>(ordinal), rows, cols, static_cast<double*>(out_dev));
   else
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_normals: bad dtype");

@@ -1,6 +1,7 @@
 // Internal helpers shared by the translation units of libspectralmc_hip.so.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -30,6 +31,26 @@ inline int32_t check_launch(const char* kernel) {
 }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Kernel timing (smc_time_launches): while armed, the engine's launches go through hipExtLaunchKernel with
+// these events: the first records `start` at its own start, every one records `stop` at its own end (after
+// the call: the last one's).  Those are the kernels' execution timestamps, as a kernel trace takes them,
+// without the dispatch gaps a pair of stream events around back-to-back launches also holds.
+struct LaunchTiming {
+  hipEvent_t start;
+  hipEvent_t stop;
+};
+LaunchTiming& launch_timing();  // thread-local (capi.hip)
+template <typename F, typename... Args>
+inline void launch(F kernel, const dim3& grid, const dim3& block, uint32_t lds, hipStream_t stream, Args... args) {
+  LaunchTiming& t = launch_timing();
+  if (t.start || t.stop) {
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, t.start, t.stop, 0u, args...);
+    t.start = nullptr;
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, lds, stream, args...);
+  }
+}
 
 // CUs a (CU-masked) stream may use, out of `cus` (hipExtStreamCreateWithCUMask streams: the popcount of the
 // mask; other streams: all).  Persistent launches size their grids to it, so every workgroup is resident.

@@ -491,9 +491,12 @@ class GbmCVNNPricer:
     overlap_rows: bool = True
     #: launches whose workgroups wait for each other (the sliced resident kernel, C3; the resident
     #: basket kernel, C5) need every workgroup of a group co-resident.  A collective that spins on a
-    #: few CUs while it waits for a slow peer (RCCL in data-parallel runs) can hold those CUs past the
-    #: exchange's poll budget, so such a launch is enqueued only after the previous step's network part
-    #: (and its all-reduce) has completed.  None: in data-parallel runs; True / False: always / never
+    #: few CUs while it waits for a slow peer (RCCL in data-parallel runs) could hold CUs past the
+    #: exchange's poll budget; since round 6 a data-parallel session keeps the network part and the
+    #: all-reduce (issued on the network stream: dp.RcclComm) on CU-masked CUs of their own and sizes the
+    #: exchanging launch to the other CUs, so the launch runs beside the collective as it does on one GPU.
+    #: True: enqueue an exchanging launch only after the previous step's network part (and all-reduce) has
+    #: completed (round 4-5's data-parallel default); None / False: beside it
     exchange_after_network: bool | None = None
     #: network forward/backward/Adam on the fused HIP kernels (csrc/cvnn.hip) when the CVNN is a
     #: ComplexLinear + modReLU/zReLU chain; False (or other architectures): torch-ROCm modules
@@ -896,7 +899,11 @@ class TrainingSession:
                 # (a torch-module network keeps the whole chip: network_cus_small was measured with the fused
                 # network only, profiles/r04/e2e_network_cus.txt)
                 net_cus = pricer.network_cus_small
-            if (net_cus > 0 and getattr(eng, "kernel_name", "") in WHOLE_CONTRACT_KERNELS
+            # data-parallel runs of the exchanging launches (C3 sliced, C5 basket) take the masks too: the step's
+            # all-reduce runs on the network stream (dp.RcclComm), so RCCL's kernels stay on the network's CUs and
+            # cannot keep a partner workgroup of the exchanging launch off a CU while they wait for a slow peer
+            exchanging_dp = ctx is not None and getattr(eng, "exchanges", False) and fused is not None
+            if (net_cus > 0 and (getattr(eng, "kernel_name", "") in WHOLE_CONTRACT_KERNELS or exchanging_dp)
                     and cus >= 2 * net_cus):
                 # the network on its own CUs beside the path kernels (CU-masked HIP streams); the path
                 # kernel sizes its persistent grid to its stream's CUs (gbm.hip resident_grid).  Only for
@@ -934,10 +941,9 @@ class TrainingSession:
         #: beforehand, so a timed loop pays no event creation)
         self.mc_event_pool: list[tuple[torch.cuda.Event, torch.cuda.Event]] = []
         self._closed = False
-        # exchanging path launches wait for the previous step's network part (pricer.exchange_after_network)
-        order = pricer.exchange_after_network
-        self._mc_after_nn = bool(getattr(self.engine, "exchanges", False) and
-                                 (order if order is not None else ctx is not None))
+        # exchanging path launches wait for the previous step's network part only on request
+        # (pricer.exchange_after_network; data-parallel runs keep the collective on masked CUs instead)
+        self._mc_after_nn = bool(getattr(self.engine, "exchanges", False) and pricer.exchange_after_network)
         # a session that is never closed still destroys its masked streams (after a device sync: the
         # streams may hold queued work when the session is collected)
         self._finalizer = weakref.finalize(self, _finalize_streams, self._hip_streams, dev)

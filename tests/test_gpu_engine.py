@@ -827,3 +827,46 @@ def test_exchange_timeout_sets_status_not_silent_nan(oracle, golden) -> None:
     c, t = step(cur)
     check_sync_status(sync)
     assert_rows_equal(t.cpu().numpy(), kt)
+
+
+def test_time_launches_spans_the_call_kernels(golden) -> None:
+    """smc_time_launches: the armed events take the first kernel's start and the last kernel's end of the
+    calls that follow (hipExtLaunchKernel), so they span less than stream events around the same call and
+    more than zero; disarmed, later calls leave them alone; the targets are unchanged."""
+    L = _L()
+    B, T, N, M = 64, 16, 128, 4  # packed_kernel: one launch per call
+    P = N * M
+    pitch = int(L.smc_path_pitch(P, 0))
+    eng = SobolEngine(6, 7, 0)
+    tables = torch.from_numpy(eng.tables().view(np.int32)).to(DEV)
+    lo = torch.from_numpy(golden["bounds_lower"]).to(DEV)
+    hi = torch.from_numpy(golden["bounds_upper"]).to(DEV)
+    paths = poisoned((B, T, pitch), torch.float32, DEV)
+    nsync = int(L.smc_train_step_sync_bytes(T, N, M, 0, pitch))
+    sync = torch.zeros(nsync, dtype=torch.uint8, device=DEV)
+    outs = []
+    for timed in (False, True):
+        cur = torch.tensor([0, 0], dtype=torch.int64, device=DEV)
+        c = poisoned((B, 6), torch.float64, DEV)
+        t = poisoned((B, N), torch.complex64, DEV)
+        s0, s1, k0, k1 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+        k0.record()
+        k1.record()
+        torch.cuda.synchronize()
+        s0.record()
+        if timed:
+            _lib.check(L.smc_time_launches(k0.cuda_event, k1.cuda_event))
+        try:
+            _lib.check(L.smc_train_step(_lib.ptr(tables), 6, _lib.ptr(lo), _lib.ptr(hi), _lib.ptr(cur), 0, B,
+                                        _lib.ptr(c), None, B, T, N, M, 7, _lib.SCHEME_LOG_EULER, _lib.NORM_NORMALIZE,
+                                        _lib.DTYPE_F32, _lib.STORE_ALL, _lib.ptr(paths), pitch, B, _lib.ptr(t),
+                                        _lib.ptr(sync), nsync, None))
+        finally:
+            _lib.check(L.smc_time_launches(None, None))
+        s1.record()
+        torch.cuda.synchronize()
+        outs.append(t.cpu().numpy())
+        if timed:
+            kernel, around = k0.elapsed_time(k1), s0.elapsed_time(s1)
+            assert 0.0 < kernel <= around, (kernel, around)
+    assert_rows_equal(outs[1], outs[0], "timed launch")

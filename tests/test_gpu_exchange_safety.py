@@ -5,13 +5,15 @@ W = 32) need every workgroup of a group co-resident: partners poll a bounded tim
 up with NaN targets and SMC_ERR_EXCHANGE_TIMEOUT.  In a data-parallel run the step's RCCL all-reduce is
 a kernel that can spin on a few CUs while it waits for a slow peer (e.g. rank 0 committing a
 checkpoint, reference gbm_trainer.py:1296-1302: training must not die on a slow commit); a resident
-workgroup needs a whole CU, so a launch dispatched beside it may not fit.  The session therefore
-enqueues an exchanging launch only after the previous step's network part, all-reduce included, has
-completed (GbmCVNNPricer.exchange_after_network).
+workgroup needs a whole CU, so a launch dispatched beside it may not fit.  Since round 6 a data-parallel
+session keeps the network part and the all-reduce (issued on the network stream, dp.RcclComm) on CU-masked
+CUs of their own and sizes the exchanging launch to the others, so the launch runs beside the collective
+(DESIGN.md section 5); GbmCVNNPricer.exchange_after_network = True still orders it after the previous step's
+network part, all-reduce included (round 4-5's data-parallel default).
 
 Here the all-reduce is replaced by a kernel that spins ~2 s on the network stream (a stand-in for a
 stalled peer), and training at the C3 and C5 per-contract shapes must finish bit-identical to the
-run without it, with the sync area's status word clear.
+run without it, with the sync area's status word clear, in both orders.
 """
 
 from __future__ import annotations
@@ -90,8 +92,9 @@ def _pricer(shape: str):
     return p, model
 
 
+@pytest.mark.parametrize("order", [None, True], ids=["beside_on_masked_cus", "after_network"])
 @pytest.mark.parametrize("shape,batch", [("c3", 64), ("c5", 16)])
-def test_exchanging_launch_waits_for_a_spinning_collective(monkeypatch, shape: str, batch: int) -> None:
+def test_exchanging_launch_beside_a_spinning_collective(monkeypatch, shape: str, batch: int, order) -> None:
     steps = 3
     cycles = _spin_cycles(2.0)
 
@@ -99,8 +102,10 @@ def test_exchanging_launch_waits_for_a_spinning_collective(monkeypatch, shape: s
         ctx = SpinningCollective(spin)
         monkeypatch.setattr(dp_mod, "current", lambda: ctx)
         p, model = _pricer(shape)
+        p.exchange_after_network = order
         sess = expect_success(p.open_session(make_training_config(num_batches=steps, batch_size=batch)))
-        assert sess.engine.exchanges and sess._mc_after_nn
+        assert sess.engine.exchanges and sess._mc_after_nn == bool(order)
+        assert sess.network_cus_used > 0  # the collective's stream and the exchanging launch's: disjoint CUs
         t0 = time.perf_counter()
         for i in range(steps):
             expect_success(sess.step(prefetch_next=i + 1 < steps))
