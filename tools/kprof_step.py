@@ -113,11 +113,18 @@ def main() -> None:
         L.smc_trace_copy.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         assert L.smc_trace_copy(buf.ctypes.data, 1) == 0
         torch.cuda.synchronize()
-        step()
+        # one launch alone, or (lanes > 1) 4 consecutive launches in flight, traced in slots by launch (ord / B mod 4)
+        for s_ in streams[1:]:
+            s_.wait_stream(torch.cuda.current_stream())
+        for _ in range(1 if lanes == 1 else 4):
+            step()
         torch.cuda.synchronize()
         assert L.smc_trace_copy(buf.ctypes.data, 0) == 0
         np.save(a.trace, buf)
-        summarize(buf)
+        for k in range(4):
+            if buf[k * 1024:(k + 1) * 1024, 39].any():
+                print(f"-- trace slot {k}")
+                summarize(buf[k * 1024:(k + 1) * 1024])
     print(f"{a.config} {'raw' if raw else 'normalize'} pitch={pitch} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
           f"({launches} launch(es) of {chunk}), checksum {float(t.abs().double().mean()):.6g}")
 
@@ -142,7 +149,7 @@ def summarize(buf: np.ndarray) -> None:
               f"{per.mean():.1f} us per contract, contracts {rounds[m].min()}..{rounds[m].max()}")
     first = (t[:, 2] - t[:, 0]) * us
     print(f"  first contract {first.mean():.1f} us (min {first.min():.1f} max {first.max():.1f})")
-    last_start = np.array([(t[i, 2 + r - 2] if r >= 2 else t[i, 0]) for i, r in enumerate(rounds)], dtype=np.int64)
+    last_start = np.array([(t[i, 2 + min(r, 36) - 2] if r >= 2 else t[i, 0]) for i, r in enumerate(rounds)], dtype=np.int64)
     print(f"  last contract starts {((last_start - t0) * us).min():.1f}..{((last_start - t0) * us).max():.1f} us")
 
 
