@@ -640,7 +640,7 @@ def main() -> None:
                      # bytes the kernel actually moved (PMC) over its live time, against the same peak
                      "frac_moved": (traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                      "kernel_ms": kernel_ms, "kernel_ms_isolated": kernel_ms, "kernel_timing": kernel_timing,
-                     "kernel_ms_events": kernel_ms_events,
+                     "kernel_ms_events": kernel_ms_events, "kernel_iters": args.kernel_iters,
                      "live_launches": len(live),
                      # one MC lane: the launch inside the timed region (HIP events on the MC stream), next to the
                      # network kernels of the previous step

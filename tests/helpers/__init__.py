@@ -161,7 +161,9 @@ def assert_rows_equal(got, want, err_msg: str = "", chunk: int | None = None) ->
     local = bad % chunk if chunk else bad
     xcd = np.bincount(local % 8, minlength=8)
     cnt = (~same[bad]).sum(axis=1)
+    unwritten = int(np.isnan(g[bad]).all(axis=1).sum()) if np.issubdtype(g.dtype, np.inexact) else 0
     raise AssertionError(
-        f"{err_msg}: {bad.size} of {g.shape[0]} rows differ ({int(cnt.sum())} values); rows {bad[:24].tolist()}"
+        f"{err_msg}: {bad.size} of {g.shape[0]} rows differ ({int(cnt.sum())} values, {unwritten} rows all NaN:"
+        f" never written); rows {bad[:24].tolist()}"
         f"{' ...' if bad.size > 24 else ''}; row-in-launch mod 8 histogram {xcd.tolist()}"
         + (f" (chunk {chunk})" if chunk else "") + f"; first row {int(bad[0])}: got {g[bad[0]][:4]} want {w[bad[0]][:4]}")
