@@ -81,9 +81,10 @@ def parse(argv: list[str] | None = None) -> argparse.Namespace:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
-    ap.add_argument("--math", default="hw", choices=["portable", "hw", "reference"],
+    ap.add_argument("--math", default="hw", choices=["portable", "hw", "reference", "reference_hw"],
                     help="path math: hw (hardware f32 transcendentals), portable (CPU-reproducible f32), reference "
-                         "(the reference kernel's typing: f64 state and step, f32 normals and stores; float32 configs)")
+                         "(the reference kernel's typing: f64 state and step, f32 normals and stores; float32 configs), "
+                         "reference_hw (that step on the hardware-transcendental normals)")
     ap.add_argument("--network", default=None, choices=["auto", "valu", "mfma", "bf16"],
                     help="network kernels (default: bf16 for c3, auto otherwise)")
     ap.add_argument("--overlap-rows", default="on", choices=["on", "off"],

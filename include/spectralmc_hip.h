@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SMC_ABI_VERSION 14  /* 14: smc_time_launches */
+#define SMC_ABI_VERSION 15  /* 14: smc_time_launches; 15: SMC_MATH_REF | SMC_MATH_HW */
 
 /* ---- status codes ------------------------------------------------------- */
 #define SMC_OK                      0
@@ -61,14 +61,16 @@ extern "C" {
                                       f32 hardware transcendentals (v_exp/v_log/v_sin/v_cos/v_sqrt)
                                       instead of the portable, CPU-reproducible kernels */
 #define SMC_MATH_REF         0x400  /* flag, OR into smc_train_targets' / smc_train_step's `scheme` (f32
-                                      only, not with SMC_MATH_HW): the reference kernel's own typing
-                                      (gbm.py:224-257 under Numba: f64 state and step of the f32 normals,
-                                      f32 stores): portable normals, the f64 engine's step, rounded f32
-                                      paths (rows_ref_kernel + cf_kernel).  The f64 step's exp is within
-                                      2 ulp of libm's, so a stored f32 value equals the reference
-                                      arithmetic's except where the two exps round to different floats
-                                      (C2 shape: <= 1e-6 of the values, 1 ulp; tests/test_oracle.py); in
-                                      the kernel queries' dtype: that kernel's name */
+                                      only): the reference kernel's own typing (gbm.py:224-257 under
+                                      Numba: f64 state and step of the f32 normals, f32 stores): portable
+                                      normals, the f64 engine's step, rounded f32 paths (rows_ref_kernel +
+                                      cf_kernel).  The f64 step's exp is within 2 ulp of libm's, so a
+                                      stored f32 value equals the reference arithmetic's except where the
+                                      two exps round to different floats (C2 shape: <= 1e-6 of the values,
+                                      1 ulp; tests/test_oracle.py).  With SMC_MATH_HW (ABI 15): the same
+                                      step on the hardware-transcendental f32 normals (~1 ulp from the
+                                      portable ones, so not bit-reproducible on a CPU).  In the kernel
+                                      queries' dtype: that kernel's name */
 #define SMC_TRAIN_DYNAMIC    0x200  /* flag, OR into smc_train_step's `scheme`: the whole-contract resident
                                       launch hands out every contract from its contract queue (default:
                                       the first three quarters of the rounds statically), for launches that

@@ -40,7 +40,7 @@ TRAIN_DYNAMIC = 0x200
 MATH_REF = 0x400  # the reference kernel's typing: f64 state and step, f32 normals and stores
 STORE_ALL = 2
 SOBOL_BITS = 30
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _c_i32, _c_i64, _c_u64, _c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
 

@@ -861,7 +861,10 @@ void rows_kernel(EngineArgs a) {
 // pipeline's terminal sum and CF phase (cf_kernel<float>).  Any P: a lane past P draws and stores
 // nothing (stream positions never depend on P), a lane straddling P stores its valid paths one by one.
 // Terminal-sum order of rows_kernel (oracle kernel mode with step64, wg = 512).
-template <bool LOG_EULER, bool STORE_ALL>
+// HWN (SMC_MATH_REF | SMC_MATH_HW): the same draws through the hardware-transcendental Box-Muller
+// (normal_pair<true>, rescaled to N(0, 1) in f32), the f64 step unchanged: the portable normals' software
+// log / sincos were ~40 % of the launch (C2: 4.56 against 6.57 ms, profiles/r06/ab_refmath_hw_normals.txt)
+template <bool LOG_EULER, bool STORE_ALL, bool HWN>
 __device__ __forceinline__ void lane_rows_ref(const EngineArgs& a, const Stepper<double, LOG_EULER, false>& step,
                                               double x0, uint64_t ordinal, int64_t chunk, float* contract_base,
                                               int T, int64_t pitch, double& acc) {
@@ -891,10 +894,17 @@ __device__ __forceinline__ void lane_rows_ref(const EngineArgs& a, const Stepper
       for (int j = 0; j < nvalid; ++j) r[j] = w[j];
     }
   };
+  constexpr float kz = static_cast<float>(PathStream::kNormalScale<HWN>);  // 1 for the portable normals
 #pragma unroll 1
   for (int t = 0; t + 1 < T; t += 2) {
 #pragma unroll
-    for (int j = 0; j < kPathsPerLane; ++j) s.template normal_pair<false>(zl[j], zh[j]);
+    for (int j = 0; j < kPathsPerLane; ++j) {
+      s.template normal_pair<HWN>(zl[j], zh[j]);
+      if constexpr (HWN) {
+        zl[j] *= kz;
+        zh[j] *= kz;
+      }
+    }
     advance(zl);
     if constexpr (STORE_ALL) store();
     row += rstride;
@@ -903,7 +913,11 @@ __device__ __forceinline__ void lane_rows_ref(const EngineArgs& a, const Stepper
     row += rstride;
   }
   if (T & 1) {  // the last step of an odd T: two Box-Muller pairs for the 4 paths
-    s.template normal_tail<false>(zl);
+    s.template normal_tail<HWN>(zl);
+    if constexpr (HWN) {
+#pragma unroll
+      for (int j = 0; j < kPathsPerLane; ++j) zl[j] *= kz;
+    }
     advance(zl);
     if constexpr (STORE_ALL) store();
   }
@@ -918,7 +932,7 @@ __device__ __forceinline__ void lane_rows_ref(const EngineArgs& a, const Stepper
 // 6 waves per SIMD (three 8-wave workgroups per CU with the 51 KB table image each): C2 6.59 ms against 6.65
 // at 4 and 6.69 at 8 waves (profiles/r05/ab_ref_waves.txt)
 constexpr int kRowsRefWaves = 6;
-template <bool LOG_EULER, bool STORE_ALL>
+template <bool LOG_EULER, bool STORE_ALL, bool HWN>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kRowsRefWaves)))
 void rows_ref_kernel(EngineArgs a) {
   extern __shared__ double lds[];
@@ -933,7 +947,7 @@ void rows_ref_kernel(EngineArgs a) {
     float* base = static_cast<float*>(a.paths) + (STORE_ALL ? b * T * pitch : b * pitch);
     double acc = 0.0;
     for (int64_t chunk = 0; chunk < a.P; chunk += kChunk)
-      lane_rows_ref<LOG_EULER, STORE_ALL>(a, step, c.X0, static_cast<uint64_t>(ord0 + b), chunk, base, T, pitch, acc);
+      lane_rows_ref<LOG_EULER, STORE_ALL, HWN>(a, step, c.X0, static_cast<uint64_t>(ord0 + b), chunk, base, T, pitch, acc);
     const double w = wave_sum(acc);
     double* ws = lds + parity * kWaves;
     if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = w;
@@ -1843,10 +1857,10 @@ int32_t launch_rows_k(const EngineArgs& a, hipStream_t stream) {
   return check_launch("cf_kernel");
 }
 
-template <bool LOG_EULER, bool STORE_ALL>
+template <bool LOG_EULER, bool STORE_ALL, bool HWN>
 int32_t launch_rows_ref_k(const EngineArgs& a, hipStream_t stream) {
   const size_t lds1 = 2 * kWaves * sizeof(double), lds2 = lds_bytes(a.T, a.N, true);
-  auto k1 = rows_ref_kernel<LOG_EULER, STORE_ALL>;
+  auto k1 = rows_ref_kernel<LOG_EULER, STORE_ALL, HWN>;
   auto k2 = cf_kernel<float>;
   if (lds2 > kMaxLds) return fail(SMC_ERR_INVALID_SHAPE, "engine: network_size exceeds the LDS budget");
   if (lds2 > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(k2),
@@ -1943,8 +1957,14 @@ int32_t launch_engine(EngineArgs a, hipStream_t stream) {
                                          "a padded pitch (smc_path_pitch)");
     const bool log_euler = (a.scheme & 0xff) == SMC_SCHEME_LOG_EULER;
     const bool sa = a.store == SMC_STORE_ALL;
-    if (log_euler) return sa ? launch_rows_ref_k<true, true>(a, stream) : launch_rows_ref_k<true, false>(a, stream);
-    return sa ? launch_rows_ref_k<false, true>(a, stream) : launch_rows_ref_k<false, false>(a, stream);
+    if ((a.scheme & SMC_MATH_HW) != 0) {  // hardware-transcendental normals
+      if (log_euler)
+        return sa ? launch_rows_ref_k<true, true, true>(a, stream) : launch_rows_ref_k<true, false, true>(a, stream);
+      return sa ? launch_rows_ref_k<false, true, true>(a, stream) : launch_rows_ref_k<false, false, true>(a, stream);
+    }
+    if (log_euler)
+      return sa ? launch_rows_ref_k<true, true, false>(a, stream) : launch_rows_ref_k<true, false, false>(a, stream);
+    return sa ? launch_rows_ref_k<false, true, false>(a, stream) : launch_rows_ref_k<false, false, false>(a, stream);
   }
   if constexpr (sizeof(Real) == 4) {
     if (wave_ok(a, true)) {  // RAW, T <= 2: one wave per contract
@@ -2080,10 +2100,9 @@ int32_t dispatch_engine(const EngineArgs& a, int32_t dtype, hipStream_t stream) 
   return fail(SMC_ERR_INVALID_ARGUMENT, "engine: dtype must be SMC_DTYPE_F32 or SMC_DTYPE_F64");
 }
 
-bool valid_scheme(int32_t scheme) {
+bool valid_scheme(int32_t scheme) {  // SMC_MATH_REF | SMC_MATH_HW: reference arithmetic on hardware normals
   const int32_t base = scheme & 0xff, flags = scheme & ~0xff;
-  return (base == SMC_SCHEME_LOG_EULER || base == SMC_SCHEME_SIMPLE_EULER) &&
-         (flags & ~(SMC_MATH_HW | SMC_MATH_REF)) == 0 && (flags & (SMC_MATH_HW | SMC_MATH_REF)) != (SMC_MATH_HW | SMC_MATH_REF);
+  return (base == SMC_SCHEME_LOG_EULER || base == SMC_SCHEME_SIMPLE_EULER) && (flags & ~(SMC_MATH_HW | SMC_MATH_REF)) == 0;
 }
 
 int32_t validate_common(const double* contracts, int64_t B, int32_t T, int64_t P, int32_t dtype) {

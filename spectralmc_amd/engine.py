@@ -79,19 +79,22 @@ class TrainingEngine:
         self.device = device
         self.sim_dtype = sp.dtype
         self._dtype_code = dtype_code(sp.dtype)
-        if math not in ("portable", "hw", "reference"):
-            raise ValueError(f"math must be 'portable', 'hw' or 'reference', got {math!r}")
-        if math == "reference" and sp.dtype != Precision.float32:
-            raise ValueError("math='reference' is the reference kernel's f32 typing (float32 simulations only)")
-        if math == "reference" and sliced:
+        if math not in ("portable", "hw", "reference", "reference_hw"):
+            raise ValueError(f"math must be 'portable', 'hw', 'reference' or 'reference_hw', got {math!r}")
+        ref = math in ("reference", "reference_hw")
+        if ref and sp.dtype != Precision.float32:
+            raise ValueError(f"math={math!r} is the reference kernel's f32 typing (float32 simulations only)")
+        if ref and sliced:
             # rows_ref_kernel runs whole contracts per workgroup: every sliced launch would fail INVALID_SHAPE
-            raise ValueError("math='reference' runs whole contracts per workgroup (rows_ref_kernel); sliced=True "
+            raise ValueError(f"math={math!r} runs whole contracts per workgroup (rows_ref_kernel); sliced=True "
                              "is not supported")
         _lib.require_device()
         self.math = math
         # "hw": f32 hardware transcendentals in the path kernel (faster, ~1 ulp, not CPU-reproducible);
-        # "reference": the reference kernel's typing (f64 state and step, f32 normals and stores: rows_ref_kernel)
-        self._scheme = scheme_code(cfg.path_scheme) | {"hw": _lib.MATH_HW, "reference": _lib.MATH_REF}.get(math, 0)
+        # "reference": the reference kernel's typing (f64 state and step, f32 normals and stores: rows_ref_kernel);
+        # "reference_hw": the same step on the hardware-transcendental f32 normals (SMC_MATH_REF | SMC_MATH_HW)
+        self._scheme = scheme_code(cfg.path_scheme) | {"hw": _lib.MATH_HW, "reference": _lib.MATH_REF,
+                                                       "reference_hw": _lib.MATH_REF | _lib.MATH_HW}.get(math, 0)
         self._norm = normalization_code(cfg.normalization)
         self.store_mode = _lib.STORE_ALL if store_paths else _lib.STORE_TERMINAL
         sim_torch = sp.dtype.to_torch()
@@ -113,7 +116,7 @@ class TrainingEngine:
         # scratch rows at a padded pitch: a power-of-two row stride aliases in HBM
         # (math="reference": rows_ref_kernel keeps the terminal sum in the row padding, so the pitch must leave
         # room after column P even where P is itself an odd multiple of 4 KiB)
-        self.pitch = int(_lib.lib().smc_path_pitch(self.P + (4 if math == "reference" else 0), self._dtype_code))
+        self.pitch = int(_lib.lib().smc_path_pitch(self.P + (4 if ref else 0), self._dtype_code))
         per_contract = (self.T * self.pitch if store_paths else self.pitch) * torch.finfo(sim_torch).bits // 8
         budget = path_buffer_bytes if path_buffer_bytes is not None else path_buffer_budget(device)
         max_chunk = max(1, min(B, budget // per_contract))
@@ -136,7 +139,7 @@ class TrainingEngine:
         self._uses_train_step = self._f32_in and self.dim == 6 and self._workspace is None
         # the path/CF kernel the step runs for this shape (bench labels, rocprof cross-check)
         query = self._dtype_code | (_lib.QUERY_RAW if self._norm == _lib.NORM_RAW else 0) | \
-            (_lib.MATH_REF if math == "reference" else 0)
+            (_lib.MATH_REF if ref else 0)
         if self._uses_train_step:
             self.kernel_name = _lib.lib().smc_train_step_kernel(self.T, self.N, self.M, query, self.pitch).decode()
         else:

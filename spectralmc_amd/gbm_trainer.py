@@ -443,7 +443,8 @@ class GbmCVNNPricer:
     #: CPU path at the stated fp32 tolerance); "portable": IEEE-only polynomial transcendentals,
     #: bit-identical to the oracle's kernel mode (CPU-reproducible paths and targets); "reference":
     #: the reference kernel's own typing (gbm.py:224-257 under Numba: f64 state and step of the f32
-    #: normals, f32 stores), float32 simulations only (rows_ref_kernel + cf_kernel)
+    #: normals, f32 stores), float32 simulations only (rows_ref_kernel + cf_kernel); "reference_hw": that step
+    #: on the hardware-transcendental f32 normals (within the "hw" tolerance of "reference", 1.4x faster)
     math_mode: str = "hw"
     #: run step s+1's Monte-Carlo part on its own stream, concurrently with step s's network part
     overlap_mc: bool = True

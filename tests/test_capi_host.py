@@ -225,6 +225,11 @@ def test_train_targets_kernel_choice() -> None:
     assert L.smc_train_targets_kernel(16, 256, 65536, ref, 0, 0) == b"unsupported"          # no room for the sum
     assert L.smc_train_step_kernel(16, 256, 256, ref, 65536) == b"unsupported"
     assert L.smc_train_targets_kernel(16, 256, 65536, ref, 66560, 1) == b"unsupported"      # sliced
+    # SMC_MATH_REF | SMC_MATH_HW (ABI 15): the same kernels on the hardware-transcendental normals
+    hwref = _lib.MATH_REF | _lib.MATH_HW
+    assert L.smc_train_targets_kernel(16, 256, 65536, hwref, 66560, 0) == b"rows_ref_kernel+cf_kernel"
+    assert L.smc_train_step_kernel(16, 256, 256, hwref, 66560) == b"rows_ref_kernel+cf_kernel"
+    assert L.smc_train_targets_kernel(16, 256, 65536, 1 | hwref, 66560, 0) == b"unsupported"  # f64
 
 
 def test_engine_rejects_reference_math_it_cannot_run() -> None:
@@ -238,15 +243,18 @@ def test_engine_rejects_reference_math_it_cannot_run() -> None:
     from spectralmc_amd.sobol_sampler import SobolSampler, build_sobol_config
     from tests.helpers import expect_success, make_black_scholes_config, make_domain_bounds, make_simulation_params
 
-    for dtype, sliced, msg in ((Precision.float32, True, "sliced"), (Precision.float64, False, "float32")):
-        sp = make_simulation_params(timesteps=16, network_size=64, batches_per_mc_run=8, threads_per_block=256,
-                                    mc_seed=7, buffer_size=4, dtype=dtype)
-        cfg = make_black_scholes_config(sim_params=sp)
-        sampler = expect_success(SobolSampler.create(BlackScholes.Inputs, make_domain_bounds(),
-                                                     config=build_sobol_config(seed=7, skip=0).unwrap()))
-        with pytest.raises(ValueError, match=msg):
-            TrainingEngine(cfg, sampler, 4, model_dtype=torch.float32, device=torch.device("cpu"), math="reference",
-                           sliced=sliced)
+    for math in ("reference", "reference_hw"):
+        for dtype, sliced, msg in ((Precision.float32, True, "sliced"), (Precision.float64, False, "float32")):
+            sp = make_simulation_params(timesteps=16, network_size=64, batches_per_mc_run=8, threads_per_block=256,
+                                        mc_seed=7, buffer_size=4, dtype=dtype)
+            cfg = make_black_scholes_config(sim_params=sp)
+            sampler = expect_success(SobolSampler.create(BlackScholes.Inputs, make_domain_bounds(),
+                                                         config=build_sobol_config(seed=7, skip=0).unwrap()))
+            with pytest.raises(ValueError, match=msg):
+                TrainingEngine(cfg, sampler, 4, model_dtype=torch.float32, device=torch.device("cpu"), math=math,
+                               sliced=sliced)
+    with pytest.raises(ValueError, match="reference_hw"):
+        TrainingEngine(cfg, sampler, 4, model_dtype=torch.float32, device=torch.device("cpu"), math="fast")
 
 
 def test_basket_entry_points_validate_before_any_device_work() -> None:

@@ -25,7 +25,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=sorted(SHAPES))
     ap.add_argument("--B", type=int, default=0, help="contracts per step (default: the config's)")
-    ap.add_argument("--math", default="hw", choices=["hw", "portable", "reference"])
+    ap.add_argument("--math", default="hw", choices=["hw", "portable", "reference", "reference_hw"])
     ap.add_argument("--store", default="all", choices=["all", "terminal"])
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--iters", type=int, default=5)
@@ -34,14 +34,22 @@ def main() -> None:
     ap.add_argument("--pitch", type=int, default=0, help="row pitch in elements (0: smc_path_pitch)")
     ap.add_argument("--lanes", type=int, default=1, help="launches alternate over this many streams, each with "
                     "its own cursor, sync area and path scratch (consecutive launches may overlap)")
+    ap.add_argument("--split", type=int, default=0, help="each call: this many concurrent launches of B / split "
+                    "contracts, each on its own CU-masked stream of 1 / split of the CUs (every XCD in each)")
+    ap.add_argument("--one-stream", action="store_true", help="--lanes buffers and sync areas, all on one stream")
     ap.add_argument("--dynamic", action="store_true", help="SMC_TRAIN_DYNAMIC: every contract from the queue")
     ap.add_argument("--trace", default="", help="trace variant library (tools/micro/trace_variant.sh): after the timed "
                     "loop run one launch alone and save its per-workgroup timestamps to this .npy file")
+    ap.add_argument("--trace-timed", default="", help="trace variant library: save the per-workgroup stamps of the "
+                    "timed launches (16 slots of 256 workgroups, one per launch) to this .npy")
     ap.add_argument("--norm", default="", choices=["", "raw", "normalize"],
                     help="targets normalisation (default: RAW for the lock-step shape, else NORMALIZE)")
     a = ap.parse_args()
     B, T, N, M = SHAPES[a.config]
     B = a.B or B
+    if a.split:  # one call = a.split concurrent launches of B / a.split contracts on complementary CU-masked streams
+        B //= a.split
+        a.lanes = a.split
     P = N * M
     L = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -75,7 +83,22 @@ def main() -> None:
     nsync = int(L.smc_train_step_sync_bytes(T, N, M, dcode, pitch))
     syncs = [torch.zeros(max(nsync, 8), dtype=torch.uint8, device=dev) for _ in range(lanes)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(lanes - 1)]
-    scheme = _lib.SCHEME_LOG_EULER | {"hw": _lib.MATH_HW, "reference": _lib.MATH_REF}.get(a.math, 0) | \
+    owned: list[int] = []
+    if a.split:
+        from spectralmc_amd.gbm_trainer import _masked_stream
+
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        per_lane = ncu // a.split
+        streams = []
+        for k in range(a.split):
+            mask = [0] * ((ncu + 31) // 32)
+            for cu in range(k * per_lane, (k + 1) * per_lane):  # logical ids interleave the XCDs (gbm_trainer._cu_masks)
+                mask[cu // 32] |= 1 << (cu % 32)
+            streams.append(_masked_stream(dev, mask, owned))
+    if a.one_stream:  # the lanes' buffers, one stream: launches serialised, rotating over the path buffers
+        streams = [torch.cuda.current_stream()] * lanes
+    scheme = _lib.SCHEME_LOG_EULER | {"hw": _lib.MATH_HW, "reference": _lib.MATH_REF,
+                                        "reference_hw": _lib.MATH_REF | _lib.MATH_HW}.get(a.math, 0) | \
         (_lib.TRAIN_DYNAMIC if a.dynamic else 0)
     n_launched = [0]
     raw = a.norm == "raw" or (a.norm == "" and a.config == "lockstep")
@@ -92,20 +115,32 @@ def main() -> None:
     for _ in range(lanes):
         step()
     torch.cuda.synchronize()
+    if a.trace_timed:  # trace the timed launches themselves (16 slots of 256 workgroups by launch)
+        import ctypes
+
+        tbuf = np.zeros((4096, 40), dtype=np.uint64)
+        L.smc_trace_copy.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        assert L.smc_trace_copy(tbuf.ctypes.data, 1) == 0
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for s_ in streams[1:]:
-        s_.wait_stream(torch.cuda.current_stream())
-    for _ in range(a.iters):
+    for s_ in streams:
+        if s_ is not torch.cuda.current_stream():
+            s_.wait_stream(torch.cuda.current_stream())
+    for _ in range(a.iters * (a.split or 1)):
         step()
-    for s_ in streams[1:]:
-        torch.cuda.current_stream().wait_stream(s_)
+    for s_ in streams:
+        if s_ is not torch.cuda.current_stream():
+            torch.cuda.current_stream().wait_stream(s_)
     e1.record()
     torch.cuda.synchronize()
     assert all(_lib.sync_status(sy) == 0 for sy in syncs)
     name = L.smc_train_step_kernel(T, N, M, dcode | (_lib.QUERY_RAW if raw else 0) |
-                                   (_lib.MATH_REF if a.math == "reference" else 0), pitch).decode()
-    ms = e0.elapsed_time(e1) / a.iters
+                                   (_lib.MATH_REF if a.math.startswith("reference") else 0), pitch).decode()
+    ms = e0.elapsed_time(e1) / a.iters  # per call (a.split launches with --split)
+    if a.trace_timed:
+        assert L.smc_trace_copy(tbuf.ctypes.data, 0) == 0
+        np.save(a.trace_timed, tbuf)
     if a.trace:
         import ctypes
 
@@ -121,10 +156,10 @@ def main() -> None:
         torch.cuda.synchronize()
         assert L.smc_trace_copy(buf.ctypes.data, 0) == 0
         np.save(a.trace, buf)
-        for k in range(4):
-            if buf[k * 1024:(k + 1) * 1024, 39].any():
+        for k in range(16):
+            if buf[k * 256:(k + 1) * 256, 39].any():
                 print(f"-- trace slot {k}")
-                summarize(buf[k * 1024:(k + 1) * 1024])
+                summarize(buf[k * 256:(k + 1) * 256])
     print(f"{a.config} {'raw' if raw else 'normalize'} pitch={pitch} B={B} T={T} N={N} M={M} {a.dtype} {a.math} {a.store} {name}: {ms:.3f} ms/step "
           f"({launches} launch(es) of {chunk}), checksum {float(t.abs().double().mean()):.6g}")
 
@@ -149,7 +184,7 @@ def summarize(buf: np.ndarray) -> None:
               f"{per.mean():.1f} us per contract, contracts {rounds[m].min()}..{rounds[m].max()}")
     first = (t[:, 2] - t[:, 0]) * us
     print(f"  first contract {first.mean():.1f} us (min {first.min():.1f} max {first.max():.1f})")
-    last_start = np.array([(t[i, 2 + min(r, 36) - 2] if r >= 2 else t[i, 0]) for i, r in enumerate(rounds)], dtype=np.int64)
+    last_start = np.array([(t[i, 2 + min(r, 34) - 2] if r >= 2 else t[i, 0]) for i, r in enumerate(rounds)], dtype=np.int64)
     print(f"  last contract starts {((last_start - t0) * us).min():.1f}..{((last_start - t0) * us).max():.1f} us")
 
 

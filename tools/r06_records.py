@@ -18,7 +18,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CONFIGS = ("c2", "c2h256", "c3", "c5", "lockstep", "e2e", "c2f64", "c2ref")
+CONFIGS = ("c2", "c2h256", "c3", "c5", "lockstep", "e2e", "c2f64", "c2ref", "c2refhw")
 
 
 def trace_rows(trace: str, names: tuple[str, ...]) -> list[tuple[str, int, int]]:
