@@ -124,6 +124,11 @@ def algorithmic_bytes_per_contract(T: int, N: int, M: int, store_all: bool, esz:
     return (T * P * esz if store_all else P * esz) + P * esz + N * 2 * esz
 
 
+def progress(msg: str) -> None:
+    """A progress line on stderr (stdout carries only the JSON line): long CPU legs stay visibly alive."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_threads() -> int:
     """Host threads for the CPU legs: the process's affinity set, capped by OMP_NUM_THREADS (the
     GPU box gives one GPU's job a 16-core share; os.cpu_count() there is the whole machine)."""
@@ -213,12 +218,19 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
     # torch.set_num_threads(len(os.sched_getaffinity(0)))): the GPU box shows the whole host there, while one
     # GPU's job gets a 16-core share (OMP_NUM_THREADS), which the leg above uses
     aff = len(os.sched_getaffinity(0))
+    progress(f"cpu_baseline: {threads}-thread leg done ({per_c * done + t_nn * reps:.1f} s)")
     if aff != threads and not n_assets:
-        torch.set_num_threads(aff)
+        # contract-level parallelism over the affinity set: one worker thread per core, each contract's torch ops
+        # single-threaded (nested intra-op pools of `aff` threads in each of `aff` workers oversubscribe a shared
+        # host by aff^2); the CVNN/Adam step on up to 64 intra-op threads
+        workers = min(aff, 256)
+        nn_threads = min(aff, 64)
+        torch.set_num_threads(1)
         try:
             per_a, done_a, _ = sample(lambda c, o: cpu_path_targets(c, T, N, M, 7, o, dtype=dtype, normals="numpy",
-                                                                    normalize=normalize, workers=min(aff, 64)),
-                                      budget_s * 0.4, 2 * min(aff, 64))
+                                                                    normalize=normalize, workers=workers),
+                                      budget_s * 0.4, 2 * workers)
+            torch.set_num_threads(nn_threads)
             oracle.torch_step(model, x, torch.zeros_like(x), tgt, adam)  # warm at this thread count
             t0 = time.perf_counter()
             for _ in range(reps):
@@ -227,10 +239,12 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
         finally:
             torch.set_num_threads(threads)
         line["affinity_leg"] = {
-            "value": B * N * M / (per_a * B + t_nn_a), "unit": "contracts*paths/s", "cores": aff, "kind": "port",
-            "sample": (f"{path}, {aff} threads (torch.set_num_threads(len(os.sched_getaffinity(0)))), on "
-                       f"{done_a}/{B} contracts ({per_a * done_a:.1f}s), extrapolated x{B / done_a:.1f}, + full B={B} "
-                       f"CVNN/Adam step ({t_nn_a * 1e3:.1f} ms)")}
+            "value": B * N * M / (per_a * B + t_nn_a), "unit": "contracts*paths/s", "cores": workers, "kind": "port",
+            "sample": (f"{path}, {workers} worker threads over the process's {aff}-core affinity set (BASELINE.md 2.2: "
+                       f"len(os.sched_getaffinity(0))), one single-threaded contract each, on {done_a}/{B} contracts "
+                       f"({per_a * done_a:.1f}s), extrapolated x{B / done_a:.1f}, + full B={B} CVNN/Adam step on "
+                       f"{nn_threads} threads ({t_nn_a * 1e3:.1f} ms)")}
+        progress(f"cpu_baseline: affinity leg done ({per_a * done_a + t_nn_a * reps:.1f} s)")
     else:
         line["affinity_leg"] = {"value": line["value"], "unit": "contracts*paths/s", "cores": aff, "kind": "port",
                                 "sample": "the affinity set is the leg above's thread count" if aff == threads else
@@ -243,6 +257,7 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
         line["c_openmp_leg"] = {"value": B * N * M / (per_c2 * B + t_nn), "unit": "contracts*paths/s",
                                 "cores": threads, "kind": "port",
                                 "sample": f"oracle/gbm_oracle.c (OpenMP) on {done2}/{B} contracts, extrapolated"}
+        progress("cpu_baseline: C/OpenMP leg done")
         # C1, the reference's own CPU-runnable config (BASELINE configs[0]): 10 whole steps
         c1B, c1N, c1M = 64, 256, 4
         m1 = make_test_cvnn(n_inputs=6, n_outputs=c1N, seed=123, dtype=torch.float32, device="cpu", hidden_layers=1)
@@ -257,6 +272,7 @@ def cpu_baseline(B: int, T: int, N: int, M: int, widths: list[int], budget_s: fl
                       "ms_per_step": t1 * 1e3, "steps": 10, "warmup": 1,
                       "workload": "C1: 64 contracts x 1024 paths (N=256 x M=4), T=16, 2-layer CVNN 6->32->256, "
                                   "torch-cpu + numpy.fft, whole steps"}
+        progress(f"cpu_baseline: C1 done ({t1 * 11:.1f} s)")
     return line
 
 
