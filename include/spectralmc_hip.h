@@ -85,11 +85,12 @@ typedef struct smc_sobol smc_sobol;
 int32_t     smc_abi_version(void);
 const char* smc_last_error_string(void);
 /* Kernel timing for measurement (ABI 14): arms two caller-created hipEvent_t for the engine calls that
- * follow on this thread (smc_train_step, smc_train_targets, smc_basket_train_targets, smc_sobol_draw, ...):
- * their first kernel records start_event at its own start, every kernel records stop_event at its own
- * end (hipExtLaunchKernel), so after the call the pair spans the call's kernels as a kernel trace times
- * them, without the dispatch gaps of stream events around back-to-back launches.  NULL, NULL disarms.
- * Stream-ordered like the launches; captured launches record nothing. */
+ * follow on this thread (smc_train_step, smc_train_targets, smc_basket_train_targets): their first path /
+ * CF kernel records start_event at its own start, every path / CF kernel records stop_event at its own
+ * end (hipExtLaunchKernel), so after the call the pair spans the call's path and CF kernels as a kernel
+ * trace times them, without the dispatch gaps of stream events around back-to-back launches.  The
+ * auxiliary kernels (Sobol draw, cursor update, normalisation, normals) are not timed.  NULL, NULL
+ * disarms.  Stream-ordered like the launches; captured launches record nothing. */
 int32_t     smc_time_launches(void* start_event, void* stop_event);
 
 /* ---- sync-area status (smc_train_step, smc_basket_train_targets) ---------- */

@@ -2144,10 +2144,10 @@ int32_t smc_gbm_normalize(const double* contracts_dev, int64_t n_contracts, int3
   if (rows == 0) return SMC_OK;
   const unsigned blocks = static_cast<unsigned>(rows < 65536 ? rows : 65536);
   if (dtype == SMC_DTYPE_F32)
-    launch(normalize_kernel<float>, dim3(blocks), dim3(256), 0, as_stream(stream), contracts_dev,
+    launch_aux(normalize_kernel<float>, dim3(blocks), dim3(256), 0, as_stream(stream), contracts_dev,
                        n_contracts, timesteps, n_paths, static_cast<float*>(paths_dev), rowsum_dev);
   else
-    launch(normalize_kernel<double>, dim3(blocks), dim3(256), 0, as_stream(stream), contracts_dev,
+    launch_aux(normalize_kernel<double>, dim3(blocks), dim3(256), 0, as_stream(stream), contracts_dev,
                        n_contracts, timesteps, n_paths, static_cast<double*>(paths_dev), rowsum_dev);
   return check_launch("normalize_kernel");
 }
@@ -2313,7 +2313,7 @@ int32_t smc_train_step(const uint32_t* sobol_tables_dev, int32_t dim, const doub
                                  cursor_dev + 1, index_offset, scheme, normalization, dtype, store_mode, paths_dev,
                                  path_pitch, chunk_contracts, nullptr, targets_dev, nullptr, 0, stream))
     return st;
-  launch(advance_cursor_kernel, dim3(1), dim3(64), 0, s, cursor_dev, advance);
+  launch_aux(advance_cursor_kernel, dim3(1), dim3(64), 0, s, cursor_dev, advance);
   return check_launch("advance_cursor_kernel");
 }
 
@@ -2417,13 +2417,13 @@ int32_t smc_normals(uint64_t mc_seed, int64_t ordinal, int32_t rows, int64_t col
   const bool hw = (dtype & SMC_MATH_HW) != 0;
   dtype &= 0xff;
   if (dtype == SMC_DTYPE_F32 && !hw)
-    launch((normals_kernel<float, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
+    launch_aux((normals_kernel<float, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
                        static_cast<uint64_t>(ordinal), rows, cols, static_cast<float*>(out_dev));
   else if (dtype == SMC_DTYPE_F32)
-    launch((normals_kernel<float, true>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
+    launch_aux((normals_kernel<float, true>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
                        static_cast<uint64_t>(ordinal), rows, cols, static_cast<float*>(out_dev));
   else if (dtype == SMC_DTYPE_F64)
-    launch((normals_kernel<double, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
+    launch_aux((normals_kernel<double, false>), dim3(blocks), dim3(256), 0, as_stream(stream), mc_seed,
                        static_cast<uint64_t>(ordinal), rows, cols, static_cast<double*>(out_dev));
   else
     return fail(SMC_ERR_INVALID_ARGUMENT, "smc_normals: bad dtype");

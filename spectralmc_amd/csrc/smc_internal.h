@@ -51,6 +51,12 @@ inline void launch(F kernel, const dim3& grid, const dim3& block, uint32_t lds, 
     hipLaunchKernelGGL(kernel, grid, block, lds, stream, args...);
   }
 }
+// An auxiliary kernel of an engine call (Sobol draw, cursor update, normalisation, normals): never timed by
+// smc_time_launches, so the armed pair spans the path / CF kernels the roofline is quoted on.
+template <typename F, typename... Args>
+inline void launch_aux(F kernel, const dim3& grid, const dim3& block, uint32_t lds, hipStream_t stream, Args... args) {
+  hipLaunchKernelGGL(kernel, grid, block, lds, stream, args...);
+}
 
 // CUs a (CU-masked) stream may use, out of `cus` (hipExtStreamCreateWithCUMask streams: the popcount of the
 // mask; other streams: all).  Persistent launches size their grids to it, so every workgroup is resident.

@@ -267,7 +267,7 @@ int32_t smc_sobol_draw(const uint32_t* tables_dev, int32_t dim, const int64_t* i
   if (n == 0) return SMC_OK;
   constexpr int threads = 256;
   const unsigned blocks = static_cast<unsigned>((n + threads - 1) / threads);
-  smc::launch(sobol_draw_kernel, dim3(blocks), dim3(threads), 0, smc::as_stream(stream),
+  smc::launch_aux(sobol_draw_kernel, dim3(blocks), dim3(threads), 0, smc::as_stream(stream),
                      tables_dev, dim, index_dev, index0, n, lower_dev, upper_dev, out_f64, out_f32);
   return smc::check_launch("sobol_draw_kernel");
 }

@@ -57,14 +57,17 @@ def main() -> None:
     lines = ["# Round-6 closing records (tools/micro/r06_final.sh on one MI355X; tools/r06_records.py)", "",
              "`kernel_ms` is the bench's own timing of the dominant launch: `kernel_iters` calls after the timed region,",
              "each alone on a drained stream, from the first kernel's start to the last kernel's end by the kernels' own",
-             "execution timestamps (`smc_time_launches`), ÷ launches per call. `same launches` is the bench command's",
-             "rocprofv3 trace of exactly those calls (its last `kernel_iters` calls of the kernel(s);",
-             "`prof_<cfg>_kernel_trace_tail.txt`); `alone` is the launch shape in `tools/kprof_*`, dispatches 2 .. 11",
-             "(`iso_<cfg>_*`). `frac` is the line's; `frac (file)` recomputes it from the line's algorithmic bytes and",
-             "the same-launch trace time.", "",
-             "| config | ms/step | kernel (line) | kernel_ms | same launches (trace) | agree | alone (kprof) | frac | "
-             "frac (file) |",
-             "|---|---|---|---|---|---|---|---|---|"]
+             "execution timestamps (`smc_time_launches`), ÷ launches per call. The same bench command run again under",
+             "rocprofv3 (`prof_<cfg>`) prints its own line; `trace` is that run's rocprofv3 record of exactly the calls",
+             "its line times (the trace's last `kernel_iters` calls of the kernel(s), `prof_<cfg>_kernel_trace_tail.txt`).",
+             "`own` compares the prof run's kernel_ms with its trace (one set of launches timed two ways; under the",
+             "profiler the launch events of the 43-µs e2e launch read high); `line` compares the bench line's kernel_ms",
+             "(an unprofiled run) with that trace (two runs of the same command: run-to-run spread). `frac (trace)`",
+             "is the line's algorithmic bytes over the trace time ÷ 8 TB/s. `alone` is the launch shape in `tools/kprof_*`,",
+             "dispatches 2 .. 11 (`iso_<cfg>_*`).", "",
+             "| config | ms/step | kernel (line) | kernel_ms (line) | frac (line) | trace | line vs trace | kernel_ms (prof run) "
+             "| own vs trace | frac (trace) | alone (kprof) |",
+             "|---|---|---|---|---|---|---|---|---|---|---|"]
     for cfg in CONFIGS:
         bench = os.path.join(a.src, f"bench_{cfg}.out")
         if not os.path.exists(bench):
@@ -106,11 +109,20 @@ def main() -> None:
                 sums = [sum(per[i:i + k]) for i in range(0, len(per) - k + 1, k)]
                 sel = sums[1:11] if len(sums) > 2 else sums
                 alone = sum(sel) / len(sel) if sel else None
-        agree = f"{(r['kernel_ms'] / same - 1) * 100:+.1f} %" if same else "-"
+        kp = None
+        pout = os.path.join(a.src, f"prof_{cfg}.out")
+        if os.path.exists(pout):
+            plines = [ln for ln in open(pout).read().splitlines() if ln.startswith("{")]
+            if plines:
+                kp = json.loads(plines[-1])["roofline"]["kernel_ms"]
+                with open(os.path.join(final, f"prof_{cfg}_line.json"), "w") as f:
+                    f.write(plines[-1] + "\n")
+        agree = f"{(kp / same - 1) * 100:+.1f} %" if same and kp else "-"
+        agree_line = f"{(r['kernel_ms'] / same - 1) * 100:+.1f} %" if same else "-"
         frac_file = r["algorithmic_bytes_per_launch"] / (same * 1e-3) / (r["peak"] * 1e9) if same else None
         fmt = lambda x: f"{x:.4f}" if x is not None else "-"  # noqa: E731
-        lines.append(f"| {cfg} | {d['ms_per_step']:.4f} | `{r['kernel']}` | {r['kernel_ms']:.4f} | {fmt(same)} | "
-                     f"{agree} | {fmt(alone)} | {r['frac']:.4f} | {fmt(frac_file)} |")
+        lines.append(f"| {cfg} | {d['ms_per_step']:.4f} | `{r['kernel']}` | {r['kernel_ms']:.4f} | {r['frac']:.4f} | "
+                     f"{fmt(same)} | {agree_line} | {fmt(kp)} | {agree} | {fmt(frac_file)} | {fmt(alone)} |")
     pm = sorted(glob.glob(os.path.join(a.src, "pmc_*")))
     for p in pm:
         cc = glob.glob(os.path.join(p, "**", "*counter_collection.csv"), recursive=True)
