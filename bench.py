@@ -100,6 +100,9 @@ def parse(argv: list[str] | None = None) -> argparse.Namespace:
     ap.add_argument("--lanes-short", type=int, default=None,
                     help="pricer.mc_lanes_short (MC lanes for launches below --net-cu-min-path-steps)")
     ap.add_argument("--net-cus", type=int, default=32, help="CUs reserved for the network (pricer.network_cus)")
+    ap.add_argument("--exchanging-masks", default="auto", choices=["auto", "on", "off"],
+                    help="CU-masked network stream beside the exchanging C3 / C5 launches (pricer.exchanging_masks; "
+                         "auto: data-parallel runs only)")
     ap.add_argument("--net-cus-small", type=int, default=None,
                     help="pricer.network_cus_small (network CUs beside launches below --net-cu-min-path-steps)")
     ap.add_argument("--net-cu-min-path-steps", type=int, default=None,
@@ -320,6 +323,7 @@ def make_pricer(args: argparse.Namespace, dev):
     if args.lanes_short is not None:
         pricer.mc_lanes_short = args.lanes_short
     pricer.network_cus = args.net_cus
+    pricer.exchanging_masks = {"auto": None, "on": True, "off": False}[args.exchanging_masks]
     pricer.network_cus_wide = args.net_cus_wide
     pricer.network_cu_pattern = args.net_cu_pattern
     if args.net_cus_small is not None:

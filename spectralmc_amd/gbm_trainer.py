@@ -499,6 +499,10 @@ class GbmCVNNPricer:
     #: True: enqueue an exchanging launch only after the previous step's network part (and all-reduce) has
     #: completed (round 4-5's data-parallel default); None / False: beside it
     exchange_after_network: bool | None = None
+    #: CU masks for the exchanging launches (C3 sliced, C5 basket) with a fused network: None = in data-parallel
+    #: runs only (the collective on the network's CUs); True = also on one GPU (the network
+    #: beside the path launch instead of after it); False = never
+    exchanging_masks: bool | None = None
     #: network forward/backward/Adam on the fused HIP kernels (csrc/cvnn.hip) when the CVNN is a
     #: ComplexLinear + modReLU/zReLU chain; False (or other architectures): torch-ROCm modules
     fused_network: bool = True
@@ -903,7 +907,8 @@ class TrainingSession:
             # data-parallel runs of the exchanging launches (C3 sliced, C5 basket) take the masks too: the step's
             # all-reduce runs on the network stream (dp.RcclComm), so RCCL's kernels stay on the network's CUs and
             # cannot keep a partner workgroup of the exchanging launch off a CU while they wait for a slow peer
-            exchanging_dp = ctx is not None and getattr(eng, "exchanges", False) and fused is not None
+            want = pricer.exchanging_masks if pricer.exchanging_masks is not None else ctx is not None
+            exchanging_dp = want and getattr(eng, "exchanges", False) and fused is not None
             if (net_cus > 0 and (getattr(eng, "kernel_name", "") in WHOLE_CONTRACT_KERNELS or exchanging_dp)
                     and cus >= 2 * net_cus):
                 # the network on its own CUs beside the path kernels (CU-masked HIP streams); the path
