@@ -500,8 +500,10 @@ class GbmCVNNPricer:
     #: completed (round 4-5's data-parallel default); None / False: beside it
     exchange_after_network: bool | None = None
     #: CU masks for the exchanging launches (C3 sliced, C5 basket) with a fused network: None = in data-parallel
-    #: runs only (the collective on the network's CUs); True = also on one GPU (the network
-    #: beside the path launch instead of after it); False = never
+    #: runs (the collective on the network's CUs) and, on one GPU, for the sliced resident
+    #: kernel (C3: the network on 32 CUs beside the launch, 48.06-48.11 against 48.51-48.64 ms/step; the W = 32
+    #: basket launch loses a whole group per XCD to the mask: 51.1 against 46.5, profiles/r06/r06_xmasks.txt);
+    #: True = always; False = never
     exchanging_masks: bool | None = None
     #: network forward/backward/Adam on the fused HIP kernels (csrc/cvnn.hip) when the CVNN is a
     #: ComplexLinear + modReLU/zReLU chain; False (or other architectures): torch-ROCm modules
@@ -907,7 +909,8 @@ class TrainingSession:
             # data-parallel runs of the exchanging launches (C3 sliced, C5 basket) take the masks too: the step's
             # all-reduce runs on the network stream (dp.RcclComm), so RCCL's kernels stay on the network's CUs and
             # cannot keep a partner workgroup of the exchanging launch off a CU while they wait for a slow peer
-            want = pricer.exchanging_masks if pricer.exchanging_masks is not None else ctx is not None
+            want = pricer.exchanging_masks if pricer.exchanging_masks is not None else (
+                ctx is not None or getattr(eng, "kernel_name", "") == "resident_kernel(sliced)")
             exchanging_dp = want and getattr(eng, "exchanges", False) and fused is not None
             if (net_cus > 0 and (getattr(eng, "kernel_name", "") in WHOLE_CONTRACT_KERNELS or exchanging_dp)
                     and cus >= 2 * net_cus):

@@ -69,6 +69,7 @@ def _session(config: str, overlap: bool, steps: int) -> dict:
     eng = session.engine
     facts = {"kernel": eng.kernel_name, "chunk": eng.chunk, "launches": -(-eng.B // eng.chunk),
              "streams": len(session.mc_streams), "overlapped": session.stream is not session.mc_stream,
+             "network_cus": session.network_cus_used,
              "captured": prog.captured, "network": prog.fused.kernels if prog.fused is not None else None,
              "table": ([(t.in_features, t.out_features, t.activation, t.w_re, t.w_im, t.b_re, t.b_im, t.act_bias)
                         for t in prog.fused.table] if prog.fused is not None else None)}
@@ -101,17 +102,19 @@ def _free_cache():
     _CACHE.clear()
 
 
-EXPECT = {"c3": ("resident_kernel(sliced)", 8192, 2, "mfma_bf16"),
-          "c5": ("basket_resident_kernel", 2731, 3, "mfma_f32")}
+EXPECT = {"c3": ("resident_kernel(sliced)", 8192, 2, "mfma_bf16", 32),
+          "c5": ("basket_resident_kernel", 2731, 3, "mfma_f32", 0)}
 
 
 @pytest.mark.parametrize("config", ["c3", "c5"])
 def test_session_uses_the_bench_policy(config) -> None:
     f = session(config)["facts"]
-    kernel, chunk, launches, network = EXPECT[config]
+    kernel, chunk, launches, network, net_cus = EXPECT[config]
     assert (f["kernel"], f["chunk"], f["launches"], f["network"]) == (kernel, chunk, launches, network)
-    # exchanging launches: one MC stream, the network on its own (unmasked) stream beside it, graphs replayed
+    # exchanging launches: one MC stream, the network on its own stream beside it (C3: on 32 CU-masked CUs, the
+    # sliced launch sized to the rest; C5: unmasked), graphs replayed
     assert f["streams"] == 1 and f["overlapped"] and f["captured"]
+    assert f["network_cus"] == net_cus
 
 
 @pytest.mark.parametrize("config", ["c3", "c5"])
