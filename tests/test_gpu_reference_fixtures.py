@@ -95,6 +95,17 @@ def test_reference_math_targets_bit_exact_and_match_reference(oracle, gbm_golden
     assert per_contract_rel(got, want).max() < 4e-6
 
 
+@pytest.mark.parametrize("name", [n for n in CASE_NAMES if "f64" not in n])
+def test_reference_math_on_hw_normals_matches_reference_fixture(gbm_golden, name) -> None:
+    """SMC_MATH_REF | SMC_MATH_HW (math_mode "reference_hw": the reference typing's f64 step on the
+    hardware-transcendental normals) on every f32 fixture case: within the hw mode's 1e-5 per contract of the
+    reference's own targets (gbm_golden.npz, generated by the reference's gbm.py)."""
+    contracts, want, m = unpack(gbm_golden, name)
+    got = train_targets(contracts, m, hw=True, ref=True)
+    assert np.isfinite(got).all()
+    assert per_contract_rel(got, want).max() < 1e-5
+
+
 def test_c2_bench_instantiation_whole_rounds(oracle, gbm_golden) -> None:
     """The kernel BENCH times, at its shape, over two whole rounds of resident workgroups
     (2 per CU): hw math within 1e-5 per contract of the reference-mode oracle, and the first two
