@@ -36,6 +36,8 @@ def main() -> None:
                     "its own cursor, sync area and path scratch (consecutive launches may overlap)")
     ap.add_argument("--split", type=int, default=0, help="each call: this many concurrent launches of B / split "
                     "contracts, each on its own CU-masked stream of 1 / split of the CUs (every XCD in each)")
+    ap.add_argument("--stream", default="current", choices=["current", "created", "high", "low"],
+                    help="lane 0's stream: torch's current stream, or a created one (high: priority -1)")
     ap.add_argument("--one-stream", action="store_true", help="--lanes buffers and sync areas, all on one stream")
     ap.add_argument("--dynamic", action="store_true", help="SMC_TRAIN_DYNAMIC: every contract from the queue")
     ap.add_argument("--trace", default="", help="trace variant library (tools/micro/trace_variant.sh): after the timed "
@@ -95,6 +97,10 @@ def main() -> None:
             for cu in range(k * per_lane, (k + 1) * per_lane):  # logical ids interleave the XCDs (gbm_trainer._cu_masks)
                 mask[cu // 32] |= 1 << (cu % 32)
             streams.append(_masked_stream(dev, mask, owned))
+    if a.stream != "current":  # lane 0 on a created stream instead of torch's current (default) stream
+        prio = {"created": 0, "high": -1, "low": 0}[a.stream]
+        streams[0] = torch.cuda.Stream(priority=prio)
+        streams[0].wait_stream(torch.cuda.current_stream())
     if a.one_stream:  # the lanes' buffers, one stream: launches serialised, rotating over the path buffers
         streams = [torch.cuda.current_stream()] * lanes
     scheme = _lib.SCHEME_LOG_EULER | {"hw": _lib.MATH_HW, "reference": _lib.MATH_REF,
