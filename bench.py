@@ -681,14 +681,22 @@ def main() -> None:
                      "algorithmic_bytes_survey_per_launch": bytes_survey,
                      # the f64 rows kernel is bound by VALU issue at the clock the chip sustains under it, not
                      # by HBM (PMC): the HBM fraction above is not its ceiling
-                     "bound_note": ("rows_kernel (f64) runs at the clock the power limiter allows (1.3-1.66 GHz): 38 VALU "
-                                    "instructions per path-step (math v4) hold the SIMDs 81-84 % of the launch "
-                                    "(profiles/r05/pmc_f64_v4.txt)" if eng.kernel_name.startswith("rows_")
-                                   and f64 else None),
+                     "bound_note": ("rows_kernel (f64) runs at the clock the power limiter allows (1.3-1.67 GHz): 38 VALU "
+                                    "instructions per path-step (math v4) hold the SIMDs 80-83 % of the launch "
+                                    "(profiles/r06/pmc_clock.txt)" if eng.kernel_name.startswith("rows_")
+                                   and f64 else
+                                    "rows_ref_kernel runs at the VALU issue ceiling (profiles/r06/pmc_c2ref.txt)"
+                                    if eng.kernel_name.startswith("rows_ref") else None),
                      "bytes_note": ("the kernel keeps each contract's terminal row on chip: achieved counts the path "
                                     "store, targets and contract rows, not the terminal re-read of SURVEY 8(d)'s "
                                     "per-contract figure (algorithmic_bytes_survey_per_launch)" if on_chip else None),
                      "contracts_per_launch": contracts_per_launch,
+                     # SURVEY 8(d)'s step level (its headline definition): the step's algorithmic bytes (8(d)'s
+                     # per-contract figure x B per GPU) over the measured step time (Sobol, paths, CF, CVNN, Adam)
+                     "step_level": {"bytes_per_step": bytes_survey / contracts_per_launch * B,
+                                    "achieved": bytes_survey / contracts_per_launch * B / (elapsed / args.steps) / 1e9,
+                                    "frac": bytes_survey / contracts_per_launch * B / (elapsed / args.steps) / 1e9
+                                    / HBM_PEAK_GBS},
                      "measured_stream_gbs": stream_gbs,
                      "frac_of_measured_write": (achieved / stream_gbs["write"]) if "write" in stream_gbs else None},
         "network": network,
