@@ -87,8 +87,9 @@ def parse(argv: list[str] | None = None) -> argparse.Namespace:
                          "reference_hw (that step on the hardware-transcendental normals)")
     ap.add_argument("--network", default=None, choices=["auto", "valu", "mfma", "bf16"],
                     help="network kernels (default: bf16 for c3, auto otherwise)")
-    ap.add_argument("--overlap-rows", default="on", choices=["on", "off"],
-                    help="pricer.overlap_rows: the f64 (rows_kernel) steps' network beside the next rows launch")
+    ap.add_argument("--overlap-rows", default="auto", choices=["auto", "on", "off"],
+                    help="pricer.overlap_rows: the rows_kernel / rows_ref_kernel steps' network beside the next rows "
+                         "launch (auto: f64 overlapped, the reference typing on one stream)")
     ap.add_argument("--overlap", default="on", choices=["on", "off"],
                     help="MC part of step s+1 on its own stream beside step s's network part (pricer.overlap_mc)")
     ap.add_argument("--priority", default="network", choices=["network", "mc", "none"],
@@ -315,7 +316,7 @@ def make_pricer(args: argparse.Namespace, dev):
     pricer.warmup_steps = max(1, min(2, args.warmup)) if args.graphs == "on" else 0
     pricer.network_compute = args.network or NETWORK_COMPUTE.get(args.config, "auto")
     pricer.overlap_mc = args.overlap == "on"
-    pricer.overlap_rows = args.overlap_rows == "on"
+    pricer.overlap_rows = {"auto": None, "on": True, "off": False}[args.overlap_rows]
     pricer.high_priority_stream = args.priority
     pricer.mc_lanes = args.lanes
     if args.lanes_long is not None:

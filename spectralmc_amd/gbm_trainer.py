@@ -486,10 +486,14 @@ class GbmCVNNPricer:
     #: (e2e shape: 0.110 ms/step unmasked, 0.141 on 64 CUs, 0.101 on 128, 0.111 on 160;
     #: profiles/r04/e2e_network_cus.txt)
     network_cus_small: int = 128
-    #: overlap_mc for the rows_kernel + cf_kernel shapes (f64): step s's network part beside step s+1's
-    #: rows launch, whose persistent workgroups leave registers and LDS for a network workgroup per CU
-    #: at the f64 register budget; False runs those shapes on one stream
-    overlap_rows: bool = True
+    #: overlap_mc for the rows_kernel / rows_ref_kernel + cf_kernel shapes (f64, the reference typing): True puts
+    #: step s's network part beside step s+1's rows launch (a network workgroup fits beside the persistent
+    #: workgroups at the f64 register budget); False runs those shapes on one stream;
+    #: None (default): overlapped for f64's rows_kernel (box-dependent: 8.35 against 8.43-8.47 ms/step on one
+    #: box, 8.64 against 8.50-8.52 on another, profiles/r06/r06_f64_overlap*.txt), one stream for the reference
+    #: typing's rows_ref_kernel, whose launch the network's workgroups stretch by more than the network takes
+    #: (6.64-6.66 against 7.03-7.10, reference_hw 4.44-4.47 against 4.71-4.72, r06_ref_overlap*.txt)
+    overlap_rows: bool | None = None
     #: launches whose workgroups wait for each other (the sliced resident kernel, C3; the resident
     #: basket kernel, C5) need every workgroup of a group co-resident.  A collective that spins on a
     #: few CUs while it waits for a slow peer (RCCL in data-parallel runs) could hold CUs past the
@@ -887,9 +891,11 @@ class TrainingSession:
         # 10.55 ms/step overlapped, 10.35 sequential); at the f64 register budget (two workgroups per CU,
         # 4 waves per SIMD) a network workgroup fits beside it and the latency-bound f64 network hides
         # under the VALU-bound path launch (round 4: 8.64-8.71 against 8.81-8.89 ms/step,
-        # profiles/r04/ab_f64_overlap_rows.txt).  overlap_rows=False runs those shapes on one stream.
-        overlap = pricer.overlap_mc and (pricer.overlap_rows or
-                                         not getattr(self.engine, "kernel_name", "").startswith("rows_"))
+        # profiles/r04/ab_f64_overlap_rows.txt).  Round 6: for f64 a box-dependent wash (+-1.5 %); for the
+        # reference typing's rows_ref_kernel one stream is 4-6 % faster (pricer.overlap_rows = None).
+        kname = getattr(self.engine, "kernel_name", "")
+        rows_overlap = pricer.overlap_rows if pricer.overlap_rows is not None else not kname.startswith("rows_ref")
+        overlap = pricer.overlap_mc and (rows_overlap or not kname.startswith("rows_"))
         if overlap:
             # the network part is a few short launches: a high-priority queue lets its workgroups
             # take CU slots as the long MC kernel frees them instead of queueing behind it

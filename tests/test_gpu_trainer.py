@@ -408,7 +408,7 @@ def test_overlapped_mc_matches_sequential() -> None:
 
 def test_overlapped_rows_network_matches_sequential() -> None:
     """f64 at P = 2048 (rows_kernel + cf_kernel): step s's network part beside step s+1's rows launch
-    (pricer.overlap_rows, the default) == the one-stream step, bit for bit."""
+    (pricer.overlap_rows = True, f64's default) == the one-stream step, bit for bit."""
     def mk(overlap_rows: bool):
         sp = make_simulation_params(timesteps=T, network_size=N, batches_per_mc_run=16, threads_per_block=256,
                                     mc_seed=7, buffer_size=512, dtype=Precision.float64)
