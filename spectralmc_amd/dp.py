@@ -51,11 +51,15 @@ class RcclComm:
     def __init__(self, rank: int, world: int) -> None:
         self.lib = _librccl()
         uid = _UniqueId()
+        box: list[object] = [None]
         if rank == 0:
-            self._check(self.lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        # the raw 128 bytes (uid.internal would stop at the first NUL byte)
-        box = [ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid)) if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
+            rc = self.lib.ncclGetUniqueId(ctypes.byref(uid))
+            # the raw 128 bytes (uid.internal would stop at the first NUL byte), or the failure for every rank
+            box = [ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid)) if rc == 0 else
+                   f"ncclGetUniqueId: {self.lib.ncclGetErrorString(rc).decode()} ({rc})"]
+        dist.broadcast_object_list(box, src=0)  # every rank takes part, so a failure on rank 0 raises everywhere
+        if isinstance(box[0], str):
+            raise RuntimeError(box[0])
         uid = _UniqueId.from_buffer_copy(box[0])
         self.comm = ctypes.c_void_p()
         self._check(self.lib.ncclCommInitRank(ctypes.byref(self.comm), world, uid, rank), "ncclCommInitRank")

@@ -149,3 +149,26 @@ def test_device_enum_follows_the_bound_rank_device(monkeypatch) -> None:
     assert Device.cpu.to_torch() == torch.device("cpu")
     monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
     assert Device.cuda.to_torch() == torch.device("cuda:0")
+
+
+def test_rccl_comm_reports_a_rank0_id_failure(monkeypatch, tmp_path) -> None:
+    """dp.RcclComm: when rank 0 cannot create the RCCL unique id, the failure is broadcast in its place, so every
+    rank raises instead of waiting in the id broadcast (here a one-rank gloo group and a stub librccl)."""
+    import ctypes
+
+    from spectralmc_amd import dp
+
+    class _Stub:
+        def ncclGetUniqueId(self, uid):  # noqa: N802 - the librccl symbol name
+            return 3
+
+        def ncclGetErrorString(self, rc):  # noqa: N802
+            return ctypes.c_char_p(b"internal error").value
+
+    monkeypatch.setattr(dp, "_librccl", lambda: _Stub())
+    dist.init_process_group("gloo", init_method=f"file://{tmp_path}/rdzv", rank=0, world_size=1)
+    try:
+        with pytest.raises(RuntimeError, match="ncclGetUniqueId: internal error"):
+            dp.RcclComm(0, 1)
+    finally:
+        dist.destroy_process_group()
