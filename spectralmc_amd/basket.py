@@ -185,12 +185,9 @@ class BasketEngine:
         per_contract = self.A * rows * self.pitch * 4
         budget = path_buffer_bytes if path_buffer_bytes is not None else _engine.path_buffer_budget(device)
         max_chunk = max(1, min(B, budget // per_contract))
-        # the persistent resident kernel (sync area) takes any chunk (a dynamic contract tail); the one-workgroup-
-        # per-contract basket_kernel runs in rounds of its resident workgroups
-        resident = sync_bytes(cfg, 1) > 0
-        if max_chunk < B and not resident:
+        if max_chunk < B:
             # several launches: whole rounds of resident workgroups, so no launch ends in a
-            # part-filled round (1171 -> 1024 contracts per launch, 2 full rounds each)
+            # part-filled round (C5: 1171 -> 1024 contracts per launch, 2 full rounds each)
             slots = int(_lib.lib().smc_basket_resident_slots(self.A, self.N, self._math))
             if 0 < slots <= max_chunk:
                 max_chunk -= max_chunk % slots

@@ -6,7 +6,7 @@ builds it for ``--config c3`` / ``--config c5`` (``bench.make_pricer(bench.parse
   8192-contract ``resident_kernel(sliced)`` launches per step (W = 4 workgroups per contract, the dynamic
   exchange tail) through half the HBM of path scratch, the 6 -> 32 -> 32 -> 1024 network on the bf16 MFMA
   kernels, per-slot hipGraphs after 2 eager steps, the next step's MC part beside the network part;
-* C5: 8192 contracts x 131,072 paths (N = 256, M = 512) of 4 correlated assets, two 4096-contract
+* C5: 8192 contracts x 131,072 paths (N = 256, M = 512) of 4 correlated assets, three 2731-contract
   ``basket_resident_kernel`` launches (W = 32) per step, the 16 -> 32 -> 32 -> 256 f32 MFMA network.
 
 For each:
@@ -103,7 +103,7 @@ def _free_cache():
 
 
 EXPECT = {"c3": ("resident_kernel(sliced)", 8192, 2, "mfma_bf16", 32),
-          "c5": ("basket_resident_kernel", 4096, 2, "mfma_f32", 0)}
+          "c5": ("basket_resident_kernel", 2731, 3, "mfma_f32", 0)}
 
 
 @pytest.mark.parametrize("config", ["c3", "c5"])
