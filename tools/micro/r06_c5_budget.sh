@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 6: C5 with the default path budget (2 launches of 4096 since the resident chunk is not rounded) vs a 97-GiB budget (3 launches of 2731, the round-5 chunking)
+# Round 6 (run with the chunking of commit c19b222, since reverted): C5 with 2 launches of 4096 (default budget,
+# no slot rounding) vs a 97-GiB budget (3 launches of 2731, the chunking kept): profiles/r06/r06_c5_budget_samebox.txt
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 o=gpurun_out/r06_c5_budget.txt; : > $o
