@@ -36,6 +36,7 @@ def main() -> None:
                     "its own cursor, sync area and path scratch (consecutive launches may overlap)")
     ap.add_argument("--split", type=int, default=0, help="each call: this many concurrent launches of B / split "
                     "contracts, each on its own CU-masked stream of 1 / split of the CUs (every XCD in each)")
+    ap.add_argument("--cus", type=int, default=0, help="run every lane on a CU-masked stream of this many CUs")
     ap.add_argument("--stream", default="current", choices=["current", "created", "high", "low"],
                     help="lane 0's stream: torch's current stream, or a created one (high: priority -1)")
     ap.add_argument("--one-stream", action="store_true", help="--lanes buffers and sync areas, all on one stream")
@@ -97,7 +98,15 @@ def main() -> None:
             for cu in range(k * per_lane, (k + 1) * per_lane):  # logical ids interleave the XCDs (gbm_trainer._cu_masks)
                 mask[cu // 32] |= 1 << (cu % 32)
             streams.append(_masked_stream(dev, mask, owned))
-    if a.stream != "current":  # lane 0 on a created stream instead of torch's current (default) stream
+    if a.cus:  # every lane on a stream masked to logical CUs [0, cus): cus / 32 CUs of every shader engine
+        from spectralmc_amd.gbm_trainer import _masked_stream
+
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        mask = [0] * ((ncu + 31) // 32)
+        for cu in range(a.cus):
+            mask[cu // 32] |= 1 << (cu % 32)
+        streams = [_masked_stream(dev, mask, owned) for _ in range(lanes)]
+    elif a.stream != "current":  # lane 0 on a created stream instead of torch's current (default) stream
         prio = {"created": 0, "high": -1, "low": 0}[a.stream]
         streams[0] = torch.cuda.Stream(priority=prio)
         streams[0].wait_stream(torch.cuda.current_stream())
